@@ -1,0 +1,112 @@
+// act_quant.hip -- q8_1 activation quantizer on the GPU.
+//
+// Bit-exact with the reference's producer utils/quantize/q8_1.py:18-70:
+//   d = fp16(amax/127) (0 for an all-zero block), q = clamp(rne(fp16(x / d')), +-127) with
+//   d' = 1 where d == 0, s = fp16(d * fp16(sum q)).
+// The reference's Triton kernels fuse an fp32 variant of this step (kernels/mmq_q4_k.py:202-207,
+// x*127/amax, no fp16 rounding); this build keeps the oracle's exact q8_1 semantics so the
+// GPU path and kernels/cpu_impls see identical integer activations.
+//
+// Eight lanes own one 32-element block (4 fp16 each); amax and sum(q) are reduced with
+// 3-step xor shuffles inside the 8-lane group.  fp32 division is IEEE correctly rounded
+// (hipcc default), so fp16(x/d) matches torch's CPU fp16 division.
+//
+// Output forms (one kernel template, chosen by the caller):
+//   AOS  : the q8_1 byte layout itself (36 B per block) -- gq_quantize_q8_1 / tests
+//   SOA  : codes int8 [rows][K] + d float [rows][K/32] + s float [rows][K/32] -- GEMV input
+//   DEQ  : x~ = fp16(d * q) [rows][K] -- the dequantized activation fed to the fp16 MFMA GEMM
+#include "gguf_blocks.hpp"
+#include "gguf_internal.hpp"
+
+namespace gq {
+
+template <int MODE>
+__global__ __launch_bounds__(256) void act_quant_kernel(const uint16_t *__restrict__ X, int64_t ldx, int64_t rows,
+                                                        int64_t K, uint8_t *__restrict__ out, int8_t *__restrict__ codes,
+                                                        float *__restrict__ dout, float *__restrict__ sout,
+                                                        uint16_t *__restrict__ xdeq)
+{
+    const int64_t nb = K / 32;
+    const int64_t blk = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
+    const int sub = threadIdx.x & 7;
+    const bool live = blk < rows * nb;
+    const int64_t row = live ? blk / nb : 0;
+    const int64_t j = live ? blk - row * nb : 0;
+
+    uint32_t w0 = 0, w1 = 0;
+    if (live) {
+        u32x2 v = ld8(X + row * ldx + 32 * j + 4 * sub);
+        w0 = v.x;
+        w1 = v.y;
+    }
+    float x[4] = {h2f(w0 & 0xffff), h2f(w0 >> 16), h2f(w1 & 0xffff), h2f(w1 >> 16)};
+    float amax = fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3])));
+    amax = fmaxf(amax, __shfl_xor(amax, 1, 8));
+    amax = fmaxf(amax, __shfl_xor(amax, 2, 8));
+    amax = fmaxf(amax, __shfl_xor(amax, 4, 8));
+
+    const uint16_t dbits = amax != 0.f ? f2h_bits(amax / 127.0f) : (uint16_t)0;
+    const float d = h2f(dbits);
+    const float div = d == 0.f ? 1.0f : d;
+    int q[4];
+    int sum = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float r = __builtin_rintf(h2f(f2h_bits(x[i] / div)));
+        r = fminf(127.f, fmaxf(-127.f, r));
+        q[i] = (int)r;
+        sum += q[i];
+    }
+    sum += __shfl_xor(sum, 1, 8);
+    sum += __shfl_xor(sum, 2, 8);
+    sum += __shfl_xor(sum, 4, 8);
+    const uint16_t sbits = f2h_bits(d * h2f(f2h_bits((float)sum)));
+    if (!live) return;
+
+    const uint32_t packed = (uint32_t)(q[0] & 0xff) | ((uint32_t)(q[1] & 0xff) << 8) |
+                            ((uint32_t)(q[2] & 0xff) << 16) | ((uint32_t)(q[3] & 0xff) << 24);
+    if constexpr (MODE == ACT_AOS) {
+        uint8_t *o = out + blk * 36;
+        __builtin_memcpy(o + 4 + 4 * sub, &packed, 4);
+        if (sub == 0) {
+            uint32_t ds = (uint32_t)dbits | ((uint32_t)sbits << 16);
+            __builtin_memcpy(o, &ds, 4);
+        }
+    } else if constexpr (MODE == ACT_SOA) {
+        *(uint32_t *)(codes + row * K + 32 * j + 4 * sub) = packed;
+        if (sub == 0) {
+            dout[row * nb + j] = d;
+            sout[row * nb + j] = h2f(sbits);
+        }
+    } else {
+        u32x2 o;
+        o.x = (uint32_t)f2h_bits(d * (float)q[0]) | ((uint32_t)f2h_bits(d * (float)q[1]) << 16);
+        o.y = (uint32_t)f2h_bits(d * (float)q[2]) | ((uint32_t)f2h_bits(d * (float)q[3]) << 16);
+        *(u32x2 *)(xdeq + row * K + 32 * j + 4 * sub) = o;
+    }
+}
+
+hipError_t launch_act_quant(int mode, const uint16_t *X, int64_t ldx, int64_t rows, int64_t K, void *out0,
+                            void *out1, void *out2, hipStream_t s)
+{
+    const int64_t nblk = rows * (K / 32);
+    if (nblk == 0) return hipSuccess;
+    dim3 grid((unsigned)((nblk + 31) / 32)), block(256);
+    switch (mode) {
+    case ACT_AOS:
+        act_quant_kernel<ACT_AOS><<<grid, block, 0, s>>>(X, ldx, rows, K, (uint8_t *)out0, nullptr, nullptr,
+                                                          nullptr, nullptr);
+        break;
+    case ACT_SOA:
+        act_quant_kernel<ACT_SOA><<<grid, block, 0, s>>>(X, ldx, rows, K, nullptr, (int8_t *)out0, (float *)out1,
+                                                          (float *)out2, nullptr);
+        break;
+    default:
+        act_quant_kernel<ACT_DEQ><<<grid, block, 0, s>>>(X, ldx, rows, K, nullptr, nullptr, nullptr, nullptr,
+                                                          (uint16_t *)out0);
+        break;
+    }
+    return hipGetLastError();
+}
+
+} // namespace gq

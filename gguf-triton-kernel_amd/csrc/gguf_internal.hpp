@@ -1,0 +1,23 @@
+// gguf_internal.hpp -- launchers shared between the kernel translation units and the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gq {
+
+enum ActMode : int { ACT_AOS = 0, ACT_SOA = 1, ACT_DEQ = 2 };
+
+// Activation quantizer (act_quant.hip).  AOS: out0 = q8_1 bytes.  SOA: out0 = int8 codes
+// [rows][K], out1 = float d [rows][K/32], out2 = float s [rows][K/32].  DEQ: out0 = fp16 x~.
+hipError_t launch_act_quant(int mode, const uint16_t *X, int64_t ldx, int64_t rows, int64_t K, void *out0,
+                            void *out1, void *out2, hipStream_t s);
+
+// Decode-shaped GEMV (mmq_gemv.hip): C[t][m] for t < N_tok <= 8 from SOA activations.
+hipError_t launch_gemv(int fmt, const uint8_t *A, const int8_t *xq, const float *xd, const float *xs, uint16_t *C,
+                       int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
+
+// Batched GEMM on fp16 MFMA (mmq_gemm.hip): C[t][m] from the dequantized activation x~.
+hipError_t launch_gemm(int fmt, const uint8_t *A, const uint16_t *xdeq, uint16_t *C, int64_t M, int64_t N,
+                       int64_t K, int64_t ldc, hipStream_t s);
+
+} // namespace gq

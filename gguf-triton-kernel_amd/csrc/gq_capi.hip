@@ -1,0 +1,170 @@
+// gq_capi.hip -- the C ABI (include/gguf_mmq.h): argument checks, workspace carving,
+// path selection (decode GEMV vs MFMA GEMM) and launches.  Stateless and re-entrant.
+#include <cstdio>
+#include <cstdarg>
+#include <string>
+
+#include "../../include/gguf_mmq.h"
+#include "gguf_blocks.hpp"
+#include "gguf_internal.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int block_elems(int t) { return t == GQ_Q8_0 ? 32 : 256; }
+int block_bytes(int t) { return t == GQ_Q8_0 ? 34 : (t == GQ_Q4_K ? 144 : 210); }
+
+size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
+
+// Decode path up to this many tokens; beyond it the fp16-MFMA GEMM.
+constexpr int64_t kGemvMaxTokens = 8;
+
+bool use_gemv(int64_t N) { return N <= kGemvMaxTokens; }
+
+size_t ws_bytes(int64_t N, int64_t K)
+{
+    if (use_gemv(N)) {
+        // SOA q8_1: codes + d + s
+        return align_up((size_t)N * K) + 2 * align_up((size_t)N * (K / 32) * sizeof(float));
+    }
+    return align_up((size_t)N * K * 2); // dequantized fp16 activation
+}
+
+} // namespace
+
+extern "C" {
+
+int gq_block_elems(gq_type t) { return block_elems(t); }
+int gq_block_bytes(gq_type t) { return block_bytes(t); }
+int gq_version(void) { return 100; }
+const char *gq_last_error(void) { return g_err.c_str(); }
+
+size_t gq_mmq_workspace_size(gq_type t, int64_t M, int64_t N, int64_t K)
+{
+    (void)t;
+    (void)M;
+    if (N <= 0 || K <= 0) return 0;
+    return ws_bytes(N, K);
+}
+
+static int check_common(gq_type t, int64_t M, int64_t N, int64_t K)
+{
+    if (t != GQ_Q8_0 && t != GQ_Q4_K && t != GQ_Q6_K) return fail(GQ_EUNSUPPORTED, "unknown gguf type %d", (int)t);
+    if (M < 0 || N < 0 || K < 0)
+        return fail(GQ_EINVAL, "negative size M=%lld N=%lld K=%lld", (long long)M, (long long)N, (long long)K);
+    const int qk = block_elems(t);
+    if (K % qk != 0) return fail(GQ_EINVAL, "K=%lld is not a multiple of %d", (long long)K, qk);
+    return GQ_OK;
+}
+
+struct Carved {
+    int8_t *xq;
+    float *xd, *xs;
+    uint16_t *xdeq;
+};
+
+static Carved carve(void *workspace, int64_t N, int64_t K)
+{
+    uint8_t *ws = (uint8_t *)workspace;
+    Carved c{};
+    if (use_gemv(N)) {
+        c.xq = (int8_t *)ws;
+        c.xd = (float *)(ws + align_up((size_t)N * K));
+        c.xs = (float *)((uint8_t *)c.xd + align_up((size_t)N * (K / 32) * sizeof(float)));
+    } else {
+        c.xdeq = (uint16_t *)ws;
+    }
+    return c;
+}
+
+static int prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *workspace, size_t workspace_bytes,
+                   hipStream_t s)
+{
+    if (!B) return fail(GQ_EINVAL, "null activation pointer");
+    if (ldb < K) return fail(GQ_EINVAL, "ldb=%lld < K=%lld", (long long)ldb, (long long)K);
+    const size_t need = ws_bytes(N, K);
+    if (!workspace || workspace_bytes < need)
+        return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace ? workspace_bytes : (size_t)0, need);
+    Carved c = carve(workspace, N, K);
+    hipError_t e = use_gemv(N) ? gq::launch_act_quant(gq::ACT_SOA, (const uint16_t *)B, ldb, N, K, c.xq, c.xd, c.xs, s)
+                               : gq::launch_act_quant(gq::ACT_DEQ, (const uint16_t *)B, ldb, N, K, c.xdeq, nullptr,
+                                                      nullptr, s);
+    if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (act_quant): %s", hipGetErrorString(e));
+    return GQ_OK;
+}
+
+static int compute(gq_type t, const void *A, const void *workspace, void *C, int64_t M, int64_t N, int64_t K,
+                   int64_t ldc, hipStream_t s)
+{
+    if (!A || !C || !workspace) return fail(GQ_EINVAL, "null pointer (A=%p C=%p workspace=%p)", A, C, workspace);
+    if (ldc < M) return fail(GQ_EINVAL, "ldc=%lld < M=%lld", (long long)ldc, (long long)M);
+    Carved c = carve((void *)workspace, N, K);
+    hipError_t e = use_gemv(N) ? gq::launch_gemv(t, (const uint8_t *)A, c.xq, c.xd, c.xs, (uint16_t *)C, M, N, K, ldc, s)
+                               : gq::launch_gemm(t, (const uint8_t *)A, c.xdeq, (uint16_t *)C, M, N, K, ldc, s);
+    if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (mmq): %s", hipGetErrorString(e));
+    return GQ_OK;
+}
+
+int gq_mmq(gq_type t, const void *A, const void *B, void *C, int64_t M, int64_t N, int64_t K, int64_t ldb,
+           int64_t ldc, void *workspace, size_t workspace_bytes, void *stream)
+{
+    g_err.clear();
+    int rc = check_common(t, M, N, K);
+    if (rc != GQ_OK) return rc;
+    if (M == 0 || N == 0) return GQ_OK;
+    if (K == 0) return fail(GQ_EINVAL, "K must be positive");
+    if (!A || !B || !C) return fail(GQ_EINVAL, "null pointer (A=%p B=%p C=%p)", A, B, C);
+    if (ldc < M) return fail(GQ_EINVAL, "ldc=%lld < M=%lld", (long long)ldc, (long long)M);
+    rc = prepare(B, N, K, ldb, workspace, workspace_bytes, (hipStream_t)stream);
+    if (rc != GQ_OK) return rc;
+    return compute(t, A, workspace, C, M, N, K, ldc, (hipStream_t)stream);
+}
+
+int gq_act_prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *workspace, size_t workspace_bytes,
+                   void *stream)
+{
+    g_err.clear();
+    if (N < 0 || K < 0) return fail(GQ_EINVAL, "negative size");
+    if (K % 32 != 0) return fail(GQ_EINVAL, "K=%lld is not a multiple of 32", (long long)K);
+    if (N == 0 || K == 0) return GQ_OK;
+    return prepare(B, N, K, ldb, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int gq_mmq_prepared(gq_type t, const void *A, const void *workspace, void *C, int64_t M, int64_t N, int64_t K,
+                    int64_t ldc, void *stream)
+{
+    g_err.clear();
+    int rc = check_common(t, M, N, K);
+    if (rc != GQ_OK) return rc;
+    if (M == 0 || N == 0) return GQ_OK;
+    if (K == 0) return fail(GQ_EINVAL, "K must be positive");
+    return compute(t, A, workspace, C, M, N, K, ldc, (hipStream_t)stream);
+}
+
+int gq_quantize_q8_1(const void *X, void *Y, int64_t rows, int64_t K, int64_t ldx, void *stream)
+{
+    g_err.clear();
+    if (rows < 0 || K < 0) return fail(GQ_EINVAL, "negative size");
+    if (K % 32 != 0) return fail(GQ_EINVAL, "K=%lld is not a multiple of 32", (long long)K);
+    if (rows == 0 || K == 0) return GQ_OK;
+    if (!X || !Y) return fail(GQ_EINVAL, "null pointer");
+    if (ldx < K) return fail(GQ_EINVAL, "ldx=%lld < K=%lld", (long long)ldx, (long long)K);
+    hipError_t e = gq::launch_act_quant(gq::ACT_AOS, (const uint16_t *)X, ldx, rows, K, Y, nullptr, nullptr,
+                                        (hipStream_t)stream);
+    if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed: %s", hipGetErrorString(e));
+    return GQ_OK;
+}
+
+} // extern "C"

@@ -1,0 +1,260 @@
+// mmq_gemv.hip -- decode-shaped MMQ (few tokens): weight rows streamed once from HBM.
+//
+// Computes C[t][m] = sum_k W[m][k] * x~[t][k] for t < N_tok (<= 4 per launch column) where
+// x~ is the q8_1-quantized activation (act_quant.hip, SOA form) and W is the packed GGUF
+// row m.  The per-block arithmetic is the reference's (kernels/cpu_impls/*):
+//   Q8_0 : dA*dB*sum(qA*qB)                                  mmq_q8_0_q8_1_cpu.py:37-54
+//   Q4_K : d*sc*dB*sum(q*qB) - dmin*m*sB                     mmq_q4_k_q8_1_cpu.py:94-117
+//   Q6_K : dB*(d*sc1*sum((q-32)*qB)_lo + d*sc2*sum(...)_hi)  mmq_q6_k_q8_1_cpu.py:117-150
+// with exact int32 dot products (v_dot4_i32_i8) and fp32 accumulation (the reference
+// accumulates in fp16), one fp16 rounding at the store.
+//
+// Mapping (wave64, no LDS): a wave owns R weight rows at a time; lane l owns "unit" u
+// (64 consecutive K elements) u = l, l+64, ...  Per unit and row a lane issues 16-byte
+// loads straight to registers (Q4_K: header + 32 qs bytes; Q6_K: 32 ql + 32 qh + 8
+// scales + d; Q8_0: two 34-byte blocks), dequantizes nothing -- the integer codes go
+// straight into dot4 against the int8 activation codes, which the lane loads once per
+// unit and reuses for its R rows.  A 6-step xor-shuffle reduction per (row, token) ends
+// the row group.  Loop over row groups is grid-strided.
+#include "gguf_blocks.hpp"
+#include "gguf_internal.hpp"
+
+namespace gq {
+
+namespace {
+
+template <int F>
+__device__ __forceinline__ void unit_blocks(int u, int &b0, int &b1)
+{
+    if constexpr (F == Q6_K) {
+        // unit u = 4*sb + 2*h + v covers elements 128h+32v+[0,32) and 128h+64+32v+[0,32)
+        const int sb = u >> 2, h = (u >> 1) & 1, v = u & 1;
+        b0 = 8 * sb + 4 * h + v;
+        b1 = b0 + 2;
+    } else {
+        b0 = 2 * u;
+        b1 = 2 * u + 1;
+    }
+}
+
+template <int F, int NT>
+struct Act {
+    uint32_t q[NT][16]; // int8 codes of the two activation blocks
+    float d[NT][2];
+    float s[NT][2];  // q8_1 s (Q4_K min term)
+    int sum[NT][4];  // sum of codes per 16-element quarter (Q6_K -32 offset)
+};
+
+template <int F, int NT>
+__device__ __forceinline__ void load_act(Act<F, NT> &a, const int8_t *__restrict__ xq, const float *__restrict__ xd,
+                                         const float *__restrict__ xs, int64_t tok0, int64_t N, int64_t K, int u)
+{
+    const int64_t nb = K / 32;
+    int b0, b1;
+    unit_blocks<F>(u, b0, b1);
+    const bool has1 = b1 < nb;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int64_t tok = (tok0 + t < N) ? tok0 + t : N - 1;
+        const int8_t *base = xq + tok * K;
+        u32x4 c0 = ld16(base + 32 * b0), c1 = ld16(base + 32 * b0 + 16);
+        u32x4 c2 = {0, 0, 0, 0}, c3 = {0, 0, 0, 0};
+        if (has1) {
+            c2 = ld16(base + 32 * b1);
+            c3 = ld16(base + 32 * b1 + 16);
+        }
+        a.q[t][0] = c0.x; a.q[t][1] = c0.y; a.q[t][2] = c0.z; a.q[t][3] = c0.w;
+        a.q[t][4] = c1.x; a.q[t][5] = c1.y; a.q[t][6] = c1.z; a.q[t][7] = c1.w;
+        a.q[t][8] = c2.x; a.q[t][9] = c2.y; a.q[t][10] = c2.z; a.q[t][11] = c2.w;
+        a.q[t][12] = c3.x; a.q[t][13] = c3.y; a.q[t][14] = c3.z; a.q[t][15] = c3.w;
+        a.d[t][0] = xd[tok * nb + b0];
+        a.d[t][1] = has1 ? xd[tok * nb + b1] : 0.f;
+        if constexpr (F == Q4_K) {
+            a.s[t][0] = xs[tok * nb + b0];
+            a.s[t][1] = has1 ? xs[tok * nb + b1] : 0.f;
+        }
+        if constexpr (F == Q6_K) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                int acc = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc = dot4(a.q[t][4 * k + i], 0x01010101u, acc);
+                a.sum[t][k] = acc;
+            }
+        }
+    }
+}
+
+// Adds row `rowp`'s unit-u contribution for every token into acc[t].
+template <int F, int NT>
+__device__ __forceinline__ void unit_dot(const uint8_t *__restrict__ rowp, int u, int64_t nb, const Act<F, NT> &a,
+                                         float (&acc)[NT])
+{
+    if constexpr (F == Q8_0) {
+        const uint8_t *p = rowp + 68 * u;
+        const bool has1 = 2 * u + 1 < nb;
+        const float dw0 = h2f(ld2(p));
+        const u32x4 a0 = ld16(p + 2), a1 = ld16(p + 18);
+        float dw1 = 0.f;
+        u32x4 a2 = {0, 0, 0, 0}, a3 = {0, 0, 0, 0};
+        if (has1) {
+            dw1 = h2f(ld2(p + 34));
+            a2 = ld16(p + 36);
+            a3 = ld16(p + 52);
+        }
+        const uint32_t w[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                                a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            int i0 = 0, i1 = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                i0 = dot4(w[i], a.q[t][i], i0);
+                i1 = dot4(w[8 + i], a.q[t][8 + i], i1);
+            }
+            acc[t] += dw0 * a.d[t][0] * (float)i0 + dw1 * a.d[t][1] * (float)i1;
+        }
+    } else if constexpr (F == Q4_K) {
+        const int sb = u >> 2, q = u & 3;
+        const uint8_t *p = rowp + 144 * sb;
+        const u32x4 hdr = ld16(p);
+        const u32x4 qa = ld16(p + 16 + 32 * q), qb = ld16(p + 32 + 32 * q);
+        const float d = h2f(hdr.x & 0xffffu), dmin = h2f(hdr.x >> 16);
+        const uint32_t sw[3] = {hdr.y, hdr.z, hdr.w};
+        int sc0, m0, sc1, m1;
+        q4k_sc_m(sw, 2 * q, sc0, m0);
+        q4k_sc_m(sw, 2 * q + 1, sc1, m1);
+        const uint32_t w[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+        const float ds0 = d * (float)sc0, ds1 = d * (float)sc1;
+        const float dm0 = dmin * (float)m0, dm1 = dmin * (float)m1;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            int i0 = 0, i1 = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                i0 = dot4(w[i] & 0x0f0f0f0fu, a.q[t][i], i0);
+                i1 = dot4((w[i] >> 4) & 0x0f0f0f0fu, a.q[t][8 + i], i1);
+            }
+            acc[t] += ds0 * a.d[t][0] * (float)i0 - dm0 * a.s[t][0] + ds1 * a.d[t][1] * (float)i1 - dm1 * a.s[t][1];
+        }
+    } else {
+        const int sb = u >> 2, h = (u >> 1) & 1, v = u & 1;
+        const uint8_t *p = rowp + 210 * sb;
+        const u32x4 l0 = ld16(p + 64 * h + 32 * v), l1 = ld16(p + 64 * h + 32 * v + 16);
+        const u32x4 g0 = ld16(p + 128 + 32 * h), g1 = ld16(p + 144 + 32 * h);
+        const u32x2 sc8 = ld8(p + 192 + 8 * h);
+        const float d = h2f(ld2(p + 208));
+        const uint32_t ql[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+        const uint32_t qh[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+        const int shA = 2 * v, shB = 4 + 2 * v;
+        uint32_t ca[8], cb[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            ca[i] = (ql[i] & 0x0f0f0f0fu) | (((qh[i] >> shA) & 0x03030303u) << 4);
+            cb[i] = ((ql[i] >> 4) & 0x0f0f0f0fu) | (((qh[i] >> shB) & 0x03030303u) << 4);
+        }
+        // sub-block scales inside this h-half: A -> 2v, 2v+1 ; B -> 4+2v, 5+2v
+        const uint32_t sA = v ? (sc8.x >> 16) : sc8.x;
+        const uint32_t sB = v ? (sc8.y >> 16) : sc8.y;
+        const float fa1 = d * (float)(int8_t)(sA & 0xff), fa2 = d * (float)(int8_t)((sA >> 8) & 0xff);
+        const float fb1 = d * (float)(int8_t)(sB & 0xff), fb2 = d * (float)(int8_t)((sB >> 8) & 0xff);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            int a1 = 0, a2 = 0, b1 = 0, b2 = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                a1 = dot4(ca[i], a.q[t][i], a1);
+                a2 = dot4(ca[4 + i], a.q[t][4 + i], a2);
+                b1 = dot4(cb[i], a.q[t][8 + i], b1);
+                b2 = dot4(cb[4 + i], a.q[t][12 + i], b2);
+            }
+            a1 -= 32 * a.sum[t][0];
+            a2 -= 32 * a.sum[t][1];
+            b1 -= 32 * a.sum[t][2];
+            b2 -= 32 * a.sum[t][3];
+            acc[t] += a.d[t][0] * (fa1 * (float)a1 + fa2 * (float)a2) + a.d[t][1] * (fb1 * (float)b1 + fb2 * (float)b2);
+        }
+    }
+}
+
+__device__ __forceinline__ float wave_sum(float v)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+template <int F, int NT, int R>
+__global__ __launch_bounds__(256) void gemv_kernel(const uint8_t *__restrict__ A, const int8_t *__restrict__ xq,
+                                                   const float *__restrict__ xd, const float *__restrict__ xs,
+                                                   uint16_t *__restrict__ C, int64_t M, int64_t N, int64_t K,
+                                                   int64_t ldc)
+{
+    using L = Layout<F>;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int64_t tok0 = (int64_t)blockIdx.y * NT;
+    const int64_t nb = K / 32;
+    const int64_t row_bytes = (K / L::QK) * L::BYTES;
+    const int nunits = (int)((K + 63) / 64);
+
+    for (int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * R; row0 < M; row0 += (int64_t)gridDim.x * 4 * R) {
+        float acc[R][NT];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[r][t] = 0.f;
+
+        for (int u = lane; u < nunits; u += 64) {
+            Act<F, NT> a;
+            load_act<F, NT>(a, xq, xd, xs, tok0, N, K, u);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int64_t row = row0 + r < M ? row0 + r : M - 1;
+                unit_dot<F, NT>(A + row * row_bytes, u, nb, a, acc[r]);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const float v = wave_sum(acc[r][t]);
+                if (lane == 0 && row0 + r < M && tok0 + t < N) C[(tok0 + t) * ldc + row0 + r] = f2h_bits(v);
+            }
+        }
+    }
+}
+
+template <int F, int NT, int R>
+hipError_t launch_one(const uint8_t *A, const int8_t *xq, const float *xd, const float *xs, uint16_t *C, int64_t M,
+                      int64_t N, int64_t K, int64_t ldc, hipStream_t s)
+{
+    const int64_t groups = (M + 4 * R - 1) / (4 * R);
+    const int64_t cap = 2048;
+    dim3 grid((unsigned)(groups < cap ? groups : cap), (unsigned)((N + NT - 1) / NT)), block(256);
+    gemv_kernel<F, NT, R><<<grid, block, 0, s>>>(A, xq, xd, xs, C, M, N, K, ldc);
+    return hipGetLastError();
+}
+
+template <int F>
+hipError_t launch_fmt(const uint8_t *A, const int8_t *xq, const float *xd, const float *xs, uint16_t *C, int64_t M,
+                      int64_t N, int64_t K, int64_t ldc, hipStream_t s)
+{
+    if (N == 1) return launch_one<F, 1, 4>(A, xq, xd, xs, C, M, N, K, ldc, s);
+    if (N == 2) return launch_one<F, 2, 4>(A, xq, xd, xs, C, M, N, K, ldc, s);
+    return launch_one<F, 4, 2>(A, xq, xd, xs, C, M, N, K, ldc, s);
+}
+
+} // namespace
+
+hipError_t launch_gemv(int fmt, const uint8_t *A, const int8_t *xq, const float *xd, const float *xs, uint16_t *C,
+                       int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s)
+{
+    switch (fmt) {
+    case Q8_0: return launch_fmt<Q8_0>(A, xq, xd, xs, C, M, N, K, ldc, s);
+    case Q4_K: return launch_fmt<Q4_K>(A, xq, xd, xs, C, M, N, K, ldc, s);
+    default: return launch_fmt<Q6_K>(A, xq, xd, xs, C, M, N, K, ldc, s);
+    }
+}
+
+} // namespace gq

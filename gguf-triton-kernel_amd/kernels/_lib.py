@@ -1,0 +1,123 @@
+"""Loader and thin torch front end for libgguf_mmq.so (the C ABI in include/gguf_mmq.h).
+
+The library is built in-tree (`make -C gguf-triton-kernel_amd`, or __graft_entry__.build()).
+There is no fallback: if the HIP library is missing or no ROCm device is present, the
+MMQ entry points raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(os.path.dirname(_HERE), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libgguf_mmq.so")
+
+GQ_Q8_0, GQ_Q4_K, GQ_Q6_K = 0, 1, 2
+TYPES = {"q8_0": GQ_Q8_0, "q4_k": GQ_Q4_K, "q6_k": GQ_Q6_K}
+BLOCK_ELEMS = {GQ_Q8_0: 32, GQ_Q4_K: 256, GQ_Q6_K: 256}
+BLOCK_BYTES = {GQ_Q8_0: 34, GQ_Q4_K: 144, GQ_Q6_K: 210}
+
+# symbol -> (argtypes, restype); mirrors include/gguf_mmq.h
+_P, _I64, _I, _SZ = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_size_t
+SIGNATURES = {
+    "gq_block_elems": ([_I], _I),
+    "gq_block_bytes": ([_I], _I),
+    "gq_mmq_workspace_size": ([_I, _I64, _I64, _I64], _SZ),
+    "gq_mmq": ([_I, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P], _I),
+    "gq_act_prepare": ([_P, _I64, _I64, _I64, _P, _SZ, _P], _I),
+    "gq_mmq_prepared": ([_I, _P, _P, _P, _I64, _I64, _I64, _I64, _P], _I),
+    "gq_quantize_q8_1": ([_P, _P, _I64, _I64, _I64, _P], _I),
+    "gq_last_error": ([], ctypes.c_char_p),
+    "gq_version": ([], _I),
+}
+
+_lib = None
+
+
+def lib():
+    """The loaded libgguf_mmq.so (raises RuntimeError when it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} not found: build the HIP library first "
+                "(make -C gguf-triton-kernel_amd, or python -c 'import __graft_entry__ as g; g.build()')")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (argtypes, restype) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.argtypes = argtypes
+            fn.restype = restype
+        _lib = handle
+    return _lib
+
+
+def _check(status: int):
+    if status != 0:
+        msg = lib().gq_last_error().decode(errors="replace")
+        raise RuntimeError(f"gguf_mmq error {status}: {msg}")
+
+
+def _require_device(t: torch.Tensor, name: str):
+    if not t.is_cuda:
+        raise RuntimeError(f"{name} must be a ROCm device tensor (got device {t.device}); "
+                           "the MMQ kernels have no CPU path")
+
+
+def workspace_size(gtype: int, M: int, N: int, K: int) -> int:
+    return int(lib().gq_mmq_workspace_size(gtype, M, N, K))
+
+
+def mmq(gtype: int, A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int,
+        out: torch.Tensor | None = None, workspace: torch.Tensor | None = None) -> torch.Tensor:
+    """C = (A @ B^T)^T as fp16 (N, M) on A's device; the common body of mmq_q8_0/q4_k/q6_k."""
+    qk, bb = BLOCK_ELEMS[gtype], BLOCK_BYTES[gtype]
+    _require_device(A, "A")
+    _require_device(B, "B")
+    if A.device != B.device:
+        raise RuntimeError(f"A on {A.device} but B on {B.device}")
+    if A.dtype not in (torch.int8, torch.uint8):
+        raise RuntimeError(f"A must be the packed int8/uint8 block tensor, got {A.dtype}")
+    if not A.is_contiguous():
+        raise RuntimeError("A (packed blocks) must be contiguous")
+    if A.numel() != M * (K // qk) * bb:
+        raise RuntimeError(f"A has {A.numel()} bytes, expected M*K/{qk}*{bb} = {M * (K // qk) * bb}")
+    if B.dtype != torch.float16:
+        B = B.to(torch.float16)
+    if B.dim() != 2 or B.shape[0] != N or B.shape[1] != K:
+        B = B.reshape(N, K)
+    if B.stride(1) != 1:
+        B = B.contiguous()
+    C = out if out is not None else torch.empty((N, M), dtype=torch.float16, device=A.device)
+    if C.dtype != torch.float16 or C.dim() != 2 or C.stride(1) != 1 or C.shape[0] != N or C.shape[1] != M:
+        raise RuntimeError("out must be an fp16 (N, M) tensor with unit column stride")
+    if M == 0 or N == 0:
+        return C
+    need = workspace_size(gtype, M, N, K)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(max(need, 1), dtype=torch.uint8, device=A.device)
+    with torch.cuda.device(A.device):
+        stream = torch.cuda.current_stream(A.device).cuda_stream
+        _check(lib().gq_mmq(gtype, A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, B.stride(0), C.stride(0),
+                            workspace.data_ptr(), workspace.numel(), stream))
+    return C
+
+
+def quantize_q8_1_device(X: torch.Tensor) -> torch.Tensor:
+    """Device q8_1 quantizer (bit-exact with utils/quantize/q8_1.py) -> flat int8 bytes."""
+    _require_device(X, "X")
+    if X.dtype != torch.float16:
+        X = X.to(torch.float16)
+    X2 = X.reshape(-1, X.shape[-1]) if X.dim() > 1 else X.reshape(1, -1)
+    if X2.stride(-1) != 1:
+        X2 = X2.contiguous()
+    rows, K = X2.shape
+    if K % 32 != 0:
+        raise ValueError("The total number of elements must be divisible by 32.")
+    Y = torch.empty(rows * (K // 32) * 36, dtype=torch.int8, device=X.device)
+    with torch.cuda.device(X.device):
+        stream = torch.cuda.current_stream(X.device).cuda_stream
+        _check(lib().gq_quantize_q8_1(X2.data_ptr(), Y.data_ptr(), rows, K, X2.stride(0), stream))
+    return Y

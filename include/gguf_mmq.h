@@ -1,0 +1,84 @@
+/*
+ * gguf_mmq.h -- C ABI of the MI355X GGUF mixed-precision matmul library (libgguf_mmq.so).
+ *
+ * Plain pointers and sizes only: no torch, no HIP types (streams are passed as void*,
+ * i.e. a hipStream_t cast to void*; NULL = the default stream).  All device pointers are
+ * HIP device memory on the current device.  Calls are asynchronous on `stream`, never
+ * synchronise the host and never allocate (graph-capturable).
+ *
+ * Notation follows the reference: A is the packed weight matrix with M rows (output
+ * features), B the fp16 activations with N rows (tokens), C = (A @ B^T)^T is fp16 (N, M).
+ *
+ * Reference interfaces these replace (PowerfulGhost/gguf-triton-kernel @ 2025-11-21):
+ *   gq_mmq(GQ_Q8_0, ...)  <- kernels/mmq_q8_0.py:102  mmq_q8_0(A, B, M, N, K)
+ *   gq_mmq(GQ_Q4_K, ...)  <- kernels/mmq_q4_k.py:240  mmq_q4_k(A, B, M, N, K)
+ *   gq_mmq(GQ_Q6_K, ...)  <- kernels/mmq_q6_k.py:197  mmq_q6_k(A, B, M, N, K)
+ *   gq_quantize_q8_1      <- utils/quantize/q8_1.py:18 quantize_to_q8_1 (on the device)
+ */
+#ifndef GGUF_MMQ_H
+#define GGUF_MMQ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum { GQ_Q8_0 = 0, GQ_Q4_K = 1, GQ_Q6_K = 2 } gq_type;
+
+enum {
+    GQ_OK = 0,
+    GQ_EINVAL = 1,      /* bad argument: null pointer, K not a multiple of the block, ld too small ... */
+    GQ_EHIP = 2,        /* a HIP launch failed (message in gq_last_error) */
+    GQ_EUNSUPPORTED = 3 /* valid but not implemented (unknown type) */
+};
+
+/* Elements per block (32 / 256 / 256) and bytes per block (34 / 144 / 210). */
+int gq_block_elems(gq_type t);
+int gq_block_bytes(gq_type t);
+
+/* Device workspace gq_mmq needs for this shape (bytes; the activation quantizer's output). */
+size_t gq_mmq_workspace_size(gq_type t, int64_t M, int64_t N, int64_t K);
+
+/*
+ * C[n * ldc + m] = sum_k W[m][k] * x~[n][k]  for m < M, n < N (fp16 out, fp32 accumulate)
+ *   A : packed `t` weights, M rows of K/QK blocks, row m at byte m*(K/QK)*block_bytes
+ *   B : fp16 activations, row n at element n*ldb (ldb >= K)
+ *   x~: B quantized exactly as utils/quantize/q8_1.py does (int8 per 32 elements), the
+ *       input the reference's parity oracle (kernels/cpu_impls) consumes.
+ * K must be a multiple of gq_block_elems(t) (the reference asserts the same).
+ * workspace: >= gq_mmq_workspace_size(t, M, N, K) bytes of device memory.
+ * Returns GQ_OK or an error code (gq_last_error() has the text; nothing was launched).
+ */
+int gq_mmq(gq_type t, const void *A, const void *B, void *C, int64_t M, int64_t N, int64_t K, int64_t ldb,
+           int64_t ldc, void *workspace, size_t workspace_bytes, void *stream);
+
+/*
+ * Split form of gq_mmq.  gq_act_prepare quantizes B into `workspace` (layout depends only
+ * on N and K); gq_mmq_prepared then runs the matmul for any weight type/M with that K.
+ * One prepare can serve several weight matrices that share an input (Q/K/V, gate/up).
+ * gq_mmq(...) == gq_act_prepare(...) followed by gq_mmq_prepared(...).
+ */
+int gq_act_prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *workspace, size_t workspace_bytes,
+                   void *stream);
+int gq_mmq_prepared(gq_type t, const void *A, const void *workspace, void *C, int64_t M, int64_t N, int64_t K,
+                    int64_t ldc, void *stream);
+
+/*
+ * q8_1 quantization of fp16 rows on the device, byte-identical to utils/quantize/q8_1.py:
+ * rows x K fp16 (row stride ldx elements) -> rows * K/32 blocks of 36 bytes, row-major.
+ */
+int gq_quantize_q8_1(const void *X, void *Y, int64_t rows, int64_t K, int64_t ldx, void *stream);
+
+/* Text of the last error on this thread ("" if none). */
+const char *gq_last_error(void);
+
+/* Library ABI version (major * 100 + minor). */
+int gq_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GGUF_MMQ_H */

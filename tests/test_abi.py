@@ -1,0 +1,101 @@
+"""The C-ABI libraries load and export every symbol include/*.h declares; host-side argument
+checks behave (no GPU needed: they return before any launch); the drop-in API refuses to
+run anywhere but on a ROCm device (no silent CPU fallback).  CPU only."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "gguf-triton-kernel_amd", "lib")
+
+
+def declared(header):
+    text = open(os.path.join(ROOT, "include", header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(gq_\w+)\s*\(", text)))
+
+
+@pytest.mark.parametrize("header,lib", [("gguf_mmq.h", "libgguf_mmq.so"), ("gguf_quant.h", "libgguf_quant.so")])
+def test_exports_every_declared_symbol(header, lib):
+    names = declared(header)
+    assert len(names) >= 5
+    h = ctypes.CDLL(os.path.join(LIB, lib))
+    missing = [n for n in names if not hasattr(h, n)]
+    assert not missing, missing
+
+
+def test_python_signatures_cover_header():
+    import kernels._lib as kl
+    assert sorted(kl.SIGNATURES) == declared("gguf_mmq.h")
+
+
+def test_block_sizes_and_version():
+    import kernels._lib as kl
+    L = kl.lib()
+    assert [L.gq_block_elems(t) for t in (0, 1, 2)] == [32, 256, 256]
+    assert [L.gq_block_bytes(t) for t in (0, 1, 2)] == [34, 144, 210]
+    assert L.gq_version() >= 100
+
+
+def test_host_argument_checks():
+    import kernels._lib as kl
+    L = kl.lib()
+    p = ctypes.c_void_p(16)
+    # K not a multiple of the block
+    assert L.gq_mmq(1, p, p, p, 4, 4, 100, 100, 4, p, 1 << 20, None) == 1
+    assert b"multiple of 256" in L.gq_last_error()
+    assert L.gq_mmq(0, p, p, p, 4, 4, 48, 48, 4, p, 1 << 20, None) == 1
+    # unknown type
+    assert L.gq_mmq(7, p, p, p, 4, 4, 256, 256, 4, p, 1 << 20, None) == 3
+    # empty problems are a no-op, even with null pointers
+    assert L.gq_mmq(1, None, None, None, 0, 4, 256, 256, 4, None, 0, None) == 0
+    assert L.gq_mmq(1, None, None, None, 4, 0, 256, 256, 4, None, 0, None) == 0
+    # null pointers, short leading dimensions, short workspace
+    assert L.gq_mmq(1, None, p, p, 4, 4, 256, 256, 4, p, 1 << 20, None) == 1
+    assert L.gq_mmq(1, p, p, p, 4, 4, 256, 255, 4, p, 1 << 20, None) == 1
+    assert L.gq_mmq(1, p, p, p, 4, 4, 256, 256, 3, p, 1 << 20, None) == 1
+    need = L.gq_mmq_workspace_size(1, 4, 4, 256)
+    assert need > 0
+    assert L.gq_mmq(1, p, p, p, 4, 4, 256, 256, 4, p, need - 1, None) == 1
+    assert b"workspace" in L.gq_last_error()
+    assert L.gq_quantize_q8_1(p, p, 2, 40, 40, None) == 1
+
+
+def test_workspace_sizes():
+    import kernels._lib as kl
+    for t in (0, 1, 2):
+        small = kl.workspace_size(t, 4096, 1, 4096)
+        big = kl.workspace_size(t, 4096, 128, 4096)
+        assert 0 < small < big
+        assert kl.workspace_size(t, 4096, 0, 4096) == 0
+
+
+def test_dropin_refuses_cpu_tensors():
+    from kernels.mmq_q4_k import mmq_q4_k
+    from kernels.mmq_q6_k import mmq_q6_k
+    from kernels.mmq_q8_0 import mmq_q8_0
+    A = torch.zeros(144 * 2, dtype=torch.int8)
+    B = torch.zeros(1, 256, dtype=torch.float16)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        mmq_q4_k(A, B, 2, 1, 256)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        mmq_q6_k(torch.zeros(210 * 2, dtype=torch.int8), B, 2, 1, 256)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        mmq_q8_0(torch.zeros(34 * 16, dtype=torch.int8), B, 2, 1, 256)
+
+
+def test_dropin_k_assertions():
+    """The reference asserts K divisibility (mmq_q8_0.py:124, mmq_q4_k.py:263, mmq_q6_k.py:211)."""
+    from kernels.mmq_q4_k import mmq_q4_k
+    from kernels.mmq_q6_k import mmq_q6_k
+    from kernels.mmq_q8_0 import mmq_q8_0
+    B = torch.zeros(1, 48, dtype=torch.float16)
+    with pytest.raises(AssertionError):
+        mmq_q8_0(torch.zeros(34, dtype=torch.int8), B, 1, 1, 48)
+    with pytest.raises(AssertionError):
+        mmq_q4_k(torch.zeros(144, dtype=torch.int8), B, 1, 1, 128)
+    with pytest.raises(AssertionError):
+        mmq_q6_k(torch.zeros(210, dtype=torch.int8), B, 1, 1, 300)
