@@ -123,8 +123,8 @@ class Runner:
 
     def kernel(self, i):
         A = self.weights[i % self.ncopies]
-        rc = self.L.gq_mmq_prepared(self.gtype, A.data_ptr(), self.ws.data_ptr(), self.C[i & 1].data_ptr(), self.M,
-                                    self.N, self.K, self.M, self._stream())
+        rc = self.L.gq_mmq_prepared(self.gtype, A.data_ptr(), self.ws.data_ptr(), self.ws_bytes,
+                                    self.C[i & 1].data_ptr(), self.M, self.N, self.K, self.M, self._stream())
         if rc:
             raise RuntimeError(self.L.gq_last_error().decode())
 

@@ -17,7 +17,13 @@ hipError_t launch_gemv(int fmt, const uint8_t *A, const int8_t *xq, const float 
                        int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
 
 // Batched GEMM on fp16 MFMA (mmq_gemm.hip): C[t][m] from the dequantized activation x~.
-hipError_t launch_gemm(int fmt, const uint8_t *A, const uint16_t *xdeq, uint16_t *C, int64_t M, int64_t N,
-                       int64_t K, int64_t ldc, hipStream_t s);
+struct GemmPlan {
+    int splits = 1;            // split-K factor (grid.z)
+    int chunks_per_split = 1;  // 128-wide K chunks per split
+    size_t partial_bytes = 0;  // fp32 partial slabs needed when splits > 1
+};
+GemmPlan plan_gemm(int64_t M, int64_t N, int64_t K);
+hipError_t launch_gemm(int fmt, const uint8_t *A, const uint16_t *xdeq, uint16_t *C, float *partials,
+                       const GemmPlan &plan, int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
 
 } // namespace gq

@@ -33,13 +33,22 @@ constexpr int64_t kGemvMaxTokens = 8;
 
 bool use_gemv(int64_t N) { return N <= kGemvMaxTokens; }
 
-size_t ws_bytes(int64_t N, int64_t K)
+// Activation part of the workspace (what gq_act_prepare writes); depends on N, K only.
+size_t act_bytes(int64_t N, int64_t K)
 {
     if (use_gemv(N)) {
         // SOA q8_1: codes + d + s
         return align_up((size_t)N * K) + 2 * align_up((size_t)N * (K / 32) * sizeof(float));
     }
     return align_up((size_t)N * K * 2); // dequantized fp16 activation
+}
+
+// Whole workspace: activations + (GEMM split-K) fp32 partial slabs.
+size_t ws_bytes(int64_t M, int64_t N, int64_t K)
+{
+    size_t b = act_bytes(N, K);
+    if (!use_gemv(N)) b += align_up(gq::plan_gemm(M, N, K).partial_bytes);
+    return b;
 }
 
 } // namespace
@@ -54,9 +63,8 @@ const char *gq_last_error(void) { return g_err.c_str(); }
 size_t gq_mmq_workspace_size(gq_type t, int64_t M, int64_t N, int64_t K)
 {
     (void)t;
-    (void)M;
-    if (N <= 0 || K <= 0) return 0;
-    return ws_bytes(N, K);
+    if (N <= 0 || K <= 0 || M < 0) return 0;
+    return ws_bytes(M, N, K);
 }
 
 static int check_common(gq_type t, int64_t M, int64_t N, int64_t K)
@@ -73,6 +81,7 @@ struct Carved {
     int8_t *xq;
     float *xd, *xs;
     uint16_t *xdeq;
+    float *partials;
 };
 
 static Carved carve(void *workspace, int64_t N, int64_t K)
@@ -85,6 +94,7 @@ static Carved carve(void *workspace, int64_t N, int64_t K)
         c.xs = (float *)((uint8_t *)c.xd + align_up((size_t)N * (K / 32) * sizeof(float)));
     } else {
         c.xdeq = (uint16_t *)ws;
+        c.partials = (float *)(ws + act_bytes(N, K));
     }
     return c;
 }
@@ -94,7 +104,7 @@ static int prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *works
 {
     if (!B) return fail(GQ_EINVAL, "null activation pointer");
     if (ldb < K) return fail(GQ_EINVAL, "ldb=%lld < K=%lld", (long long)ldb, (long long)K);
-    const size_t need = ws_bytes(N, K);
+    const size_t need = act_bytes(N, K);
     if (!workspace || workspace_bytes < need)
         return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace ? workspace_bytes : (size_t)0, need);
     Carved c = carve(workspace, N, K);
@@ -105,14 +115,17 @@ static int prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *works
     return GQ_OK;
 }
 
-static int compute(gq_type t, const void *A, const void *workspace, void *C, int64_t M, int64_t N, int64_t K,
-                   int64_t ldc, hipStream_t s)
+static int compute(gq_type t, const void *A, void *workspace, size_t workspace_bytes, void *C, int64_t M,
+                   int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
     if (!A || !C || !workspace) return fail(GQ_EINVAL, "null pointer (A=%p C=%p workspace=%p)", A, C, workspace);
     if (ldc < M) return fail(GQ_EINVAL, "ldc=%lld < M=%lld", (long long)ldc, (long long)M);
-    Carved c = carve((void *)workspace, N, K);
+    const size_t need = ws_bytes(M, N, K);
+    if (workspace_bytes < need) return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace_bytes, need);
+    Carved c = carve(workspace, N, K);
     hipError_t e = use_gemv(N) ? gq::launch_gemv(t, (const uint8_t *)A, c.xq, c.xd, c.xs, (uint16_t *)C, M, N, K, ldc, s)
-                               : gq::launch_gemm(t, (const uint8_t *)A, c.xdeq, (uint16_t *)C, M, N, K, ldc, s);
+                               : gq::launch_gemm(t, (const uint8_t *)A, c.xdeq, (uint16_t *)C, c.partials,
+                                                 gq::plan_gemm(M, N, K), M, N, K, ldc, s);
     if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (mmq): %s", hipGetErrorString(e));
     return GQ_OK;
 }
@@ -127,9 +140,12 @@ int gq_mmq(gq_type t, const void *A, const void *B, void *C, int64_t M, int64_t 
     if (K == 0) return fail(GQ_EINVAL, "K must be positive");
     if (!A || !B || !C) return fail(GQ_EINVAL, "null pointer (A=%p B=%p C=%p)", A, B, C);
     if (ldc < M) return fail(GQ_EINVAL, "ldc=%lld < M=%lld", (long long)ldc, (long long)M);
+    if (!workspace || workspace_bytes < ws_bytes(M, N, K))
+        return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace ? workspace_bytes : (size_t)0,
+                    ws_bytes(M, N, K));
     rc = prepare(B, N, K, ldb, workspace, workspace_bytes, (hipStream_t)stream);
     if (rc != GQ_OK) return rc;
-    return compute(t, A, workspace, C, M, N, K, ldc, (hipStream_t)stream);
+    return compute(t, A, workspace, workspace_bytes, C, M, N, K, ldc, (hipStream_t)stream);
 }
 
 int gq_act_prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *workspace, size_t workspace_bytes,
@@ -142,15 +158,15 @@ int gq_act_prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *works
     return prepare(B, N, K, ldb, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
-int gq_mmq_prepared(gq_type t, const void *A, const void *workspace, void *C, int64_t M, int64_t N, int64_t K,
-                    int64_t ldc, void *stream)
+int gq_mmq_prepared(gq_type t, const void *A, void *workspace, size_t workspace_bytes, void *C, int64_t M, int64_t N,
+                    int64_t K, int64_t ldc, void *stream)
 {
     g_err.clear();
     int rc = check_common(t, M, N, K);
     if (rc != GQ_OK) return rc;
     if (M == 0 || N == 0) return GQ_OK;
     if (K == 0) return fail(GQ_EINVAL, "K must be positive");
-    return compute(t, A, workspace, C, M, N, K, ldc, (hipStream_t)stream);
+    return compute(t, A, workspace, workspace_bytes, C, M, N, K, ldc, (hipStream_t)stream);
 }
 
 int gq_quantize_q8_1(const void *X, void *Y, int64_t rows, int64_t K, int64_t ldx, void *stream)

@@ -1,211 +1,305 @@
 // mmq_gemm.hip -- batched MMQ (many tokens) on the fp16 matrix cores.
 //
-// C[t][m] = sum_k W[m][k] * x~[t][k], W dequantized in registers from the packed GGUF
-// blocks, x~ = fp16(d*q) the q8_1-quantized activation (act_quant.hip, DEQ form), both fed
-// to v_mfma_f32_16x16x32_f16 with fp32 accumulation.  fp16 (not bf16) operands: the
-// reference's activations are fp16, and bf16 would drop three of their mantissa bits.
+// C[t][m] = sum_k W[m][k] * x~[t][k]: W dequantized in registers from the packed GGUF
+// blocks, x~ = fp16(d*q) the q8_1-quantized activation (act_quant.hip, DEQ form) -- the same
+// integer activations kernels/cpu_impls multiplies (mmq_*_q8_1_cpu.py) -- fed to
+// v_mfma_f32_32x32x16_f16 with fp32 accumulation.  fp16 operands, not bf16: the reference's
+// activations are fp16 and bf16 would drop three of their mantissa bits.
 //
-// Tile: a 256-thread workgroup owns BM=64 weight rows x BN=64 tokens; its 4 waves split
-// that 2x2 into 32x32 sub-tiles (2x2 MFMA tiles of 16x16 each).  K advances one 256-wide
-// step at a time (one Q4_K/Q6_K super-block, eight Q8_0 blocks):
-//   1. the 64-token x 256-k activation tile is copied to LDS (16-byte loads / ds_write_b128,
-//      rows padded by 16 B so the 16-lane ds_read_b128 groups hit distinct banks);
-//   2. every lane loads ITS weight bytes for the step straight from HBM -- lane (r, kg)
-//      needs elements 32s+8kg..+7 of row r for s = 0..7 -- and dequantizes them to 8
-//      fp16 fragments per row tile (w = d*q, d*sc*q - dmin*m, d*sc*(q-32));
-//   3. 8 sub-steps x 2x2 MFMAs, B fragments read from LDS.
-// MFMA operand maps (gfx950 16x16x32 f16): lane l holds A[row l&15][k 8(l>>4)+j] and
-// B[k 8(l>>4)+j][col l&15]; D[row 4(l>>4)+i][col l&15] in acc element i.
+// Work decomposition
+//   workgroup = 4 waves = 128 weight rows x 32*NT tokens (NT = 1..4 token tiles of 32);
+//   wave w owns rows 32w..32w+31 of the tile and all NT token tiles (NT accumulators of
+//   32x32 f32).  K advances in 128-element chunks; grid.z splits the chunks (split-K) when
+//   the row x token tiles alone would not fill the chip -- fp32 partial slabs, summed in
+//   fixed order by gemm_reduce_kernel (deterministic).
+// Per chunk
+//   B (activations): the 32*NT x 128 fp16 tile goes HBM/L2 -> LDS by LDS-DMA
+//     (global_load_lds_dwordx4, no VGPRs), double-buffered so chunk c+1 streams in while
+//     chunk c is multiplied.  LDS rows are 256 B; 16-byte pieces are XOR-swizzled by
+//     (row & 15) on the SOURCE address (the DMA destination is lane-linear), and reads apply
+//     the same XOR, so each 16-lane ds_read_b128 group touches 16 distinct bank quads.
+//   A (weights): lane (row = lane&31, half = lane>>5) loads its 64-weight "unit" u = 2c+half
+//     straight from HBM with 16-byte loads (gguf_units.hpp), one chunk ahead, and
+//     dequantizes 8 weights per MFMA k-step into fp16 in registers.  The 64 weights of a
+//     unit are mapped onto the 8 k-steps of the chunk in whatever order the unit stores
+//     them; the B fragment is read from LDS with the same permutation (MFMA sums over k,
+//     so any consistent permutation is exact).
+// MFMA 32x32x16 f16 operand maps (gfx950): lane l holds A[row l&31][k 8(l>>5)+j] and
+// B[k 8(l>>5)+j][col l&31]; D[row (i&3)+8(i>>2)+4(l>>5)][col l&31] in acc element i.
 #include "gguf_blocks.hpp"
 #include "gguf_internal.hpp"
+#include "gguf_units.hpp"
 
 namespace gq {
 
 namespace {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void lds_void;
 
-constexpr int BM = 64, BN = 64, KS = 256;
-constexpr int LDS_ROW = KS * 2 + 16; // bytes per token row in LDS (padded)
+constexpr int KC = 128;         // K elements per chunk
+constexpr int ROW_B = KC * 2;   // LDS bytes per token row of a chunk
+constexpr int BM = 128;         // weight rows per workgroup
 
-// Eight sub-step fragments of one weight row for K-step kb: frag[s][j] = W[row][256kb+32s+8kg+j].
-template <int F>
-__device__ __forceinline__ void load_afrag(const uint8_t *__restrict__ rowp, int64_t kb, int kg, int64_t nb32,
-                                           f16x8 (&frag)[8])
+__device__ __forceinline__ uint32_t pk_f16(float a, float b)
 {
-    if constexpr (F == Q8_0) {
+    return (uint32_t)f2h_bits(a) | ((uint32_t)f2h_bits(b) << 16);
+}
+
+__device__ __forceinline__ f16x8 as_f16x8(uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+{
+    u32x4 v = {a, b, c, d};
+    return __builtin_bit_cast(f16x8, v);
+}
+
+// fp16 fragment for k-step t (0..7) of a unit: 8 weights.
+template <int F>
+__device__ __forceinline__ f16x8 unit_frag(const UnitRaw<F> &r, int t);
+
+template <>
+__device__ __forceinline__ f16x8 unit_frag<Q8_0>(const UnitRaw<Q8_0> &r, int t)
+{
+    const float d = t < 4 ? r.d0 : r.d1;
+    const uint32_t w0 = r.w[2 * t], w1 = r.w[2 * t + 1];
+    float v[8];
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            const int64_t blk = 8 * kb + s;
-            if (blk < nb32) {
-                const uint8_t *p = rowp + 34 * blk;
-                const float d = h2f(ld2(p));
-                const u32x2 q = ld8(p + 2 + 8 * kg);
+    for (int j = 0; j < 4; ++j) {
+        v[j] = d * (float)(int8_t)((w0 >> (8 * j)) & 0xff);
+        v[4 + j] = d * (float)(int8_t)((w1 >> (8 * j)) & 0xff);
+    }
+    return as_f16x8(pk_f16(v[0], v[1]), pk_f16(v[2], v[3]), pk_f16(v[4], v[5]), pk_f16(v[6], v[7]));
+}
+
+template <>
+__device__ __forceinline__ f16x8 unit_frag<Q4_K>(const UnitRaw<Q4_K> &r, int t)
+{
+    const int tt = t & 3, sh = t < 4 ? 0 : 4;
+    const float ds = t < 4 ? r.ds0 : r.ds1, dm = t < 4 ? r.dm0 : r.dm1;
+    const uint32_t w0 = r.w[2 * tt] >> sh, w1 = r.w[2 * tt + 1] >> sh;
+    float v[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const uint32_t w = j < 4 ? q.x : q.y;
-                    const int v = (int)(int8_t)((w >> (8 * (j & 3))) & 0xff);
-                    frag[s][j] = (_Float16)(d * (float)v);
+    for (int j = 0; j < 4; ++j) {
+        v[j] = ds * (float)((w0 >> (8 * j)) & 0xf) - dm;
+        v[4 + j] = ds * (float)((w1 >> (8 * j)) & 0xf) - dm;
+    }
+    return as_f16x8(pk_f16(v[0], v[1]), pk_f16(v[2], v[3]), pk_f16(v[4], v[5]), pk_f16(v[6], v[7]));
+}
+
+template <>
+__device__ __forceinline__ f16x8 unit_frag<Q6_K>(const UnitRaw<Q6_K> &r, int t)
+{
+    const int tt = t & 3;
+    const uint32_t *c = t < 4 ? r.ca : r.cb;
+    const float s = t < 4 ? (tt < 2 ? r.fa1 : r.fa2) : (tt < 2 ? r.fb1 : r.fb2);
+    const uint32_t w0 = c[2 * tt], w1 = c[2 * tt + 1];
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        v[j] = s * (float)((int)((w0 >> (8 * j)) & 0xff) - 32);
+        v[4 + j] = s * (float)((int)((w1 >> (8 * j)) & 0xff) - 32);
+    }
+    return as_f16x8(pk_f16(v[0], v[1]), pk_f16(v[2], v[3]), pk_f16(v[4], v[5]), pk_f16(v[6], v[7]));
+}
+
+// Which 8-element piece (0..15) of the 128-wide chunk k-step t of half h multiplies.
+template <int F>
+__device__ __forceinline__ int piece_of(int h, int t)
+{
+    if constexpr (F == Q6_K) return t < 4 ? 4 * h + t : 8 + 4 * h + (t - 4);
+    return 8 * h + t;
+}
+
+// Issue the LDS-DMA for chunk c of the activation tile into `buf` (tokens n0.., 32*NT rows).
+template <int NT>
+__device__ __forceinline__ void stage_b(uint8_t *buf, const uint16_t *__restrict__ X, int64_t n0, int64_t N,
+                                        int64_t K, int64_t c, int wave, int lane)
+{
+    constexpr int INSTR = 8 * NT; // 1 KiB (4 token rows) per wave-instruction
+#pragma unroll
+    for (int q = wave; q < INSTR; q += 4) {
+        const int row = 4 * q + (lane >> 4);
+        const int piece = (lane & 15) ^ (row & 15);
+        int64_t tok = n0 + row;
+        tok = tok < N ? tok : N - 1;
+        int64_t k = c * KC + 8 * piece;
+        k = k < K - 8 ? k : K - 8;
+        __builtin_amdgcn_global_load_lds((const void *)(X + tok * K + k), (lds_void *)(buf + q * 1024), 16, 0, 0);
+    }
+}
+
+template <int F, int NT>
+__global__ __launch_bounds__(256) void gemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
+                                                   uint16_t *__restrict__ C, float *__restrict__ P, int64_t M,
+                                                   int64_t N, int64_t K, int64_t ldc, int chunks_per_split)
+{
+    using L = Layout<F>;
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[2 * 32 * NT * ROW_B];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, r32 = lane & 31;
+    const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * 32 * NT;
+    const int64_t nchunks = (K + KC - 1) / KC;
+    const int64_t c0 = (int64_t)blockIdx.z * chunks_per_split;
+    const int64_t c1 = c0 + chunks_per_split < nchunks ? c0 + chunks_per_split : nchunks;
+    const int64_t row_bytes = (K / L::QK) * L::BYTES;
+    const int64_t nb32 = K / 32;
+
+    int64_t row = m0 + 32 * wave + r32;
+    const uint8_t *rowp = A + (row < M ? row : M - 1) * row_bytes;
+
+    f32x16 acc[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+
+    UnitRaw<F> nxt;
+    if (c0 < c1) {
+        stage_b<NT>(lds, X, n0, N, K, c0, wave, lane);
+        nxt.load(rowp, (int)(2 * c0 + h), nb32);
+    }
+    __syncthreads();
+
+    for (int64_t c = c0; c < c1; ++c) {
+        const UnitRaw<F> cur = nxt;
+        uint8_t *buf = lds + ((c - c0) & 1) * (32 * NT * ROW_B);
+        if (c + 1 < c1) {
+            stage_b<NT>(lds + ((c + 1 - c0) & 1) * (32 * NT * ROW_B), X, n0, N, K, c + 1, wave, lane);
+            nxt.load(rowp, (int)(2 * (c + 1) + h), nb32);
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const f16x8 a = unit_frag<F>(cur, t);
+            const int piece = piece_of<F>(h, t);
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const int trow = 32 * nt + r32;
+                const f16x8 b = *(const f16x8 *)(buf + trow * ROW_B + 16 * (piece ^ (trow & 15)));
+                acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc[nt], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+
+    // epilogue: acc[nt][i] = D[row 32w + (i&3) + 8(i>>2) + 4h][token 32nt + r32]
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int64_t tok = n0 + 32 * nt + r32;
+        if (tok >= N) continue;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int64_t rr = m0 + 32 * wave + 8 * g + 4 * h;
+            const float v0 = acc[nt][4 * g], v1 = acc[nt][4 * g + 1], v2 = acc[nt][4 * g + 2], v3 = acc[nt][4 * g + 3];
+            if (P == nullptr) {
+                uint16_t *cp = C + tok * ldc + rr;
+                if (rr + 3 < M) {
+                    u32x2 o = {pk_f16(v0, v1), pk_f16(v2, v3)};
+                    __builtin_memcpy(cp, &o, 8);
+                } else {
+                    const float vv[4] = {v0, v1, v2, v3};
+                    for (int e = 0; e < 4; ++e)
+                        if (rr + e < M) cp[e] = f2h_bits(vv[e]);
                 }
             } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) frag[s][j] = (_Float16)0.f;
-            }
-        }
-    } else if constexpr (F == Q4_K) {
-        const uint8_t *p = rowp + 144 * kb;
-        const u32x4 hdr = ld16(p);
-        const float d = h2f(hdr.x & 0xffffu), dmin = h2f(hdr.x >> 16);
-        const uint32_t sw[3] = {hdr.y, hdr.z, hdr.w};
-#pragma unroll
-        for (int pch = 0; pch < 4; ++pch) {
-            const u32x2 q = ld8(p + 16 + 32 * pch + 8 * kg);
-#pragma unroll
-            for (int hi = 0; hi < 2; ++hi) {
-                const int s = 2 * pch + hi;
-                int sc, m;
-                q4k_sc_m(sw, s, sc, m);
-                const float ds = d * (float)sc, dm = dmin * (float)m;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const uint32_t w = j < 4 ? q.x : q.y;
-                    const int v = (int)((w >> (8 * (j & 3) + 4 * hi)) & 0xf);
-                    frag[s][j] = (_Float16)(ds * (float)v - dm);
-                }
-            }
-        }
-    } else {
-        const uint8_t *p = rowp + 210 * kb;
-        const float d = h2f(ld2(p + 208));
-        const u32x4 sc = ld16(p + 192);
-        const uint32_t scw[4] = {sc.x, sc.y, sc.z, sc.w};
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const u32x2 qh = ld8(p + 128 + 32 * h + 8 * kg);
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const u32x2 ql = ld8(p + 64 * h + 32 * c + 8 * kg);
-#pragma unroll
-                for (int nib = 0; nib < 2; ++nib) {
-                    const int s = 4 * h + 2 * nib + c; // s&1 = c, (s>>1)&1 = nib, s>>2 = h
-                    const int si = 2 * s + (kg >> 1);
-                    const float ds = d * (float)(int8_t)((scw[si >> 2] >> (8 * (si & 3))) & 0xff);
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const uint32_t lw = j < 4 ? ql.x : ql.y;
-                        const uint32_t hw = j < 4 ? qh.x : qh.y;
-                        const int lo = (int)((lw >> (8 * (j & 3) + 4 * nib)) & 0xf);
-                        const int hb = (int)((hw >> (8 * (j & 3) + 2 * (s & 3))) & 0x3);
-                        frag[s][j] = (_Float16)(ds * (float)((lo | (hb << 4)) - 32));
-                    }
+                float *pp = P + ((int64_t)blockIdx.z * N + tok) * M + rr;
+                if (rr + 3 < M) {
+                    u32x4 o = {__builtin_bit_cast(uint32_t, v0), __builtin_bit_cast(uint32_t, v1),
+                               __builtin_bit_cast(uint32_t, v2), __builtin_bit_cast(uint32_t, v3)};
+                    __builtin_memcpy(pp, &o, 16);
+                } else {
+                    const float vv[4] = {v0, v1, v2, v3};
+                    for (int e = 0; e < 4; ++e)
+                        if (rr + e < M) pp[e] = vv[e];
                 }
             }
         }
     }
 }
 
-template <int F>
-__global__ __launch_bounds__(256) void gemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
-                                                   uint16_t *__restrict__ C, int64_t M, int64_t N, int64_t K,
-                                                   int64_t ldc)
+// C[t][m] = fp16(sum_s P[s][t][m]), summed in split order.
+__global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restrict__ P, uint16_t *__restrict__ C,
+                                                          int64_t M, int64_t N, int64_t ldc, int S)
 {
-    using L = Layout<F>;
-    __shared__ __attribute__((aligned(16))) uint8_t Bs[BN * LDS_ROW];
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave & 1, wn = wave >> 1;
-    const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * BN;
-    const int64_t row_bytes = (K / L::QK) * L::BYTES;
-    const int64_t nb32 = K / 32;
-    const int64_t ksteps = (K + KS - 1) / KS;
-    const int r16 = lane & 15, kg = lane >> 4;
-
-    f32x4 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-    const uint8_t *rowp[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        int64_t r = m0 + 32 * wm + 16 * i + r16;
-        rowp[i] = A + (r < M ? r : M - 1) * row_bytes;
-    }
-
-    for (int64_t kb = 0; kb < ksteps; ++kb) {
-        // 1. activation tile -> LDS: 64 tokens x 512 B; thread handles 8 x 16 B
-        __syncthreads();
-#pragma unroll
-        for (int it = 0; it < 8; ++it) {
-            const int idx = it * 256 + tid; // 2048 chunks of 16 B
-            const int trow = idx >> 5, chunk = idx & 31;
-            const int64_t tok = n0 + trow;
-            const int64_t k = kb * KS + 8 * chunk;
-            u32x4 v = {0, 0, 0, 0};
-            if (tok < N && k < K) v = ld16(X + tok * K + k);
-            *(u32x4 *)(Bs + trow * LDS_ROW + 16 * chunk) = v;
+    const int64_t m4 = (M + 3) / 4;
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= N * m4) return;
+    const int64_t tok = idx / m4, m = 4 * (idx - tok * m4);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    if (m + 3 < M && (M & 3) == 0) {
+        for (int s = 0; s < S; ++s) {
+            u32x4 v = ld16(P + ((int64_t)s * N + tok) * M + m);
+            s0 += __builtin_bit_cast(float, v.x);
+            s1 += __builtin_bit_cast(float, v.y);
+            s2 += __builtin_bit_cast(float, v.z);
+            s3 += __builtin_bit_cast(float, v.w);
         }
-        __syncthreads();
-
-        // 2. weight fragments for this step
-        f16x8 fa[2][8];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) load_afrag<F>(rowp[i], kb, kg, nb32, fa[i]);
-
-        // 3. MFMAs
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            f16x8 fb[2];
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int trow = 32 * wn + 16 * j + r16;
-                fb[j] = *(const f16x8 *)(Bs + trow * LDS_ROW + 2 * (32 * s + 8 * kg));
-            }
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i][s], fb[j], acc[i][j], 0, 0, 0);
+        u32x2 o = {pk_f16(s0, s1), pk_f16(s2, s3)};
+        __builtin_memcpy(C + tok * ldc + m, &o, 8);
+    } else {
+        for (int e = 0; e < 4 && m + e < M; ++e) {
+            float acc = 0.f;
+            for (int s = 0; s < S; ++s) acc += P[((int64_t)s * N + tok) * M + m + e];
+            C[tok * ldc + m + e] = f2h_bits(acc);
         }
     }
+}
 
-    // epilogue: lane holds rows 4kg..4kg+3 of token column r16 -> 8 contiguous bytes of C
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int64_t tok = n0 + 32 * wn + 16 * j + r16;
-            const int64_t row = m0 + 32 * wm + 16 * i + 4 * kg;
-            if (tok >= N) continue;
-            uint16_t *cp = C + tok * ldc + row;
-            if (row + 3 < M) {
-                u32x2 o;
-                o.x = (uint32_t)f2h_bits(acc[i][j][0]) | ((uint32_t)f2h_bits(acc[i][j][1]) << 16);
-                o.y = (uint32_t)f2h_bits(acc[i][j][2]) | ((uint32_t)f2h_bits(acc[i][j][3]) << 16);
-                __builtin_memcpy(cp, &o, 8);
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (row + e < M) cp[e] = f2h_bits(acc[i][j][e]);
-            }
-        }
+template <int F, int NT>
+hipError_t launch_nt(const uint8_t *A, const uint16_t *X, uint16_t *C, float *P, int S, int cps, int64_t M, int64_t N,
+                     int64_t K, int64_t ldc, hipStream_t s)
+{
+    dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((N + 32 * NT - 1) / (32 * NT)), (unsigned)S), block(256);
+    gemm_kernel<F, NT><<<grid, block, 0, s>>>(A, X, C, S > 1 ? P : nullptr, M, N, K, ldc, cps);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || S == 1) return e;
+    const int64_t work = N * ((M + 3) / 4);
+    gemm_reduce_kernel<<<dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s>>>(P, C, M, N, ldc, S);
+    return hipGetLastError();
+}
+
+template <int F>
+hipError_t launch_fmt(const uint8_t *A, const uint16_t *X, uint16_t *C, float *P, int S, int cps, int64_t M,
+                      int64_t N, int64_t K, int64_t ldc, hipStream_t s)
+{
+    const int nt = N >= 97 ? 4 : (N >= 65 ? 3 : (N >= 33 ? 2 : 1));
+    switch (nt) {
+    case 1: return launch_nt<F, 1>(A, X, C, P, S, cps, M, N, K, ldc, s);
+    case 2: return launch_nt<F, 2>(A, X, C, P, S, cps, M, N, K, ldc, s);
+    case 3: return launch_nt<F, 3>(A, X, C, P, S, cps, M, N, K, ldc, s);
+    default: return launch_nt<F, 4>(A, X, C, P, S, cps, M, N, K, ldc, s);
     }
 }
 
 } // namespace
 
-hipError_t launch_gemm(int fmt, const uint8_t *A, const uint16_t *X, uint16_t *C, int64_t M, int64_t N, int64_t K,
-                       int64_t ldc, hipStream_t s)
+GemmPlan plan_gemm(int64_t M, int64_t N, int64_t K)
 {
-    dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((N + BN - 1) / BN)), block(256);
+    GemmPlan p;
+    const int nt = N >= 97 ? 4 : (N >= 65 ? 3 : (N >= 33 ? 2 : 1));
+    const int64_t tiles = ((M + BM - 1) / BM) * ((N + 32 * nt - 1) / (32 * nt));
+    const int64_t nchunks = (K + KC - 1) / KC;
+    const int64_t target = 256; // one workgroup per CU
+    int64_t S = tiles >= target ? 1 : (target + tiles / 2) / tiles;
+    const int64_t max_split = nchunks / 4 > 0 ? nchunks / 4 : 1; // >= 4 chunks per split
+    if (S > max_split) S = max_split;
+    if (S < 1) S = 1;
+    int64_t cps = (nchunks + S - 1) / S;
+    S = (nchunks + cps - 1) / cps;
+    p.splits = (int)S;
+    p.chunks_per_split = (int)cps;
+    p.partial_bytes = S > 1 ? (size_t)S * N * M * sizeof(float) : 0;
+    return p;
+}
+
+hipError_t launch_gemm(int fmt, const uint8_t *A, const uint16_t *X, uint16_t *C, float *P, const GemmPlan &plan,
+                       int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s)
+{
     switch (fmt) {
-    case Q8_0: gemm_kernel<Q8_0><<<grid, block, 0, s>>>(A, X, C, M, N, K, ldc); break;
-    case Q4_K: gemm_kernel<Q4_K><<<grid, block, 0, s>>>(A, X, C, M, N, K, ldc); break;
-    default: gemm_kernel<Q6_K><<<grid, block, 0, s>>>(A, X, C, M, N, K, ldc); break;
+    case Q8_0: return launch_fmt<Q8_0>(A, X, C, P, plan.splits, plan.chunks_per_split, M, N, K, ldc, s);
+    case Q4_K: return launch_fmt<Q4_K>(A, X, C, P, plan.splits, plan.chunks_per_split, M, N, K, ldc, s);
+    default: return launch_fmt<Q6_K>(A, X, C, P, plan.splits, plan.chunks_per_split, M, N, K, ldc, s);
     }
-    return hipGetLastError();
 }
 
 } // namespace gq

@@ -18,24 +18,11 @@
 // the row group.  Loop over row groups is grid-strided.
 #include "gguf_blocks.hpp"
 #include "gguf_internal.hpp"
+#include "gguf_units.hpp"
 
 namespace gq {
 
 namespace {
-
-template <int F>
-__device__ __forceinline__ void unit_blocks(int u, int &b0, int &b1)
-{
-    if constexpr (F == Q6_K) {
-        // unit u = 4*sb + 2*h + v covers elements 128h+32v+[0,32) and 128h+64+32v+[0,32)
-        const int sb = u >> 2, h = (u >> 1) & 1, v = u & 1;
-        b0 = 8 * sb + 4 * h + v;
-        b1 = b0 + 2;
-    } else {
-        b0 = 2 * u;
-        b1 = 2 * u + 1;
-    }
-}
 
 template <int F, int NT>
 struct Act {
@@ -51,7 +38,7 @@ __device__ __forceinline__ void load_act(Act<F, NT> &a, const int8_t *__restrict
 {
     const int64_t nb = K / 32;
     int b0, b1;
-    unit_blocks<F>(u, b0, b1);
+    act_blocks<F>(u, b0, b1);
     const bool has1 = b1 < nb;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -90,89 +77,48 @@ template <int F, int NT>
 __device__ __forceinline__ void unit_dot(const uint8_t *__restrict__ rowp, int u, int64_t nb, const Act<F, NT> &a,
                                          float (&acc)[NT])
 {
+    UnitRaw<F> r;
+    r.load(rowp, u, nb);
     if constexpr (F == Q8_0) {
-        const uint8_t *p = rowp + 68 * u;
-        const bool has1 = 2 * u + 1 < nb;
-        const float dw0 = h2f(ld2(p));
-        const u32x4 a0 = ld16(p + 2), a1 = ld16(p + 18);
-        float dw1 = 0.f;
-        u32x4 a2 = {0, 0, 0, 0}, a3 = {0, 0, 0, 0};
-        if (has1) {
-            dw1 = h2f(ld2(p + 34));
-            a2 = ld16(p + 36);
-            a3 = ld16(p + 52);
-        }
-        const uint32_t w[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
-                                a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             int i0 = 0, i1 = 0;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                i0 = dot4(w[i], a.q[t][i], i0);
-                i1 = dot4(w[8 + i], a.q[t][8 + i], i1);
+                i0 = dot4(r.w[i], a.q[t][i], i0);
+                i1 = dot4(r.w[8 + i], a.q[t][8 + i], i1);
             }
-            acc[t] += dw0 * a.d[t][0] * (float)i0 + dw1 * a.d[t][1] * (float)i1;
+            acc[t] += r.d0 * a.d[t][0] * (float)i0 + r.d1 * a.d[t][1] * (float)i1;
         }
     } else if constexpr (F == Q4_K) {
-        const int sb = u >> 2, q = u & 3;
-        const uint8_t *p = rowp + 144 * sb;
-        const u32x4 hdr = ld16(p);
-        const u32x4 qa = ld16(p + 16 + 32 * q), qb = ld16(p + 32 + 32 * q);
-        const float d = h2f(hdr.x & 0xffffu), dmin = h2f(hdr.x >> 16);
-        const uint32_t sw[3] = {hdr.y, hdr.z, hdr.w};
-        int sc0, m0, sc1, m1;
-        q4k_sc_m(sw, 2 * q, sc0, m0);
-        q4k_sc_m(sw, 2 * q + 1, sc1, m1);
-        const uint32_t w[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
-        const float ds0 = d * (float)sc0, ds1 = d * (float)sc1;
-        const float dm0 = dmin * (float)m0, dm1 = dmin * (float)m1;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             int i0 = 0, i1 = 0;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                i0 = dot4(w[i] & 0x0f0f0f0fu, a.q[t][i], i0);
-                i1 = dot4((w[i] >> 4) & 0x0f0f0f0fu, a.q[t][8 + i], i1);
+                i0 = dot4(r.w[i] & 0x0f0f0f0fu, a.q[t][i], i0);
+                i1 = dot4((r.w[i] >> 4) & 0x0f0f0f0fu, a.q[t][8 + i], i1);
             }
-            acc[t] += ds0 * a.d[t][0] * (float)i0 - dm0 * a.s[t][0] + ds1 * a.d[t][1] * (float)i1 - dm1 * a.s[t][1];
+            acc[t] += r.ds0 * a.d[t][0] * (float)i0 - r.dm0 * a.s[t][0] + r.ds1 * a.d[t][1] * (float)i1 -
+                      r.dm1 * a.s[t][1];
         }
     } else {
-        const int sb = u >> 2, h = (u >> 1) & 1, v = u & 1;
-        const uint8_t *p = rowp + 210 * sb;
-        const u32x4 l0 = ld16(p + 64 * h + 32 * v), l1 = ld16(p + 64 * h + 32 * v + 16);
-        const u32x4 g0 = ld16(p + 128 + 32 * h), g1 = ld16(p + 144 + 32 * h);
-        const u32x2 sc8 = ld8(p + 192 + 8 * h);
-        const float d = h2f(ld2(p + 208));
-        const uint32_t ql[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
-        const uint32_t qh[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
-        const int shA = 2 * v, shB = 4 + 2 * v;
-        uint32_t ca[8], cb[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            ca[i] = (ql[i] & 0x0f0f0f0fu) | (((qh[i] >> shA) & 0x03030303u) << 4);
-            cb[i] = ((ql[i] >> 4) & 0x0f0f0f0fu) | (((qh[i] >> shB) & 0x03030303u) << 4);
-        }
-        // sub-block scales inside this h-half: A -> 2v, 2v+1 ; B -> 4+2v, 5+2v
-        const uint32_t sA = v ? (sc8.x >> 16) : sc8.x;
-        const uint32_t sB = v ? (sc8.y >> 16) : sc8.y;
-        const float fa1 = d * (float)(int8_t)(sA & 0xff), fa2 = d * (float)(int8_t)((sA >> 8) & 0xff);
-        const float fb1 = d * (float)(int8_t)(sB & 0xff), fb2 = d * (float)(int8_t)((sB >> 8) & 0xff);
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             int a1 = 0, a2 = 0, b1 = 0, b2 = 0;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                a1 = dot4(ca[i], a.q[t][i], a1);
-                a2 = dot4(ca[4 + i], a.q[t][4 + i], a2);
-                b1 = dot4(cb[i], a.q[t][8 + i], b1);
-                b2 = dot4(cb[4 + i], a.q[t][12 + i], b2);
+                a1 = dot4(r.ca[i], a.q[t][i], a1);
+                a2 = dot4(r.ca[4 + i], a.q[t][4 + i], a2);
+                b1 = dot4(r.cb[i], a.q[t][8 + i], b1);
+                b2 = dot4(r.cb[4 + i], a.q[t][12 + i], b2);
             }
             a1 -= 32 * a.sum[t][0];
             a2 -= 32 * a.sum[t][1];
             b1 -= 32 * a.sum[t][2];
             b2 -= 32 * a.sum[t][3];
-            acc[t] += a.d[t][0] * (fa1 * (float)a1 + fa2 * (float)a2) + a.d[t][1] * (fb1 * (float)b1 + fb2 * (float)b2);
+            acc[t] += a.d[t][0] * (r.fa1 * (float)a1 + r.fa2 * (float)a2) +
+                      a.d[t][1] * (r.fb1 * (float)b1 + r.fb2 * (float)b2);
         }
     }
 }

@@ -1,0 +1,101 @@
+"""Row-sharded MMQ: split a packed GGUF weight matrix by rows over the ranks of a process
+group, run the local MMQ, all-gather the fp16 output shards.
+
+A packed row is a whole number of blocks, so any row boundary is a block boundary and a
+shard is a zero-copy byte range of the packed tensor: rank g owns rows [g*R, g*R + R) with
+R = ceil(M / world) rounded up to `align` (the last shard may be short or empty).  The
+activations are replicated.  Each rank writes its (N, R) output into a padded slab and one
+all_gather_into_tensor (backend "nccl" = RCCL on ROCm; "gloo" in the CPU tests) collects
+(world, N, R); the (N, M) result is that slab viewed with the rank axis moved inside each
+token row -- for N = 1 (decode) a free reshape, otherwise one permute copy.
+
+There is no reference counterpart (the reference is single-GPU); this is the north_star's
+"N partitioned across up to 8 GPUs of one node with RCCL all-gather".
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+
+BLOCK = {"q8_0": (32, 34), "q4_k": (256, 144), "q6_k": (256, 210)}
+
+
+def shard_rows(M: int, world: int, rank: int, align: int = 64):
+    """(row0, rows, R): this rank's first row, its real row count, and the padded shard size."""
+    R = -(-M // world)
+    R = -(-R // align) * align
+    row0 = min(M, rank * R)
+    rows = max(0, min(M, row0 + R) - row0)
+    return row0, rows, R
+
+
+def shard_bytes(fmt: str, A: torch.Tensor, M: int, K: int, world: int, rank: int, align: int = 64):
+    """Byte range of the packed tensor A (flat, M rows) that rank `rank` owns (a view)."""
+    qk, nbytes = BLOCK[fmt]
+    row_bytes = (K // qk) * nbytes
+    row0, rows, _ = shard_rows(M, world, rank, align)
+    return A.view(-1)[row0 * row_bytes:(row0 + rows) * row_bytes]
+
+
+def _default_compute(fmt: str):
+    from kernels._lib import TYPES, mmq
+
+    def run(A_shard, B, rows, N, K, out):
+        return mmq(TYPES[fmt], A_shard, B, rows, N, K, out=out)
+
+    return run
+
+
+class RowShardedMMQ:
+    """y = (A @ B^T)^T with A's rows spread over the group.
+
+    A_shard: this rank's packed rows (from shard_bytes), on this rank's device.
+    compute(A_shard, B, rows, N, K, out) -> writes fp16 (N, rows) into `out`
+    (default: the HIP MMQ through the C ABI).
+    """
+
+    def __init__(self, fmt: str, A_shard: torch.Tensor, M: int, K: int, group=None, align: int = 64,
+                 compute: Optional[Callable] = None):
+        self.fmt, self.M, self.K, self.group = fmt, M, K, group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.row0, self.rows, self.R = shard_rows(M, self.world, self.rank, align)
+        qk, nbytes = BLOCK[fmt]
+        assert A_shard.numel() == self.rows * (K // qk) * nbytes, "A_shard is not this rank's row range"
+        self.A = A_shard
+        self.compute = compute or _default_compute(fmt)
+
+    def local(self, B: torch.Tensor, N: int, slab: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Run the local MMQ into a padded (N, R) slab (pad columns zeroed)."""
+        if slab is None:
+            slab = torch.empty(N, self.R, dtype=torch.float16, device=B.device)
+        if self.rows < self.R:
+            slab[:, self.rows:].zero_()
+        if self.rows > 0 and N > 0:
+            self.compute(self.A, B, self.rows, N, self.K, slab[:, :self.rows])
+        return slab
+
+    def gather(self, slab: torch.Tensor, out: Optional[torch.Tensor] = None, async_op: bool = False):
+        """all_gather the (N, R) slabs into (world, N, R); returns (tensor, work)."""
+        N = slab.shape[0]
+        if out is None:
+            out = torch.empty(self.world, N, self.R, dtype=slab.dtype, device=slab.device)
+        if self.world == 1:
+            out[0].copy_(slab)
+            return out, None
+        work = dist.all_gather_into_tensor(out, slab, group=self.group, async_op=async_op)
+        return out, work
+
+    def assemble(self, gathered: torch.Tensor) -> torch.Tensor:
+        """(world, N, R) -> (N, M)."""
+        W, N, R = gathered.shape
+        if N == 1:
+            return gathered.view(1, W * R)[:, :self.M]
+        return gathered.permute(1, 0, 2).reshape(N, W * R)[:, :self.M]
+
+    def __call__(self, B: torch.Tensor, N: int) -> torch.Tensor:
+        slab = self.local(B, N)
+        gathered, _ = self.gather(slab)
+        return self.assemble(gathered)

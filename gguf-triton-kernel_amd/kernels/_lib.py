@@ -28,7 +28,7 @@ SIGNATURES = {
     "gq_mmq_workspace_size": ([_I, _I64, _I64, _I64], _SZ),
     "gq_mmq": ([_I, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P], _I),
     "gq_act_prepare": ([_P, _I64, _I64, _I64, _P, _SZ, _P], _I),
-    "gq_mmq_prepared": ([_I, _P, _P, _P, _I64, _I64, _I64, _I64, _P], _I),
+    "gq_mmq_prepared": ([_I, _P, _P, _SZ, _P, _I64, _I64, _I64, _I64, _P], _I),
     "gq_quantize_q8_1": ([_P, _P, _I64, _I64, _I64, _P], _I),
     "gq_last_error": ([], ctypes.c_char_p),
     "gq_version": ([], _I),

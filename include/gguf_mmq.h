@@ -55,15 +55,17 @@ int gq_mmq(gq_type t, const void *A, const void *B, void *C, int64_t M, int64_t 
            int64_t ldc, void *workspace, size_t workspace_bytes, void *stream);
 
 /*
- * Split form of gq_mmq.  gq_act_prepare quantizes B into `workspace` (layout depends only
- * on N and K); gq_mmq_prepared then runs the matmul for any weight type/M with that K.
- * One prepare can serve several weight matrices that share an input (Q/K/V, gate/up).
+ * Split form of gq_mmq.  gq_act_prepare quantizes B into the front of `workspace` (that
+ * part depends only on N and K); gq_mmq_prepared then runs the matmul for any weight
+ * type and M with that K, using the rest of the workspace (which must be at least
+ * gq_mmq_workspace_size(t, M, N, K) bytes in total) for split-K partial sums.  One prepare
+ * can serve several weight matrices that share an input (Q/K/V, gate/up).
  * gq_mmq(...) == gq_act_prepare(...) followed by gq_mmq_prepared(...).
  */
 int gq_act_prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *workspace, size_t workspace_bytes,
                    void *stream);
-int gq_mmq_prepared(gq_type t, const void *A, const void *workspace, void *C, int64_t M, int64_t N, int64_t K,
-                    int64_t ldc, void *stream);
+int gq_mmq_prepared(gq_type t, const void *A, void *workspace, size_t workspace_bytes, void *C, int64_t M, int64_t N,
+                    int64_t K, int64_t ldc, void *stream);
 
 /*
  * q8_1 quantization of fp16 rows on the device, byte-identical to utils/quantize/q8_1.py:

@@ -100,7 +100,9 @@ def test_golden_cases(golden, fmt):
         assert err <= tight(N), (fmt, c["i"], c["kind"], M, N, K, err)
         if not (fmt == "q8_0" and c["kind"] == "tiny"):
             assert O.allclose(c["C"], got, 0.01), (fmt, c["i"], c["kind"], O.max_rel_err(got, c["C"]))
-        if "Ctri" in c:  # and the reference's own GPU kernel's gate
+        # the reference's own GPU kernel vs this build, except the one case where that kernel
+        # misses its own gate vs cpu_impls (Q8_0 1x1x32, tests/test_oracle_golden.py)
+        if "Ctri" in c and not (fmt == "q8_0" and (M, N, K) == (1, 1, 32)):
             assert O.allclose(c["Ctri"], got, 0.01), (fmt, c["i"])
 
 
