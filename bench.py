@@ -265,7 +265,8 @@ def bench_dist(r, steps, dev, world):
         works = []
         for i in range(n):
             gstep[i & 1].replay()
-            works.append(dist.all_gather_into_tensor(gathered[i & 1], r.C[i & 1], async_op=True))
+            works.append(dist.all_gather_into_tensor(gathered[i & 1].view(world * r.N, r.M), r.C[i & 1],
+                                                     async_op=True))
             if len(works) > 1:
                 works.pop(0).wait()
         for w in works:

@@ -26,6 +26,8 @@
 //     so any consistent permutation is exact).
 // MFMA 32x32x16 f16 operand maps (gfx950): lane l holds A[row l&31][k 8(l>>5)+j] and
 // B[k 8(l>>5)+j][col l&31]; D[row (i&3)+8(i>>2)+4(l>>5)][col l&31] in acc element i.
+#include <cstdlib>
+
 #include "gguf_blocks.hpp"
 #include "gguf_internal.hpp"
 #include "gguf_units.hpp"
@@ -203,46 +205,25 @@ __global__ __launch_bounds__(256) void gemm_kernel(const uint8_t *__restrict__ A
                 }
             } else {
                 float *pp = P + ((int64_t)blockIdx.z * N + tok) * M + rr;
-                if (rr + 3 < M) {
-                    u32x4 o = {__builtin_bit_cast(uint32_t, v0), __builtin_bit_cast(uint32_t, v1),
-                               __builtin_bit_cast(uint32_t, v2), __builtin_bit_cast(uint32_t, v3)};
-                    __builtin_memcpy(pp, &o, 16);
-                } else {
-                    const float vv[4] = {v0, v1, v2, v3};
-                    for (int e = 0; e < 4; ++e)
-                        if (rr + e < M) pp[e] = vv[e];
-                }
+                const float vv[4] = {v0, v1, v2, v3};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (rr + e < M) pp[e] = vv[e];
             }
         }
     }
 }
 
-// C[t][m] = fp16(sum_s P[s][t][m]), summed in split order.
+// C[t][m] = fp16(sum_s P[s][t][m]), summed in split order (deterministic).
 __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restrict__ P, uint16_t *__restrict__ C,
                                                           int64_t M, int64_t N, int64_t ldc, int S)
 {
-    const int64_t m4 = (M + 3) / 4;
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (idx >= N * m4) return;
-    const int64_t tok = idx / m4, m = 4 * (idx - tok * m4);
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    if (m + 3 < M && (M & 3) == 0) {
-        for (int s = 0; s < S; ++s) {
-            u32x4 v = ld16(P + ((int64_t)s * N + tok) * M + m);
-            s0 += __builtin_bit_cast(float, v.x);
-            s1 += __builtin_bit_cast(float, v.y);
-            s2 += __builtin_bit_cast(float, v.z);
-            s3 += __builtin_bit_cast(float, v.w);
-        }
-        u32x2 o = {pk_f16(s0, s1), pk_f16(s2, s3)};
-        __builtin_memcpy(C + tok * ldc + m, &o, 8);
-    } else {
-        for (int e = 0; e < 4 && m + e < M; ++e) {
-            float acc = 0.f;
-            for (int s = 0; s < S; ++s) acc += P[((int64_t)s * N + tok) * M + m + e];
-            C[tok * ldc + m + e] = f2h_bits(acc);
-        }
-    }
+    if (idx >= N * M) return;
+    const int64_t tok = idx / M, m = idx - tok * M;
+    float acc = 0.f;
+    for (int s = 0; s < S; ++s) acc += P[((int64_t)s * N + tok) * M + m];
+    C[tok * ldc + m] = f2h_bits(acc);
 }
 
 template <int F, int NT>
@@ -253,7 +234,7 @@ hipError_t launch_nt(const uint8_t *A, const uint16_t *X, uint16_t *C, float *P,
     gemm_kernel<F, NT><<<grid, block, 0, s>>>(A, X, C, S > 1 ? P : nullptr, M, N, K, ldc, cps);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || S == 1) return e;
-    const int64_t work = N * ((M + 3) / 4);
+    const int64_t work = N * M;
     gemm_reduce_kernel<<<dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s>>>(P, C, M, N, ldc, S);
     return hipGetLastError();
 }
@@ -281,6 +262,7 @@ GemmPlan plan_gemm(int64_t M, int64_t N, int64_t K)
     const int64_t nchunks = (K + KC - 1) / KC;
     const int64_t target = 256; // one workgroup per CU
     int64_t S = tiles >= target ? 1 : (target + tiles / 2) / tiles;
+    if (const char *env = getenv("GQ_GEMM_SPLITS")) S = atoll(env); // tuning / test override
     const int64_t max_split = nchunks / 4 > 0 ? nchunks / 4 : 1; // >= 4 chunks per split
     if (S > max_split) S = max_split;
     if (S < 1) S = 1;

@@ -85,7 +85,9 @@ class RowShardedMMQ:
         if self.world == 1:
             out[0].copy_(slab)
             return out, None
-        work = dist.all_gather_into_tensor(out, slab, group=self.group, async_op=async_op)
+        # concatenated (world*N, R) form: accepted by both RCCL and gloo
+        work = dist.all_gather_into_tensor(out.view(self.world * N, self.R), slab, group=self.group,
+                                           async_op=async_op)
         return out, work
 
     def assemble(self, gathered: torch.Tensor) -> torch.Tensor:

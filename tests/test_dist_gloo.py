@@ -57,10 +57,14 @@ def test_row_sharded_matches_single(fmt, M, N, K, align):
         ps = [ctx.Process(target=_worker, args=(r, world, initfile, fmt, M, N, K, align, q)) for r in range(world)]
         for p in ps:
             p.start()
-        got = q.get(timeout=120)
         for p in ps:
-            p.join(timeout=60)
-            assert p.exitcode == 0
+            p.join(timeout=120)
+        codes = [p.exitcode for p in ps]
+        for p in ps:
+            if p.is_alive():
+                p.kill()
+        assert codes == [0] * world, codes
+        got = q.get(timeout=10)
     A = random_blocks(fmt, M, K, seed=9)
     B = random_activations(N, K, seed=4)
     want = O.mmq_from_fp16(fmt, A, B, M, N, K, O.IDEAL)

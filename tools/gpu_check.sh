@@ -22,7 +22,7 @@ cat "$OUT/bench.json"
 if [ "${PROFILE:-1}" = "1" ]; then
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
-      python3 "$ROOT/bench.py" --steps 50 --warmup 5 --no-cpu ${PROF_ARGS:-} > "$OUT/prof_bench.json" 2> "$OUT/prof.err" || { echo "rocprof failed"; tail -20 "$OUT/prof.err"; exit 5; }
+      python3 "$ROOT/bench.py" --steps 30 --warmup 5 --no-cpu ${PROF_ARGS:---sweep} > "$OUT/prof_bench.json" 2> "$OUT/prof.err" || { echo "rocprof failed"; tail -20 "$OUT/prof.err"; exit 5; }
   find "$OUT/prof" -name "*stats*" | head
 fi
 echo ALL_DONE
