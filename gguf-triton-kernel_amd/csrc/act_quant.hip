@@ -7,16 +7,16 @@
 // x*127/amax, no fp16 rounding); this build keeps the oracle's exact q8_1 semantics so the
 // GPU path and kernels/cpu_impls see identical integer activations.
 //
-// Eight lanes own one 32-element block (4 fp16 each); amax and sum(q) are reduced with
-// 3-step xor shuffles inside the 8-lane group.  fp32 division is IEEE correctly rounded
-// (hipcc default), so fp16(x/d) matches torch's CPU fp16 division.
+// Eight lanes own one 32-element block (4 fp16 each): gguf_q8_1.hpp.
 //
 // Output forms (one kernel template, chosen by the caller):
 //   AOS  : the q8_1 byte layout itself (36 B per block) -- gq_quantize_q8_1 / tests
 //   SOA  : codes int8 [rows][K] + d float [rows][K/32] + s float [rows][K/32] -- GEMV input
-//   DEQ  : x~ = fp16(d * q) [rows][K] -- the dequantized activation fed to the fp16 MFMA GEMM
+//   DEQ  : x~ = fp16(d * q) [rows][K] -- the dequantized activation fed to the fp16 MFMA GEMM,
+//          each 4-element group stored in the order (0,2,1,3) (see mmq_gemm.hip)
 #include "gguf_blocks.hpp"
 #include "gguf_internal.hpp"
+#include "gguf_q8_1.hpp"
 
 namespace gq {
 
@@ -39,49 +39,31 @@ __global__ __launch_bounds__(256) void act_quant_kernel(const uint16_t *__restri
         w0 = v.x;
         w1 = v.y;
     }
-    float x[4] = {h2f(w0 & 0xffff), h2f(w0 >> 16), h2f(w1 & 0xffff), h2f(w1 >> 16)};
-    float amax = fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3])));
-    amax = fmaxf(amax, __shfl_xor(amax, 1, 8));
-    amax = fmaxf(amax, __shfl_xor(amax, 2, 8));
-    amax = fmaxf(amax, __shfl_xor(amax, 4, 8));
-
-    const uint16_t dbits = amax != 0.f ? f2h_bits(amax / 127.0f) : (uint16_t)0;
-    const float d = h2f(dbits);
-    const float div = d == 0.f ? 1.0f : d;
-    int q[4];
-    int sum = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        float r = __builtin_rintf(h2f(f2h_bits(x[i] / div)));
-        r = fminf(127.f, fmaxf(-127.f, r));
-        q[i] = (int)r;
-        sum += q[i];
-    }
-    sum += __shfl_xor(sum, 1, 8);
-    sum += __shfl_xor(sum, 2, 8);
-    sum += __shfl_xor(sum, 4, 8);
-    const uint16_t sbits = f2h_bits(d * h2f(f2h_bits((float)sum)));
+    const Q81Lane q = q8_1_lane(w0, w1);
     if (!live) return;
 
-    const uint32_t packed = (uint32_t)(q[0] & 0xff) | ((uint32_t)(q[1] & 0xff) << 8) |
-                            ((uint32_t)(q[2] & 0xff) << 16) | ((uint32_t)(q[3] & 0xff) << 24);
     if constexpr (MODE == ACT_AOS) {
         uint8_t *o = out + blk * 36;
-        __builtin_memcpy(o + 4 + 4 * sub, &packed, 4);
+        __builtin_memcpy(o + 4 + 4 * sub, &q.codes, 4);
         if (sub == 0) {
-            uint32_t ds = (uint32_t)dbits | ((uint32_t)sbits << 16);
+            uint32_t ds = (uint32_t)q.dbits | ((uint32_t)q.sbits << 16);
             __builtin_memcpy(o, &ds, 4);
         }
     } else if constexpr (MODE == ACT_SOA) {
-        *(uint32_t *)(codes + row * K + 32 * j + 4 * sub) = packed;
+        *(uint32_t *)(codes + row * K + 32 * j + 4 * sub) = q.codes;
         if (sub == 0) {
-            dout[row * nb + j] = d;
-            sout[row * nb + j] = h2f(sbits);
+            dout[row * nb + j] = q.d;
+            sout[row * nb + j] = h2f(q.sbits);
         }
     } else {
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = q.d * (float)(int8_t)((q.codes >> (8 * i)) & 0xff);
+        // element order (0,2,1,3) inside each 4-group: the order mmq_gemm.hip's packed
+        // dequantization produces weight pairs in (its k-permutation; the MFMA k-sum is unchanged)
         u32x2 o;
-        o.x = (uint32_t)f2h_bits(d * (float)q[0]) | ((uint32_t)f2h_bits(d * (float)q[1]) << 16);
-        o.y = (uint32_t)f2h_bits(d * (float)q[2]) | ((uint32_t)f2h_bits(d * (float)q[3]) << 16);
+        o.x = (uint32_t)f2h_bits(v[0]) | ((uint32_t)f2h_bits(v[2]) << 16);
+        o.y = (uint32_t)f2h_bits(v[1]) | ((uint32_t)f2h_bits(v[3]) << 16);
         *(u32x2 *)(xdeq + row * K + 32 * j + 4 * sub) = o;
     }
 }

@@ -2,6 +2,7 @@
 // path selection (decode GEMV vs MFMA GEMM) and launches.  Stateless and re-entrant.
 #include <cstdio>
 #include <cstdarg>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/gguf_mmq.h"
@@ -143,6 +144,14 @@ int gq_mmq(gq_type t, const void *A, const void *B, void *C, int64_t M, int64_t 
     if (!workspace || workspace_bytes < ws_bytes(M, N, K))
         return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace ? workspace_bytes : (size_t)0,
                     ws_bytes(M, N, K));
+    if (ldb < K) return fail(GQ_EINVAL, "ldb=%lld < K=%lld", (long long)ldb, (long long)K);
+    if (use_gemv(N) && gq::decode_fused_ok(t, N, K) && !getenv("GQ_NO_FUSED_DECODE")) {
+        // one launch: activation quantization in LDS + decode GEMV
+        hipError_t e = gq::launch_decode_fused(t, (const uint8_t *)A, (const uint16_t *)B, ldb, (uint16_t *)C, M, N,
+                                               K, ldc, (hipStream_t)stream);
+        if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (decode): %s", hipGetErrorString(e));
+        return GQ_OK;
+    }
     rc = prepare(B, N, K, ldb, workspace, workspace_bytes, (hipStream_t)stream);
     if (rc != GQ_OK) return rc;
     return compute(t, A, workspace, workspace_bytes, C, M, N, K, ldc, (hipStream_t)stream);

@@ -49,10 +49,30 @@ __device__ __forceinline__ uint32_t pk_f16(float a, float b)
     return (uint32_t)f2h_bits(a) | ((uint32_t)f2h_bits(b) << 16);
 }
 
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ h2 as_h2(uint32_t v) { return __builtin_bit_cast(h2, v); }
+__device__ __forceinline__ uint32_t as_u32(h2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ h2 splat(float f) { return (h2){(_Float16)f, (_Float16)f}; }
+
 __device__ __forceinline__ f16x8 as_f16x8(uint32_t a, uint32_t b, uint32_t c, uint32_t d)
 {
     u32x4 v = {a, b, c, d};
     return __builtin_bit_cast(f16x8, v);
+}
+
+// Packed dequantization.  A fragment holds 8 weights of consecutive k in the element order
+// (0,2,1,3,4,6,5,7): the pair (byte 0, byte 2) and the pair (byte 1, byte 3) of a code
+// dword become one f16x2 each with a single AND-OR / PERM against the exponent pattern
+// 0x64 (f16 1024 + v), the bias comes off with one packed add and the scale goes on with one
+// packed mul/fma.  act_quant's DEQ form stores x~ in the same element order, so the MFMA's
+// k-sum is unchanged.  Rounding: the integer codes are exact in f16; the per-block scales
+// are rounded to f16 once (2^-11 relative), then one rounding per product.
+__device__ __forceinline__ void bytes_pairs(uint32_t w, uint32_t &p02, uint32_t &p13)
+{
+    // w holds 4 unsigned byte codes; -> f16 (1024+code) pairs (c0,c2) and (c1,c3)
+    p02 = __builtin_amdgcn_perm(0x64646464u, w, 0x04020400u);
+    p13 = __builtin_amdgcn_perm(0x64646464u, w, 0x04030401u);
 }
 
 // fp16 fragment for k-step t (0..7) of a unit: 8 weights.
@@ -62,30 +82,42 @@ __device__ __forceinline__ f16x8 unit_frag(const UnitRaw<F> &r, int t);
 template <>
 __device__ __forceinline__ f16x8 unit_frag<Q8_0>(const UnitRaw<Q8_0> &r, int t)
 {
-    const float d = t < 4 ? r.d0 : r.d1;
-    const uint32_t w0 = r.w[2 * t], w1 = r.w[2 * t + 1];
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        v[j] = d * (float)(int8_t)((w0 >> (8 * j)) & 0xff);
-        v[4 + j] = d * (float)(int8_t)((w1 >> (8 * j)) & 0xff);
-    }
-    return as_f16x8(pk_f16(v[0], v[1]), pk_f16(v[2], v[3]), pk_f16(v[4], v[5]), pk_f16(v[6], v[7]));
+    const h2 d = splat(t < 4 ? r.d0 : r.d1);
+    const h2 bias = splat(-1152.f); // codes were biased by +128 (xor 0x80)
+    uint32_t a0, a1, b0, b1;
+    bytes_pairs(r.w[2 * t] ^ 0x80808080u, a0, a1);
+    bytes_pairs(r.w[2 * t + 1] ^ 0x80808080u, b0, b1);
+    return as_f16x8(as_u32((as_h2(a0) + bias) * d), as_u32((as_h2(a1) + bias) * d),
+                    as_u32((as_h2(b0) + bias) * d), as_u32((as_h2(b1) + bias) * d));
 }
 
 template <>
 __device__ __forceinline__ f16x8 unit_frag<Q4_K>(const UnitRaw<Q4_K> &r, int t)
 {
-    const int tt = t & 3, sh = t < 4 ? 0 : 4;
-    const float ds = t < 4 ? r.ds0 : r.ds1, dm = t < 4 ? r.dm0 : r.dm1;
-    const uint32_t w0 = r.w[2 * tt] >> sh, w1 = r.w[2 * tt + 1] >> sh;
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        v[j] = ds * (float)((w0 >> (8 * j)) & 0xf) - dm;
-        v[4 + j] = ds * (float)((w1 >> (8 * j)) & 0xf) - dm;
+    const int tt = t & 3;
+    const uint32_t w0 = r.w[2 * tt], w1 = r.w[2 * tt + 1];
+    const h2 bias = splat(-1024.f);
+    uint32_t a0, a1, b0, b1;
+    h2 ds, ndm;
+    if (t < 4) { // low nibbles: code at bits 0 / 16 of (w) and of (w >> 8)
+        ds = splat(r.ds0);
+        ndm = splat(-r.dm0);
+        a0 = (w0 & 0x000f000fu) | 0x64006400u;
+        a1 = ((w0 >> 8) & 0x000f000fu) | 0x64006400u;
+        b0 = (w1 & 0x000f000fu) | 0x64006400u;
+        b1 = ((w1 >> 8) & 0x000f000fu) | 0x64006400u;
+    } else { // high nibbles: take them at bits 4 / 20, i.e. 16 * code; fold the 1/16 into ds
+        ds = splat(r.ds1 * 0.0625f);
+        ndm = splat(-r.dm1);
+        a0 = (w0 & 0x00f000f0u) | 0x64006400u;
+        a1 = ((w0 >> 8) & 0x00f000f0u) | 0x64006400u;
+        b0 = (w1 & 0x00f000f0u) | 0x64006400u;
+        b1 = ((w1 >> 8) & 0x00f000f0u) | 0x64006400u;
     }
-    return as_f16x8(pk_f16(v[0], v[1]), pk_f16(v[2], v[3]), pk_f16(v[4], v[5]), pk_f16(v[6], v[7]));
+    return as_f16x8(as_u32(__builtin_elementwise_fma(as_h2(a0) + bias, ds, ndm)),
+                    as_u32(__builtin_elementwise_fma(as_h2(a1) + bias, ds, ndm)),
+                    as_u32(__builtin_elementwise_fma(as_h2(b0) + bias, ds, ndm)),
+                    as_u32(__builtin_elementwise_fma(as_h2(b1) + bias, ds, ndm)));
 }
 
 template <>
@@ -93,15 +125,13 @@ __device__ __forceinline__ f16x8 unit_frag<Q6_K>(const UnitRaw<Q6_K> &r, int t)
 {
     const int tt = t & 3;
     const uint32_t *c = t < 4 ? r.ca : r.cb;
-    const float s = t < 4 ? (tt < 2 ? r.fa1 : r.fa2) : (tt < 2 ? r.fb1 : r.fb2);
+    const h2 sc = splat(t < 4 ? (tt < 2 ? r.fa1 : r.fa2) : (tt < 2 ? r.fb1 : r.fb2));
+    const h2 bias = splat(-1056.f); // 1024 + 32
     const uint32_t w0 = c[2 * tt], w1 = c[2 * tt + 1];
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        v[j] = s * (float)((int)((w0 >> (8 * j)) & 0xff) - 32);
-        v[4 + j] = s * (float)((int)((w1 >> (8 * j)) & 0xff) - 32);
-    }
-    return as_f16x8(pk_f16(v[0], v[1]), pk_f16(v[2], v[3]), pk_f16(v[4], v[5]), pk_f16(v[6], v[7]));
+    const uint32_t a0 = (w0 & 0x003f003fu) | 0x64006400u, a1 = ((w0 >> 8) & 0x003f003fu) | 0x64006400u;
+    const uint32_t b0 = (w1 & 0x003f003fu) | 0x64006400u, b1 = ((w1 >> 8) & 0x003f003fu) | 0x64006400u;
+    return as_f16x8(as_u32((as_h2(a0) + bias) * sc), as_u32((as_h2(a1) + bias) * sc),
+                    as_u32((as_h2(b0) + bias) * sc), as_u32((as_h2(b1) + bias) * sc));
 }
 
 // Which 8-element piece (0..15) of the 128-wide chunk k-step t of half h multiplies.
@@ -112,14 +142,15 @@ __device__ __forceinline__ int piece_of(int h, int t)
     return 8 * h + t;
 }
 
-// Issue the LDS-DMA for chunk c of the activation tile into `buf` (tokens n0.., 32*NT rows).
-template <int NT>
+// Issue the LDS-DMA for chunk c of the activation tile into `buf` (tokens n0.., 32*NT rows),
+// spread over the workgroup's NW waves.
+template <int NT, int NW>
 __device__ __forceinline__ void stage_b(uint8_t *buf, const uint16_t *__restrict__ X, int64_t n0, int64_t N,
                                         int64_t K, int64_t c, int wave, int lane)
 {
     constexpr int INSTR = 8 * NT; // 1 KiB (4 token rows) per wave-instruction
 #pragma unroll
-    for (int q = wave; q < INSTR; q += 4) {
+    for (int q = wave; q < INSTR; q += NW) {
         const int row = 4 * q + (lane >> 4);
         const int piece = (lane & 15) ^ (row & 15);
         int64_t tok = n0 + row;
@@ -130,15 +161,22 @@ __device__ __forceinline__ void stage_b(uint8_t *buf, const uint16_t *__restrict
     }
 }
 
-template <int F, int NT>
-__global__ __launch_bounds__(256) void gemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
-                                                   uint16_t *__restrict__ C, float *__restrict__ P, int64_t M,
-                                                   int64_t N, int64_t K, int64_t ldc, int chunks_per_split)
+// Workgroup = 4*WN waves: wave w owns weight rows 32*(w&3).. of the 128-row tile and token
+// tiles [ (w>>2)*NTW, (w>>2+1)*NTW ) of the NT 32-token tiles (NTW = NT/WN).  WN = 2 puts two
+// waves on every SIMD (latency hiding, VALU of one beside MFMA of the other); both waves of
+// a row group load the same weight unit (the second read hits L2).
+template <int F, int NT, int WN>
+__global__ __launch_bounds__(256 * WN) void gemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
+                                                        uint16_t *__restrict__ C, float *__restrict__ P, int64_t M,
+                                                        int64_t N, int64_t K, int64_t ldc, int chunks_per_split)
 {
     using L = Layout<F>;
+    constexpr int NTW = NT / WN;
+    constexpr int NW = 4 * WN;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[2 * 32 * NT * ROW_B];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave & 3, wn = wave >> 2;
     const int h = lane >> 5, r32 = lane & 31;
     const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * 32 * NT;
     const int64_t nchunks = (K + KC - 1) / KC;
@@ -147,18 +185,18 @@ __global__ __launch_bounds__(256) void gemm_kernel(const uint8_t *__restrict__ A
     const int64_t row_bytes = (K / L::QK) * L::BYTES;
     const int64_t nb32 = K / 32;
 
-    int64_t row = m0 + 32 * wave + r32;
+    const int64_t row = m0 + 32 * wm + r32;
     const uint8_t *rowp = A + (row < M ? row : M - 1) * row_bytes;
 
-    f32x16 acc[NT];
+    f32x16 acc[NTW];
 #pragma unroll
-    for (int i = 0; i < NT; ++i)
+    for (int i = 0; i < NTW; ++i)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
 
     UnitRaw<F> nxt;
     if (c0 < c1) {
-        stage_b<NT>(lds, X, n0, N, K, c0, wave, lane);
+        stage_b<NT, NW>(lds, X, n0, N, K, c0, wave, lane);
         nxt.load(rowp, (int)(2 * c0 + h), nb32);
     }
     __syncthreads();
@@ -167,7 +205,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const uint8_t *__restrict__ A
         const UnitRaw<F> cur = nxt;
         uint8_t *buf = lds + ((c - c0) & 1) * (32 * NT * ROW_B);
         if (c + 1 < c1) {
-            stage_b<NT>(lds + ((c + 1 - c0) & 1) * (32 * NT * ROW_B), X, n0, N, K, c + 1, wave, lane);
+            stage_b<NT, NW>(lds + ((c + 1 - c0) & 1) * (32 * NT * ROW_B), X, n0, N, K, c + 1, wave, lane);
             nxt.load(rowp, (int)(2 * (c + 1) + h), nb32);
         }
 #pragma unroll
@@ -175,37 +213,35 @@ __global__ __launch_bounds__(256) void gemm_kernel(const uint8_t *__restrict__ A
             const f16x8 a = unit_frag<F>(cur, t);
             const int piece = piece_of<F>(h, t);
 #pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-                const int trow = 32 * nt + r32;
+            for (int i = 0; i < NTW; ++i) {
+                const int trow = 32 * (wn * NTW + i) + r32;
                 const f16x8 b = *(const f16x8 *)(buf + trow * ROW_B + 16 * (piece ^ (trow & 15)));
-                acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc[nt], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc[i], 0, 0, 0);
             }
         }
         __syncthreads();
     }
 
-    // epilogue: acc[nt][i] = D[row 32w + (i&3) + 8(i>>2) + 4h][token 32nt + r32]
+    // epilogue: acc[i][e] = D[row 32wm + (e&3) + 8(e>>2) + 4h][token 32(wn*NTW+i) + r32]
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        const int64_t tok = n0 + 32 * nt + r32;
+    for (int i = 0; i < NTW; ++i) {
+        const int64_t tok = n0 + 32 * (wn * NTW + i) + r32;
         if (tok >= N) continue;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-            const int64_t rr = m0 + 32 * wave + 8 * g + 4 * h;
-            const float v0 = acc[nt][4 * g], v1 = acc[nt][4 * g + 1], v2 = acc[nt][4 * g + 2], v3 = acc[nt][4 * g + 3];
+            const int64_t rr = m0 + 32 * wm + 8 * g + 4 * h;
+            const float vv[4] = {acc[i][4 * g], acc[i][4 * g + 1], acc[i][4 * g + 2], acc[i][4 * g + 3]};
             if (P == nullptr) {
                 uint16_t *cp = C + tok * ldc + rr;
                 if (rr + 3 < M) {
-                    u32x2 o = {pk_f16(v0, v1), pk_f16(v2, v3)};
+                    u32x2 o = {pk_f16(vv[0], vv[1]), pk_f16(vv[2], vv[3])};
                     __builtin_memcpy(cp, &o, 8);
                 } else {
-                    const float vv[4] = {v0, v1, v2, v3};
                     for (int e = 0; e < 4; ++e)
                         if (rr + e < M) cp[e] = f2h_bits(vv[e]);
                 }
             } else {
                 float *pp = P + ((int64_t)blockIdx.z * N + tok) * M + rr;
-                const float vv[4] = {v0, v1, v2, v3};
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
                     if (rr + e < M) pp[e] = vv[e];
@@ -226,12 +262,13 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restric
     C[tok * ldc + m] = f2h_bits(acc);
 }
 
-template <int F, int NT>
+template <int F, int NT, int WN>
 hipError_t launch_nt(const uint8_t *A, const uint16_t *X, uint16_t *C, float *P, int S, int cps, int64_t M, int64_t N,
                      int64_t K, int64_t ldc, hipStream_t s)
 {
-    dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((N + 32 * NT - 1) / (32 * NT)), (unsigned)S), block(256);
-    gemm_kernel<F, NT><<<grid, block, 0, s>>>(A, X, C, S > 1 ? P : nullptr, M, N, K, ldc, cps);
+    dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((N + 32 * NT - 1) / (32 * NT)), (unsigned)S),
+        block(256 * WN);
+    gemm_kernel<F, NT, WN><<<grid, block, 0, s>>>(A, X, C, S > 1 ? P : nullptr, M, N, K, ldc, cps);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || S == 1) return e;
     const int64_t work = N * M;
@@ -245,10 +282,10 @@ hipError_t launch_fmt(const uint8_t *A, const uint16_t *X, uint16_t *C, float *P
 {
     const int nt = N >= 97 ? 4 : (N >= 65 ? 3 : (N >= 33 ? 2 : 1));
     switch (nt) {
-    case 1: return launch_nt<F, 1>(A, X, C, P, S, cps, M, N, K, ldc, s);
-    case 2: return launch_nt<F, 2>(A, X, C, P, S, cps, M, N, K, ldc, s);
-    case 3: return launch_nt<F, 3>(A, X, C, P, S, cps, M, N, K, ldc, s);
-    default: return launch_nt<F, 4>(A, X, C, P, S, cps, M, N, K, ldc, s);
+    case 1: return launch_nt<F, 1, 1>(A, X, C, P, S, cps, M, N, K, ldc, s);
+    case 2: return launch_nt<F, 2, 2>(A, X, C, P, S, cps, M, N, K, ldc, s);
+    case 3: return launch_nt<F, 3, 1>(A, X, C, P, S, cps, M, N, K, ldc, s);
+    default: return launch_nt<F, 4, 2>(A, X, C, P, S, cps, M, N, K, ldc, s);
     }
 }
 

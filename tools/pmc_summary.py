@@ -13,7 +13,7 @@ for f in glob.glob(os.path.join(root, "*", "p*", "**", "*counter_collection.csv"
         k = r.get("Kernel_Name", r.get("Kernel-Name", "?"))
         if "gq::" not in k:
             continue
-        short = k.split("(")[0].replace("void ", "").replace("gq::(anonymous namespace)::", "")
+        short = k.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0].replace("gq::", "")
         res[(cfg, short)][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for (cfg, k), ctrs in sorted(res.items()):
     print(f"{cfg:24s} {k}")
