@@ -38,7 +38,6 @@ namespace {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int KC = 128;         // K elements per chunk
 constexpr int ROW_B = KC * 2;   // LDS bytes per token row of a chunk
@@ -142,75 +141,78 @@ __device__ __forceinline__ int piece_of(int h, int t)
     return 8 * h + t;
 }
 
-// Issue the LDS-DMA for chunk c of the activation tile into `buf` (tokens n0.., 32*NT rows),
-// spread over the workgroup's NW waves.
-template <int NT, int NW>
-__device__ __forceinline__ void stage_b(uint8_t *buf, const uint16_t *__restrict__ X, int64_t n0, int64_t N,
-                                        int64_t K, int64_t c, int wave, int lane)
+// One pipeline stage in registers: this lane's weight unit for a chunk and its share of the
+// chunk's activation tile (BP 16-byte pieces).
+template <int F, int BP>
+struct Stage {
+    UnitRaw<F> a;
+    u32x4 b[BP];
+};
+
+// Activation tile piece p of chunk c (p = tid + i*NTHR): token row p>>4, 16-byte column p&15.
+template <int NT, int NTHR, int BP>
+__device__ __forceinline__ void load_b(u32x4 (&b)[BP], const uint16_t *__restrict__ X, int64_t n0, int64_t N,
+                                       int64_t K, int64_t c, int tid)
 {
-    constexpr int INSTR = 8 * NT; // 1 KiB (4 token rows) per wave-instruction
 #pragma unroll
-    for (int q = wave; q < INSTR; q += NW) {
-        const int row = 4 * q + (lane >> 4);
-        const int piece = (lane & 15) ^ (row & 15);
+    for (int i = 0; i < BP; ++i) {
+        const int p = tid + i * NTHR;
+        const int row = p >> 4, col = p & 15;
         int64_t tok = n0 + row;
         tok = tok < N ? tok : N - 1;
-        int64_t k = c * KC + 8 * piece;
+        int64_t k = c * KC + 8 * col;
         k = k < K - 8 ? k : K - 8;
-        __builtin_amdgcn_global_load_lds((const void *)(X + tok * K + k), (lds_void *)(buf + q * 1024), 16, 0, 0);
+        b[i] = ld16(X + tok * K + k);
+    }
+}
+
+// ... and its store into the LDS image: rows of 256 B, 16-byte pieces XOR-swizzled by row&15
+// (the read side applies the same XOR), so each 16-lane ds_read_b128 group of the MFMA's B
+// fragment reads 16 distinct bank quads.
+template <int NTHR, int BP>
+__device__ __forceinline__ void store_b(uint8_t *buf, const u32x4 (&b)[BP], int tid)
+{
+#pragma unroll
+    for (int i = 0; i < BP; ++i) {
+        const int p = tid + i * NTHR;
+        const int row = p >> 4, col = p & 15;
+        *(u32x4 *)(buf + row * ROW_B + 16 * (col ^ (row & 15))) = b[i];
     }
 }
 
 // Workgroup = 4*WN waves: wave w owns weight rows 32*(w&3).. of the 128-row tile and token
-// tiles [ (w>>2)*NTW, (w>>2+1)*NTW ) of the NT 32-token tiles (NTW = NT/WN).  WN = 2 puts two
-// waves on every SIMD (latency hiding, VALU of one beside MFMA of the other); both waves of
-// a row group load the same weight unit (the second read hits L2).
+// tiles [(w>>2)*NTW, (w>>2)*NTW + NTW) of the NT 32-token tiles (NTW = NT/WN).
+//
+// K pipeline, three register stages deep (all loads ordinary global loads, so the compiler
+// counts them with partial vmcnt waits; no LDS-DMA, whose in-flight state would force
+// vmcnt(0) at every barrier): in iteration c the wave issues chunk c+2's weight unit and
+// activation pieces, writes chunk c+1's activation pieces (loaded one iteration ago) into
+// the LDS buffer nobody reads this iteration, multiplies chunk c (weights from the stage
+// loaded two iterations ago, activations from the other LDS buffer), then one barrier.
 template <int F, int NT, int WN>
-__global__ __launch_bounds__(256 * WN) void gemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
-                                                        uint16_t *__restrict__ C, float *__restrict__ P, int64_t M,
-                                                        int64_t N, int64_t K, int64_t ldc, int chunks_per_split)
-{
-    using L = Layout<F>;
-    constexpr int NTW = NT / WN;
-    constexpr int NW = 4 * WN;
-    __shared__ __attribute__((aligned(1024))) uint8_t lds[2 * 32 * NT * ROW_B];
+struct GemmCore {
+    static constexpr int NTW = NT / WN, NW = 4 * WN, NTHR = 64 * NW;
+    static constexpr int BP = (32 * NT * 16 + NTHR - 1) / NTHR; // 16-byte pieces per thread
+    static_assert((32 * NT * 16) % NTHR == 0, "activation tile must split evenly");
+    using St = Stage<F, BP>;
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave & 3, wn = wave >> 2;
-    const int h = lane >> 5, r32 = lane & 31;
-    const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * 32 * NT;
-    const int64_t nchunks = (K + KC - 1) / KC;
-    const int64_t c0 = (int64_t)blockIdx.z * chunks_per_split;
-    const int64_t c1 = c0 + chunks_per_split < nchunks ? c0 + chunks_per_split : nchunks;
-    const int64_t row_bytes = (K / L::QK) * L::BYTES;
-    const int64_t nb32 = K / 32;
+    const uint8_t *rowp;
+    const uint16_t *X;
+    int64_t n0, N, K, nb32;
+    int tid, h, r32, wn;
+    uint8_t *lds;
 
-    const int64_t row = m0 + 32 * wm + r32;
-    const uint8_t *rowp = A + (row < M ? row : M - 1) * row_bytes;
-
-    f32x16 acc[NTW];
-#pragma unroll
-    for (int i = 0; i < NTW; ++i)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
-
-    UnitRaw<F> nxt;
-    if (c0 < c1) {
-        stage_b<NT, NW>(lds, X, n0, N, K, c0, wave, lane);
-        nxt.load(rowp, (int)(2 * c0 + h), nb32);
+    __device__ __forceinline__ void issue(St &st, int64_t c) const
+    {
+        st.a.load(rowp, (int)(2 * c + h), nb32);
+        load_b<NT, NTHR, BP>(st.b, X, n0, N, K, c, tid);
     }
-    __syncthreads();
 
-    for (int64_t c = c0; c < c1; ++c) {
-        const UnitRaw<F> cur = nxt;
-        uint8_t *buf = lds + ((c - c0) & 1) * (32 * NT * ROW_B);
-        if (c + 1 < c1) {
-            stage_b<NT, NW>(lds + ((c + 1 - c0) & 1) * (32 * NT * ROW_B), X, n0, N, K, c + 1, wave, lane);
-            nxt.load(rowp, (int)(2 * (c + 1) + h), nb32);
-        }
+    __device__ __forceinline__ void compute(const St &st, const uint8_t *buf, f32x16 (&acc)[NTW]) const
+    {
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-            const f16x8 a = unit_frag<F>(cur, t);
+            const f16x8 a = unit_frag<F>(st.a, t);
             const int piece = piece_of<F>(h, t);
 #pragma unroll
             for (int i = 0; i < NTW; ++i) {
@@ -219,10 +221,73 @@ __global__ __launch_bounds__(256 * WN) void gemm_kernel(const uint8_t *__restric
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc[i], 0, 0, 0);
             }
         }
+    }
+
+    // one iteration: cur = chunk c, nxt = chunk c+1 (loaded), fut <- chunk c+2
+    __device__ __forceinline__ void step(const St &cur, const St &nxt, St &fut, int64_t c, int64_t c0, int64_t c1,
+                                         f32x16 (&acc)[NTW]) const
+    {
+        if (c + 2 < c1) issue(fut, c + 2);
+        if (c + 1 < c1) store_b<NTHR, BP>(lds + ((c + 1 - c0) & 1) * (32 * NT * ROW_B), nxt.b, tid);
+        compute(cur, lds + ((c - c0) & 1) * (32 * NT * ROW_B), acc);
         __syncthreads();
+    }
+};
+
+template <int F, int NT, int WN>
+__global__ __launch_bounds__(256 * WN) void gemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
+                                                        uint16_t *__restrict__ C, float *__restrict__ P, int64_t M,
+                                                        int64_t N, int64_t K, int64_t ldc, int chunks_per_split)
+{
+    using L = Layout<F>;
+    using Core = GemmCore<F, NT, WN>;
+    constexpr int NTW = Core::NTW;
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[2 * 32 * NT * ROW_B];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave & 3;
+    const int64_t m0 = (int64_t)blockIdx.x * BM;
+    const int64_t nchunks = (K + KC - 1) / KC;
+    const int64_t c0 = (int64_t)blockIdx.z * chunks_per_split;
+    const int64_t c1 = c0 + chunks_per_split < nchunks ? c0 + chunks_per_split : nchunks;
+    const int64_t row_bytes = (K / L::QK) * L::BYTES;
+    const int64_t row = m0 + 32 * wm + (lane & 31);
+
+    Core core;
+    core.rowp = A + (row < M ? row : M - 1) * row_bytes;
+    core.X = X;
+    core.n0 = (int64_t)blockIdx.y * 32 * NT;
+    core.N = N;
+    core.K = K;
+    core.nb32 = K / 32;
+    core.tid = tid;
+    core.h = lane >> 5;
+    core.r32 = lane & 31;
+    core.wn = wave >> 2;
+    core.lds = lds;
+
+    f32x16 acc[NTW];
+#pragma unroll
+    for (int i = 0; i < NTW; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+
+    typename Core::St s0, s1, s2;
+    if (c0 < c1) {
+        core.issue(s0, c0);
+        if (c0 + 1 < c1) core.issue(s1, c0 + 1);
+        store_b<Core::NTHR, Core::BP>(lds, s0.b, tid);
+    }
+    __syncthreads();
+    for (int64_t c = c0; c < c1; c += 3) {
+        core.step(s0, s1, s2, c, c0, c1, acc);
+        if (c + 1 < c1) core.step(s1, s2, s0, c + 1, c0, c1, acc);
+        if (c + 2 < c1) core.step(s2, s0, s1, c + 2, c0, c1, acc);
     }
 
     // epilogue: acc[i][e] = D[row 32wm + (e&3) + 8(e>>2) + 4h][token 32(wn*NTW+i) + r32]
+    const int h = lane >> 5, r32 = lane & 31, wn = wave >> 2;
+    const int64_t n0 = core.n0;
 #pragma unroll
     for (int i = 0; i < NTW; ++i) {
         const int64_t tok = n0 + 32 * (wn * NTW + i) + r32;
