@@ -27,89 +27,131 @@ __device__ __forceinline__ void act_blocks(int u, int &b0, int &b1)
     }
 }
 
+// A unit is handled in two steps so that loads can be issued far ahead of their use:
+//   UnitLoad<F>::load()  issues the unit's loads and keeps the raw registers (no arithmetic,
+//                        so nothing waits for the loads here);
+//   UnitRaw<F>::from()   decodes them (scales, code bytes) when the unit is consumed.
+template <int F> struct UnitLoad;
 template <int F> struct UnitRaw;
 
 // ---- Q8_0: two blocks ----
+template <> struct UnitLoad<Q8_0> {
+    uint32_t d0b, d1b;
+    u32x4 a0, a1, a2, a3;
+    __device__ __forceinline__ void load(const uint8_t *__restrict__ rowp, int u, int64_t nb32)
+    {
+        // unconditional loads: a missing second block re-reads the first (its d is zeroed later)
+        const uint8_t *p = rowp + 68 * (int64_t)u;
+        const bool has0 = 2 * (int64_t)u < nb32, has1 = 2 * (int64_t)u + 1 < nb32;
+        const uint8_t *p0 = has0 ? p : rowp, *p1 = has1 ? p + 34 : p0;
+        d0b = ld2(p0);
+        d1b = ld2(p1);
+        a0 = ld16(p0 + 2);
+        a1 = ld16(p0 + 18);
+        a2 = ld16(p1 + 2);
+        a3 = ld16(p1 + 18);
+    }
+};
+
 template <> struct UnitRaw<Q8_0> {
     float d0, d1;
     uint32_t w[16]; // int8 codes: w[0..7] block 2u, w[8..15] block 2u+1
 
-    __device__ __forceinline__ void load(const uint8_t *__restrict__ rowp, int u, int64_t nb32)
+    __device__ __forceinline__ static UnitRaw from(const UnitLoad<Q8_0> &l, int u, int64_t nb32)
     {
-        const uint8_t *p = rowp + 68 * (int64_t)u;
-        const bool has0 = 2 * (int64_t)u < nb32, has1 = 2 * (int64_t)u + 1 < nb32;
-        u32x4 a0 = {0, 0, 0, 0}, a1 = a0, a2 = a0, a3 = a0;
-        d0 = 0.f;
-        d1 = 0.f;
-        if (has0) {
-            d0 = h2f(ld2(p));
-            a0 = ld16(p + 2);
-            a1 = ld16(p + 18);
+        UnitRaw r;
+        r.d0 = 2 * (int64_t)u < nb32 ? h2f(l.d0b) : 0.f;
+        r.d1 = 2 * (int64_t)u + 1 < nb32 ? h2f(l.d1b) : 0.f;
+        const u32x4 v[4] = {l.a0, l.a1, l.a2, l.a3};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            r.w[4 * i] = v[i].x;
+            r.w[4 * i + 1] = v[i].y;
+            r.w[4 * i + 2] = v[i].z;
+            r.w[4 * i + 3] = v[i].w;
         }
-        if (has1) {
-            d1 = h2f(ld2(p + 34));
-            a2 = ld16(p + 36);
-            a3 = ld16(p + 52);
-        }
-        w[0] = a0.x; w[1] = a0.y; w[2] = a0.z; w[3] = a0.w;
-        w[4] = a1.x; w[5] = a1.y; w[6] = a1.z; w[7] = a1.w;
-        w[8] = a2.x; w[9] = a2.y; w[10] = a2.z; w[11] = a2.w;
-        w[12] = a3.x; w[13] = a3.y; w[14] = a3.z; w[15] = a3.w;
+        return r;
     }
 };
 
 // ---- Q4_K: one quarter of a super-block ----
-template <> struct UnitRaw<Q4_K> {
-    float ds0, dm0, ds1, dm1; // d*sc and dmin*m of the two sub-blocks
-    uint32_t w[8];            // 32 qs bytes: low nibbles = first sub-block, high = second
-
+template <> struct UnitLoad<Q4_K> {
+    u32x4 hdr, qa, qb;
     __device__ __forceinline__ void load(const uint8_t *__restrict__ rowp, int u, int64_t /*nb32*/)
     {
         const int sb = u >> 2, q = u & 3;
         const uint8_t *p = rowp + 144 * (int64_t)sb;
-        const u32x4 hdr = ld16(p);
-        const u32x4 qa = ld16(p + 16 + 32 * q), qb = ld16(p + 32 + 32 * q);
-        const float d = h2f(hdr.x & 0xffffu), dmin = h2f(hdr.x >> 16);
-        const uint32_t sw[3] = {hdr.y, hdr.z, hdr.w};
+        hdr = ld16(p);
+        qa = ld16(p + 16 + 32 * q);
+        qb = ld16(p + 32 + 32 * q);
+    }
+};
+
+template <> struct UnitRaw<Q4_K> {
+    float ds0, dm0, ds1, dm1; // d*sc and dmin*m of the two sub-blocks
+    uint32_t w[8];            // 32 qs bytes: low nibbles = first sub-block, high = second
+
+    __device__ __forceinline__ static UnitRaw from(const UnitLoad<Q4_K> &l, int u, int64_t /*nb32*/)
+    {
+        UnitRaw r;
+        const int q = u & 3;
+        const float d = h2f(l.hdr.x & 0xffffu), dmin = h2f(l.hdr.x >> 16);
+        const uint32_t sw[3] = {l.hdr.y, l.hdr.z, l.hdr.w};
         int sc0, m0, sc1, m1;
         q4k_sc_m(sw, 2 * q, sc0, m0);
         q4k_sc_m(sw, 2 * q + 1, sc1, m1);
-        ds0 = d * (float)sc0;
-        dm0 = dmin * (float)m0;
-        ds1 = d * (float)sc1;
-        dm1 = dmin * (float)m1;
-        w[0] = qa.x; w[1] = qa.y; w[2] = qa.z; w[3] = qa.w;
-        w[4] = qb.x; w[5] = qb.y; w[6] = qb.z; w[7] = qb.w;
+        r.ds0 = d * (float)sc0;
+        r.dm0 = dmin * (float)m0;
+        r.ds1 = d * (float)sc1;
+        r.dm1 = dmin * (float)m1;
+        r.w[0] = l.qa.x; r.w[1] = l.qa.y; r.w[2] = l.qa.z; r.w[3] = l.qa.w;
+        r.w[4] = l.qb.x; r.w[5] = l.qb.y; r.w[6] = l.qb.z; r.w[7] = l.qb.w;
+        return r;
     }
 };
 
 // ---- Q6_K: two 32-element runs of one super-block half ----
-template <> struct UnitRaw<Q6_K> {
-    float fa1, fa2, fb1, fb2; // d*sc for the four 16-element sub-blocks (A lo, A hi, B lo, B hi)
-    uint32_t ca[8], cb[8];     // 6-bit codes (0..63) of run A and run B, one per byte
-
+template <> struct UnitLoad<Q6_K> {
+    u32x4 l0, l1, g0, g1;
+    u32x2 sc8;
+    uint32_t dbits;
     __device__ __forceinline__ void load(const uint8_t *__restrict__ rowp, int u, int64_t /*nb32*/)
     {
         const int sb = u >> 2, h = (u >> 1) & 1, v = u & 1;
         const uint8_t *p = rowp + 210 * (int64_t)sb;
-        const u32x4 l0 = ld16(p + 64 * h + 32 * v), l1 = ld16(p + 64 * h + 32 * v + 16);
-        const u32x4 g0 = ld16(p + 128 + 32 * h), g1 = ld16(p + 144 + 32 * h);
-        const u32x2 sc8 = ld8(p + 192 + 8 * h);
-        const float d = h2f(ld2(p + 208));
-        const uint32_t ql[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
-        const uint32_t qh[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+        l0 = ld16(p + 64 * h + 32 * v);
+        l1 = ld16(p + 64 * h + 32 * v + 16);
+        g0 = ld16(p + 128 + 32 * h);
+        g1 = ld16(p + 144 + 32 * h);
+        sc8 = ld8(p + 192 + 8 * h);
+        dbits = ld2(p + 208);
+    }
+};
+
+template <> struct UnitRaw<Q6_K> {
+    float fa1, fa2, fb1, fb2; // d*sc for the four 16-element sub-blocks (A lo, A hi, B lo, B hi)
+    uint32_t ca[8], cb[8];     // 6-bit codes (0..63) of run A and run B, one per byte
+
+    __device__ __forceinline__ static UnitRaw from(const UnitLoad<Q6_K> &l, int u, int64_t /*nb32*/)
+    {
+        UnitRaw r;
+        const int v = u & 1;
+        const float d = h2f(l.dbits);
+        const uint32_t ql[8] = {l.l0.x, l.l0.y, l.l0.z, l.l0.w, l.l1.x, l.l1.y, l.l1.z, l.l1.w};
+        const uint32_t qh[8] = {l.g0.x, l.g0.y, l.g0.z, l.g0.w, l.g1.x, l.g1.y, l.g1.z, l.g1.w};
         const int shA = 2 * v, shB = 4 + 2 * v;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            ca[i] = (ql[i] & 0x0f0f0f0fu) | (((qh[i] >> shA) & 0x03030303u) << 4);
-            cb[i] = ((ql[i] >> 4) & 0x0f0f0f0fu) | (((qh[i] >> shB) & 0x03030303u) << 4);
+            r.ca[i] = (ql[i] & 0x0f0f0f0fu) | (((qh[i] >> shA) & 0x03030303u) << 4);
+            r.cb[i] = ((ql[i] >> 4) & 0x0f0f0f0fu) | (((qh[i] >> shB) & 0x03030303u) << 4);
         }
-        const uint32_t sA = v ? (sc8.x >> 16) : sc8.x;
-        const uint32_t sB = v ? (sc8.y >> 16) : sc8.y;
-        fa1 = d * (float)(int8_t)(sA & 0xff);
-        fa2 = d * (float)(int8_t)((sA >> 8) & 0xff);
-        fb1 = d * (float)(int8_t)(sB & 0xff);
-        fb2 = d * (float)(int8_t)((sB >> 8) & 0xff);
+        const uint32_t sA = v ? (l.sc8.x >> 16) : l.sc8.x;
+        const uint32_t sB = v ? (l.sc8.y >> 16) : l.sc8.y;
+        r.fa1 = d * (float)(int8_t)(sA & 0xff);
+        r.fa2 = d * (float)(int8_t)((sA >> 8) & 0xff);
+        r.fb1 = d * (float)(int8_t)(sB & 0xff);
+        r.fb2 = d * (float)(int8_t)((sB >> 8) & 0xff);
+        return r;
     }
 };
 

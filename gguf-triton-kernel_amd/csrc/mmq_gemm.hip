@@ -145,7 +145,8 @@ __device__ __forceinline__ int piece_of(int h, int t)
 // chunk's activation tile (BP 16-byte pieces).
 template <int F, int BP>
 struct Stage {
-    UnitRaw<F> a;
+    UnitLoad<F> a;
+    int u;
     u32x4 b[BP];
 };
 
@@ -204,15 +205,17 @@ struct GemmCore {
 
     __device__ __forceinline__ void issue(St &st, int64_t c) const
     {
-        st.a.load(rowp, (int)(2 * c + h), nb32);
+        st.u = (int)(2 * c + h);
+        st.a.load(rowp, st.u, nb32);
         load_b<NT, NTHR, BP>(st.b, X, n0, N, K, c, tid);
     }
 
     __device__ __forceinline__ void compute(const St &st, const uint8_t *buf, f32x16 (&acc)[NTW]) const
     {
+        const UnitRaw<F> unit = UnitRaw<F>::from(st.a, st.u, nb32);
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-            const f16x8 a = unit_frag<F>(st.a, t);
+            const f16x8 a = unit_frag<F>(unit, t);
             const int piece = piece_of<F>(h, t);
 #pragma unroll
             for (int i = 0; i < NTW; ++i) {
@@ -223,12 +226,14 @@ struct GemmCore {
         }
     }
 
-    // one iteration: cur = chunk c, nxt = chunk c+1 (loaded), fut <- chunk c+2
+    // one iteration: cur = chunk c, nxt = chunk c+1 (loaded), fut <- chunk c+2.  Branch-free:
+    // past the end the chunk index is clamped (a redundant load, a store into the buffer no
+    // one reads again) so the compiler's vmcnt counting sees the same loads on every path.
     __device__ __forceinline__ void step(const St &cur, const St &nxt, St &fut, int64_t c, int64_t c0, int64_t c1,
                                          f32x16 (&acc)[NTW]) const
     {
-        if (c + 2 < c1) issue(fut, c + 2);
-        if (c + 1 < c1) store_b<NTHR, BP>(lds + ((c + 1 - c0) & 1) * (32 * NT * ROW_B), nxt.b, tid);
+        issue(fut, c + 2 < c1 ? c + 2 : c1 - 1);
+        store_b<NTHR, BP>(lds + ((c + 1 - c0) & 1) * (32 * NT * ROW_B), nxt.b, tid);
         compute(cur, lds + ((c - c0) & 1) * (32 * NT * ROW_B), acc);
         __syncthreads();
     }
@@ -275,14 +280,17 @@ __global__ __launch_bounds__(256 * WN) void gemm_kernel(const uint8_t *__restric
     typename Core::St s0, s1, s2;
     if (c0 < c1) {
         core.issue(s0, c0);
-        if (c0 + 1 < c1) core.issue(s1, c0 + 1);
+        core.issue(s1, c0 + 1 < c1 ? c0 + 1 : c1 - 1);
         store_b<Core::NTHR, Core::BP>(lds, s0.b, tid);
-    }
-    __syncthreads();
-    for (int64_t c = c0; c < c1; c += 3) {
-        core.step(s0, s1, s2, c, c0, c1, acc);
+        __syncthreads();
+        int64_t c = c0;
+        for (; c + 3 <= c1; c += 3) {
+            core.step(s0, s1, s2, c, c0, c1, acc);
+            core.step(s1, s2, s0, c + 1, c0, c1, acc);
+            core.step(s2, s0, s1, c + 2, c0, c1, acc);
+        }
+        if (c < c1) core.step(s0, s1, s2, c, c0, c1, acc);
         if (c + 1 < c1) core.step(s1, s2, s0, c + 1, c0, c1, acc);
-        if (c + 2 < c1) core.step(s2, s0, s1, c + 2, c0, c1, acc);
     }
 
     // epilogue: acc[i][e] = D[row 32wm + (e&3) + 8(e>>2) + 4h][token 32(wn*NTW+i) + r32]

@@ -125,9 +125,9 @@ template <int F, int NT>
 __device__ __forceinline__ void unit_dot(const uint8_t *__restrict__ rowp, int u, int64_t nb, const Act<F, NT> &a,
                                          float (&acc)[NT])
 {
-    UnitRaw<F> r;
-    r.load(rowp, u, nb);
-    dot_unit<F, NT>(r, a, acc);
+    UnitLoad<F> l;
+    l.load(rowp, u, nb);
+    dot_unit<F, NT>(UnitRaw<F>::from(l, u, nb), a, acc);
 }
 
 __device__ __forceinline__ float wave_sum(float v)
@@ -236,14 +236,14 @@ __device__ __forceinline__ void load_act_lds(Act<F, NT> &a, const uint8_t *codes
 }
 
 template <int F, int R>
-__device__ __forceinline__ void load_rows(UnitRaw<F> (&dst)[R], const uint8_t *__restrict__ A, int64_t row_bytes,
+__device__ __forceinline__ void load_rows(UnitLoad<F> (&dst)[R], const uint8_t *__restrict__ A, int64_t row_bytes,
                                           int64_t row0, int64_t M, int u, int nunits, int64_t nb)
 {
+    const int uu = u < nunits ? u : nunits - 1; // unconditional loads; lanes past the end are masked at use
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int64_t row = row0 + r < M ? row0 + r : M - 1;
-        if (u < nunits) dst[r].load(A + row * row_bytes, u, nb);
-        else dst[r] = UnitRaw<F>{};
+        dst[r].load(A + row * row_bytes, uu, nb);
     }
 }
 
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void decode_kernel(const uint8_t *__restrict__
 
     int64_t g = (int64_t)blockIdx.x * 4 + wave;
     int it = 0;
-    UnitRaw<F> cur[R];
+    UnitLoad<F> cur[R];
     if (g < ngroups) load_rows<F, R>(cur, A, row_bytes, g * R, M, lane, nunits, nb);
 
     // q8_1-quantize tokens tok0..tok0+NT-1 into LDS (8 lanes per 32-element block)
@@ -306,14 +306,14 @@ __global__ __launch_bounds__(256) void decode_kernel(const uint8_t *__restrict__
             it2 = 0;
             g2 += gstride;
         }
-        UnitRaw<F> nxt[R];
-        if (g2 < ngroups) load_rows<F, R>(nxt, A, row_bytes, g2 * R, M, lane + 64 * it2, nunits, nb);
+        UnitLoad<F> nxt[R];
+        load_rows<F, R>(nxt, A, row_bytes, (g2 < ngroups ? g2 : g) * R, M, lane + 64 * it2, nunits, nb);
         const int u = lane + 64 * it;
         if (u < nunits) {
             Act<F, NT> a;
             load_act_lds<F, NT>(a, codes, sd, ss, kp, nb, u);
 #pragma unroll
-            for (int r = 0; r < R; ++r) dot_unit<F, NT>(cur[r], a, acc[r]);
+            for (int r = 0; r < R; ++r) dot_unit<F, NT>(UnitRaw<F>::from(cur[r], u, nb), a, acc[r]);
         }
         if (it2 == 0) {
 #pragma unroll
