@@ -33,6 +33,9 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ u32x4 ld16(const void *p)
 {
+#ifdef GQ_ALIGN_TEST // diagnostic only: same access pattern with 16-byte aligned addresses
+    p = (const void *)((uintptr_t)p & ~(uintptr_t)15);
+#endif
     u32x4 v;
     __builtin_memcpy(&v, p, 16);
     return v;
@@ -40,6 +43,9 @@ __device__ __forceinline__ u32x4 ld16(const void *p)
 
 __device__ __forceinline__ u32x2 ld8(const void *p)
 {
+#ifdef GQ_ALIGN_TEST
+    p = (const void *)((uintptr_t)p & ~(uintptr_t)7);
+#endif
     u32x2 v;
     __builtin_memcpy(&v, p, 8);
     return v;

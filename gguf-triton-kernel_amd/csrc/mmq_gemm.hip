@@ -26,6 +26,9 @@
 //     so any consistent permutation is exact).
 // MFMA 32x32x16 f16 operand maps (gfx950): lane l holds A[row l&31][k 8(l>>5)+j] and
 // B[k 8(l>>5)+j][col l&31]; D[row (i&3)+8(i>>2)+4(l>>5)][col l&31] in acc element i.
+// The activations are the A operand (MFMA rows = tokens) and the weights the B operand
+// (MFMA columns = weight rows), so the accumulator's lane index runs along C's contiguous
+// dimension.
 #include <cstdlib>
 
 #include "gguf_blocks.hpp"
@@ -190,7 +193,9 @@ __device__ __forceinline__ void store_b(uint8_t *buf, const u32x4 (&b)[BP], int 
 // activation pieces, writes chunk c+1's activation pieces (loaded one iteration ago) into
 // the LDS buffer nobody reads this iteration, multiplies chunk c (weights from the stage
 // loaded two iterations ago, activations from the other LDS buffer), then one barrier.
-template <int F, int NT, int WN>
+// ABL: ablation bitmask for performance diagnosis only (tools/ablate.sh); 0 in production.
+//   1 = no MFMA, 2 = no weight loads, 4 = no activation global loads, 8 = no LDS B reads.
+template <int F, int NT, int WN, int ABL = 0>
 struct GemmCore {
     static constexpr int NTW = NT / WN, NW = 4 * WN, NTHR = 64 * NW;
     static constexpr int BP = (32 * NT * 16 + NTHR - 1) / NTHR; // 16-byte pieces per thread
@@ -206,8 +211,19 @@ struct GemmCore {
     __device__ __forceinline__ void issue(St &st, int64_t c) const
     {
         st.u = (int)(2 * c + h);
-        st.a.load(rowp, st.u, nb32);
-        load_b<NT, NTHR, BP>(st.b, X, n0, N, K, c, tid);
+        if constexpr (ABL & 2) {
+            const uint32_t z = (uint32_t)c * 0x01010101u + (uint32_t)tid;
+            __builtin_memset(&st.a, 0, sizeof(st.a));
+            *(uint32_t *)&st.a = z;
+        } else {
+            st.a.load(rowp, st.u, nb32);
+        }
+        if constexpr (ABL & 4) {
+#pragma unroll
+            for (int i = 0; i < BP; ++i) st.b[i] = (u32x4){(uint32_t)c, (uint32_t)tid, 1u, 2u};
+        } else {
+            load_b<NT, NTHR, BP>(st.b, X, n0, N, K, c, tid);
+        }
     }
 
     __device__ __forceinline__ void compute(const St &st, const uint8_t *buf, f32x16 (&acc)[NTW]) const
@@ -220,8 +236,17 @@ struct GemmCore {
 #pragma unroll
             for (int i = 0; i < NTW; ++i) {
                 const int trow = 32 * (wn * NTW + i) + r32;
-                const f16x8 b = *(const f16x8 *)(buf + trow * ROW_B + 16 * (piece ^ (trow & 15)));
-                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc[i], 0, 0, 0);
+                f16x8 b;
+                if constexpr (ABL & 8) b = a;
+                else b = *(const f16x8 *)(buf + trow * ROW_B + 16 * (piece ^ (trow & 15)));
+                if constexpr (ABL & 1) {
+                    acc[i][t] += (float)a[i] + (float)b[t];
+                } else {
+                    // tokens on the MFMA's M side, weight rows on its N side: D[token][row], so
+                    // a lane's outputs are one weight row and consecutive lanes store
+                    // consecutive rows of C (coalesced epilogue)
+                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b, a, acc[i], 0, 0, 0);
+                }
             }
         }
     }
@@ -239,13 +264,13 @@ struct GemmCore {
     }
 };
 
-template <int F, int NT, int WN>
+template <int F, int NT, int WN, int ABL = 0>
 __global__ __launch_bounds__(256 * WN) void gemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
                                                         uint16_t *__restrict__ C, float *__restrict__ P, int64_t M,
                                                         int64_t N, int64_t K, int64_t ldc, int chunks_per_split)
 {
     using L = Layout<F>;
-    using Core = GemmCore<F, NT, WN>;
+    using Core = GemmCore<F, NT, WN, ABL>;
     constexpr int NTW = Core::NTW;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[2 * 32 * NT * ROW_B];
 
@@ -293,31 +318,20 @@ __global__ __launch_bounds__(256 * WN) void gemm_kernel(const uint8_t *__restric
         if (c + 1 < c1) core.step(s1, s2, s0, c + 1, c0, c1, acc);
     }
 
-    // epilogue: acc[i][e] = D[row 32wm + (e&3) + 8(e>>2) + 4h][token 32(wn*NTW+i) + r32]
+    // epilogue: acc[i][e] = D[token 32(wn*NTW+i) + (e&3) + 8(e>>2) + 4h][row 32wm + r32]; each
+    // store instruction writes two runs of 32 consecutive rows (one per half-wave)
     const int h = lane >> 5, r32 = lane & 31, wn = wave >> 2;
     const int64_t n0 = core.n0;
+    const int64_t rr = m0 + 32 * wm + r32;
+    if (rr < M) {
 #pragma unroll
-    for (int i = 0; i < NTW; ++i) {
-        const int64_t tok = n0 + 32 * (wn * NTW + i) + r32;
-        if (tok >= N) continue;
+        for (int i = 0; i < NTW; ++i) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int64_t rr = m0 + 32 * wm + 8 * g + 4 * h;
-            const float vv[4] = {acc[i][4 * g], acc[i][4 * g + 1], acc[i][4 * g + 2], acc[i][4 * g + 3]};
-            if (P == nullptr) {
-                uint16_t *cp = C + tok * ldc + rr;
-                if (rr + 3 < M) {
-                    u32x2 o = {pk_f16(vv[0], vv[1]), pk_f16(vv[2], vv[3])};
-                    __builtin_memcpy(cp, &o, 8);
-                } else {
-                    for (int e = 0; e < 4; ++e)
-                        if (rr + e < M) cp[e] = f2h_bits(vv[e]);
-                }
-            } else {
-                float *pp = P + ((int64_t)blockIdx.z * N + tok) * M + rr;
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (rr + e < M) pp[e] = vv[e];
+            for (int e = 0; e < 16; ++e) {
+                const int64_t tok = n0 + 32 * (wn * NTW + i) + (e & 3) + 8 * (e >> 2) + 4 * h;
+                if (tok >= N) continue;
+                if (P == nullptr) C[tok * ldc + rr] = f2h_bits(acc[i][e]);
+                else P[((int64_t)blockIdx.z * N + tok) * M + rr] = acc[i][e];
             }
         }
     }
@@ -341,6 +355,22 @@ hipError_t launch_nt(const uint8_t *A, const uint16_t *X, uint16_t *C, float *P,
 {
     dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((N + 32 * NT - 1) / (32 * NT)), (unsigned)S),
         block(256 * WN);
+#ifdef GQ_ABLATION
+    if constexpr (NT == 4) {
+        static const int abl = getenv("GQ_ABLATE") ? atoi(getenv("GQ_ABLATE")) : 0;
+        float *PP = S > 1 ? P : nullptr;
+        switch (abl) {
+        case 1: gemm_kernel<F, NT, WN, 1><<<grid, block, 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+        case 2: gemm_kernel<F, NT, WN, 2><<<grid, block, 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+        case 4: gemm_kernel<F, NT, WN, 4><<<grid, block, 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+        case 8: gemm_kernel<F, NT, WN, 8><<<grid, block, 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+        case 6: gemm_kernel<F, NT, WN, 6><<<grid, block, 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+        case 9: gemm_kernel<F, NT, WN, 9><<<grid, block, 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+        case 15: gemm_kernel<F, NT, WN, 15><<<grid, block, 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+        default: gemm_kernel<F, NT, WN><<<grid, block, 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+        }
+    } else
+#endif
     gemm_kernel<F, NT, WN><<<grid, block, 0, s>>>(A, X, C, S > 1 ? P : nullptr, M, N, K, ldc, cps);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || S == 1) return e;
