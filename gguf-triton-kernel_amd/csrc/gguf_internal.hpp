@@ -25,11 +25,15 @@ hipError_t launch_decode_fused(int fmt, const uint8_t *A, const uint16_t *X, int
 
 // Batched GEMM on fp16 MFMA (mmq_gemm.hip): C[t][m] from the dequantized activation x~.
 struct GemmPlan {
+    int nb = 8;                // 16-token groups per workgroup (tile = 16*nb tokens)
+    int rg = 2;                // 16-row groups per wave (8 waves: tile = 128*rg weight rows)
     int splits = 1;            // split-K factor (grid.z)
-    int chunks_per_split = 1;  // 128-wide K chunks per split
+    int chunks_per_split = 1;  // 128-wide K stages per split
     size_t partial_bytes = 0;  // fp32 partial slabs needed when splits > 1
 };
-GemmPlan plan_gemm(int64_t M, int64_t N, int64_t K);
+// The MFMA GEMM needs K in whole 128-element stages (always true for Q4_K/Q6_K).
+bool gemm_supported(int fmt, int64_t K);
+GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K);
 hipError_t launch_gemm(int fmt, const uint8_t *A, const uint16_t *xdeq, uint16_t *C, float *partials,
                        const GemmPlan &plan, int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
 

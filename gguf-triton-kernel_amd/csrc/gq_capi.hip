@@ -32,12 +32,14 @@ size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
 // Decode path up to this many tokens; beyond it the fp16-MFMA GEMM.
 constexpr int64_t kGemvMaxTokens = 8;
 
-bool use_gemv(int64_t N) { return N <= kGemvMaxTokens; }
+// (K % 128 != 0 is only possible for Q8_0, so the choice depends on N and K alone and
+// gq_act_prepare, which does not know the weight type, makes the same one.)
+bool use_gemv(int64_t N, int64_t K) { return N <= kGemvMaxTokens || !gq::gemm_supported(gq::Q8_0, K); }
 
 // Activation part of the workspace (what gq_act_prepare writes); depends on N, K only.
 size_t act_bytes(int64_t N, int64_t K)
 {
-    if (use_gemv(N)) {
+    if (use_gemv(N, K)) {
         // SOA q8_1: codes + d + s
         return align_up((size_t)N * K) + 2 * align_up((size_t)N * (K / 32) * sizeof(float));
     }
@@ -45,10 +47,10 @@ size_t act_bytes(int64_t N, int64_t K)
 }
 
 // Whole workspace: activations + (GEMM split-K) fp32 partial slabs.
-size_t ws_bytes(int64_t M, int64_t N, int64_t K)
+size_t ws_bytes(int t, int64_t M, int64_t N, int64_t K)
 {
     size_t b = act_bytes(N, K);
-    if (!use_gemv(N)) b += align_up(gq::plan_gemm(M, N, K).partial_bytes);
+    if (!use_gemv(N, K)) b += align_up(gq::plan_gemm(t, M, N, K).partial_bytes);
     return b;
 }
 
@@ -63,9 +65,8 @@ const char *gq_last_error(void) { return g_err.c_str(); }
 
 size_t gq_mmq_workspace_size(gq_type t, int64_t M, int64_t N, int64_t K)
 {
-    (void)t;
     if (N <= 0 || K <= 0 || M < 0) return 0;
-    return ws_bytes(M, N, K);
+    return ws_bytes(t, M, N, K);
 }
 
 static int check_common(gq_type t, int64_t M, int64_t N, int64_t K)
@@ -89,7 +90,7 @@ static Carved carve(void *workspace, int64_t N, int64_t K)
 {
     uint8_t *ws = (uint8_t *)workspace;
     Carved c{};
-    if (use_gemv(N)) {
+    if (use_gemv(N, K)) {
         c.xq = (int8_t *)ws;
         c.xd = (float *)(ws + align_up((size_t)N * K));
         c.xs = (float *)((uint8_t *)c.xd + align_up((size_t)N * (K / 32) * sizeof(float)));
@@ -109,7 +110,7 @@ static int prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *works
     if (!workspace || workspace_bytes < need)
         return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace ? workspace_bytes : (size_t)0, need);
     Carved c = carve(workspace, N, K);
-    hipError_t e = use_gemv(N) ? gq::launch_act_quant(gq::ACT_SOA, (const uint16_t *)B, ldb, N, K, c.xq, c.xd, c.xs, s)
+    hipError_t e = use_gemv(N, K) ? gq::launch_act_quant(gq::ACT_SOA, (const uint16_t *)B, ldb, N, K, c.xq, c.xd, c.xs, s)
                                : gq::launch_act_quant(gq::ACT_DEQ, (const uint16_t *)B, ldb, N, K, c.xdeq, nullptr,
                                                       nullptr, s);
     if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (act_quant): %s", hipGetErrorString(e));
@@ -121,12 +122,12 @@ static int compute(gq_type t, const void *A, void *workspace, size_t workspace_b
 {
     if (!A || !C || !workspace) return fail(GQ_EINVAL, "null pointer (A=%p C=%p workspace=%p)", A, C, workspace);
     if (ldc < M) return fail(GQ_EINVAL, "ldc=%lld < M=%lld", (long long)ldc, (long long)M);
-    const size_t need = ws_bytes(M, N, K);
+    const size_t need = ws_bytes(t, M, N, K);
     if (workspace_bytes < need) return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace_bytes, need);
     Carved c = carve(workspace, N, K);
-    hipError_t e = use_gemv(N) ? gq::launch_gemv(t, (const uint8_t *)A, c.xq, c.xd, c.xs, (uint16_t *)C, M, N, K, ldc, s)
+    hipError_t e = use_gemv(N, K) ? gq::launch_gemv(t, (const uint8_t *)A, c.xq, c.xd, c.xs, (uint16_t *)C, M, N, K, ldc, s)
                                : gq::launch_gemm(t, (const uint8_t *)A, c.xdeq, (uint16_t *)C, c.partials,
-                                                 gq::plan_gemm(M, N, K), M, N, K, ldc, s);
+                                                 gq::plan_gemm(t, M, N, K), M, N, K, ldc, s);
     if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (mmq): %s", hipGetErrorString(e));
     return GQ_OK;
 }
@@ -141,11 +142,11 @@ int gq_mmq(gq_type t, const void *A, const void *B, void *C, int64_t M, int64_t 
     if (K == 0) return fail(GQ_EINVAL, "K must be positive");
     if (!A || !B || !C) return fail(GQ_EINVAL, "null pointer (A=%p B=%p C=%p)", A, B, C);
     if (ldc < M) return fail(GQ_EINVAL, "ldc=%lld < M=%lld", (long long)ldc, (long long)M);
-    if (!workspace || workspace_bytes < ws_bytes(M, N, K))
+    if (!workspace || workspace_bytes < ws_bytes(t, M, N, K))
         return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace ? workspace_bytes : (size_t)0,
-                    ws_bytes(M, N, K));
+                    ws_bytes(t, M, N, K));
     if (ldb < K) return fail(GQ_EINVAL, "ldb=%lld < K=%lld", (long long)ldb, (long long)K);
-    if (use_gemv(N) && gq::decode_fused_ok(t, N, K) && !getenv("GQ_NO_FUSED_DECODE")) {
+    if (use_gemv(N, K) && gq::decode_fused_ok(t, N, K) && !getenv("GQ_NO_FUSED_DECODE")) {
         // one launch: activation quantization in LDS + decode GEMV
         hipError_t e = gq::launch_decode_fused(t, (const uint8_t *)A, (const uint16_t *)B, ldb, (uint16_t *)C, M, N,
                                                K, ldc, (hipStream_t)stream);

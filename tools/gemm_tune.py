@@ -1,0 +1,42 @@
+"""GEMM tuning / ablation sweep on one GPU: kernel time (HIP events over a graph of launches,
+activations prepared once) for bench.py configs under env overrides.
+
+Usage: python tools/gemm_tune.py [--abl] CONFIG[:ENV=V,ENV=V...] ...
+  --abl   load build/abl/libgguf_mmq_abl.so (make -C gguf-triton-kernel_amd abl) so that
+          GQ_ABLATE=<mask> selects the ablation variants of mmq_gemm.hip.
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gguf-triton-kernel_amd")]
+import kernels._lib as kl  # noqa: E402
+
+args = sys.argv[1:]
+if args and args[0] == "--abl":
+    kl.LIB_PATH = os.path.join(ROOT, "gguf-triton-kernel_amd", "lib", "libgguf_mmq_abl.so")
+    args = args[1:]
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+dev = torch.device("cuda:0")
+KEYS = ("GQ_ABLATE", "GQ_GEMM_RG", "GQ_GEMM_NB", "GQ_GEMM_SPLITS")
+for spec in args:
+    cfg, _, envs = spec.partition(":")
+    for k in KEYS:
+        os.environ.pop(k, None)
+    for kv in filter(None, envs.split(",")):
+        k, v = kv.split("=")
+        os.environ[k] = v
+    fmt, M, K, N = bench.CONFIGS[cfg]
+    r = bench.Runner(fmt, M, K, N, dev, 40)
+    r.prepare()
+    g = r.capture(r.kernel, 40)
+    g.replay()
+    t = min(bench.timed_replay(g, dev) for _ in range(5)) / 40
+    _, alg_bytes, flops = bench.model(fmt, M, K, N)
+    print(f"{spec:60s} kernel_us={t * 1e6:8.2f}  {flops / t / 1e12:7.1f} TF/s  {alg_bytes / t / 1e9:7.1f} GB/s",
+          flush=True)
+    del r, g
+    torch.cuda.empty_cache()
