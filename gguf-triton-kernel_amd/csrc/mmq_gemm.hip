@@ -62,89 +62,69 @@ __device__ __forceinline__ h2 pair02(uint32_t c) { return as_h2(__builtin_amdgcn
 __device__ __forceinline__ h2 pair13(uint32_t c) { return as_h2(__builtin_amdgcn_perm(0x64646464u, c, 0x04030401u)); }
 
 // ---------------------------------------------------------------------------------------
-// Per-format stage geometry.  A stage's weight bytes arrive as NP 16-byte pieces per row.
-// Q4_K/Q6_K pieces are stored piece-major in LDS ([j][row][16 B]) so that one DMA
-// instruction moves piece j of 64 consecutive rows and the stage-dependent part of its source
-// offset is wave-uniform (SGPR soffset); Q8_0 pieces are row-major ([row][5 x 16 B]) because
-// its stage offset (68 B per stage) is the same for every piece.
-template <int F> struct Stage;
+// Weight stages are one super-block of K (256 elements; Q8_0: 8 blocks) per row, moved as
+// the row's contiguous bytes (16-byte pieces from a 16-byte aligned window: full cache lines,
+// the shape HBM streams at its full rate).  Activation sub-stages are 64 elements.
+// Per format: RBW = LDS bytes per row per weight stage (pieces NPW = RBW / 16), SB = packed
+// bytes per stage.  Q6_K rows are only 2-byte aligned: its window starts at floor16 of the
+// stage's first byte and the reader adds that misalignment (delta, per row and stage).
+template <int F> struct WStage;
+template <> struct WStage<Q4_K> { static constexpr int RBW = 144, SB = 144; };
+template <> struct WStage<Q6_K> { static constexpr int RBW = 224, SB = 210; };
+template <> struct WStage<Q8_0> { static constexpr int RBW = 272, SB = 272; };
 
-// Q4_K: stage c = quarter q = c&3 of super-block c>>2 = sub-blocks 2q (low nibbles) and 2q+1
-// (high nibbles) of qs bytes 32q..32q+31.  Pieces: 0 = d,dmin,scales | 1,2 = qs[32q..+32).
-template <> struct Stage<Q4_K> {
-    static constexpr int NP = 3;
-    __device__ static uint32_t soff(int64_t c, int j)
-    {
-        return (uint32_t)(144 * (c >> 2)) + (j == 0 ? 0u : (uint32_t)(16 * j + 32 * (c & 3)));
-    }
-    __device__ static uint32_t act_soff(int64_t c) { return (uint32_t)(2 * KC * c); }
-    __device__ static uint32_t act_voff(int p) { return 16u * p; }
-};
-
-// Q6_K: stage c = (super-block c>>2, half h = (c>>1)&1, v = c&1): k-step 0 = elements
-// 128h+32v+[0,32) (ql low nibbles, qh bits 2v), k-step 1 = 128h+64+32v+[0,32) (ql high
-// nibbles, qh bits 4+2v).  Pieces: 0,1 = ql[64h+32v..+32) | 2,3 = qh[32h..+32) |
-// 4 = scales[0..16) | 5 = block bytes 194..209 (d at offset 14).
-template <> struct Stage<Q6_K> {
-    static constexpr int NP = 6;
-    __device__ static uint32_t soff(int64_t c, int j)
-    {
-        const int h = (int)(c >> 1) & 1, v = (int)c & 1;
-        const int o = j < 2 ? 64 * h + 32 * v + 16 * j : (j < 4 ? 128 + 32 * h + 16 * (j - 2) : (j == 4 ? 192 : 194));
-        return (uint32_t)(210 * (c >> 2)) + (uint32_t)o;
-    }
-    __device__ static uint32_t act_soff(int64_t c)
-    {
-        return (uint32_t)(2 * (256 * (c >> 2) + 128 * ((c >> 1) & 1) + 32 * (c & 1)));
-    }
-    __device__ static uint32_t act_voff(int p) { return 2u * (64 * (p >> 2) + 8 * (p & 3)); }
-};
-
-// Q8_0: stage c = blocks 2c, 2c+1 (68 B).  Row-major pieces: [0,64) bytes 0..63 | [64,80)
-// bytes 52..67 (a read of bytes [x, x+8) with x+8 > 64 goes to LDS x + 12).
-template <> struct Stage<Q8_0> {
-    static constexpr int NP = 5;
-    __device__ static uint32_t piece_base(int j) { return j < 4 ? 16u * j : 52u; }
-    __device__ static uint32_t act_soff(int64_t c) { return (uint32_t)(2 * KC * c); }
-    __device__ static uint32_t act_voff(int p) { return 16u * p; }
-};
+// Activation sub-stage c (64 elements) = sub-stage s4 = c & 3 of super-block c >> 2: the K
+// elements whose weights the k-steps read (Q6_K: two 32-element runs, see frags below).
+template <int F>
+__device__ __forceinline__ uint32_t act_soff(int64_t c)
+{
+    if constexpr (F == Q6_K) return (uint32_t)(2 * (256 * (c >> 2) + 128 * ((c >> 1) & 1) + 32 * (c & 1)));
+    return (uint32_t)(2 * KC * c);
+}
+template <int F>
+__device__ __forceinline__ uint32_t act_voff(int p) // byte offset of piece p (8 elements) in the sub-stage
+{
+    if constexpr (F == Q6_K) return 2u * (64 * (p >> 2) + 8 * (p & 3));
+    return 16u * p;
+}
 
 constexpr int NWAVE = 8; // 512 threads: two waves per SIMD
+constexpr int NWS = 3;   // weight-stage ring: two super-blocks in flight (HBM latency ~1.5 us)
 
-template <int F, int NB, int RG>
+template <int F, int NB>
 struct Cfg {
-    static constexpr int BN = 16 * NB, BM = 16 * RG * NWAVE;
-    static constexpr int NP = Stage<F>::NP;
-    static constexpr int W_INS = BM * NP / 64;          // weight DMA instructions per stage (workgroup)
-    static constexpr int A_INS = BN * 8 / 64;           // activation DMA instructions per stage
-    static constexpr int NI = W_INS + A_INS;
-    static constexpr int MAXI = (NI + NWAVE - 1) / NWAVE; // per wave (waves w < NI % 8 own one more)
-    static constexpr int MINI = NI / NWAVE;
-    static constexpr int STAGE_BYTES = NI * 1024;
-    static constexpr int LDS_BYTES = NSTAGE * STAGE_BYTES;
-    static_assert(BM * NP % 64 == 0 && BN * 8 % 64 == 0, "whole DMA instructions");
+    static constexpr int BN = 16 * NB, BM = 16 * NWAVE; // 128 weight rows x 16*NB tokens
+    static constexpr int RBW = WStage<F>::RBW, NPW = RBW / 16;
+    static constexpr int W_REAL = BM * NPW / 64;                              // DMA instructions per stage
+    static constexpr int A_REAL = BN * 8 / 64 > 0 ? BN * 8 / 64 : 1;
+    static constexpr int NW = (W_REAL + NWAVE - 1) / NWAVE, NA = (A_REAL + NWAVE - 1) / NWAVE; // per wave
+    static constexpr int W_SLOT = W_REAL * 1024, A_SLOT = A_REAL * 1024;
+    // activation sub-stage ring: 4 slots (3 in flight) unless the LDS budget says 3
+    static constexpr int NAS = NWS * W_SLOT + 4 * A_SLOT + 1024 <= LDS_MAX ? 4 : 3;
+    static constexpr int A_BASE = NWS * W_SLOT, SCRATCH = A_BASE + NAS * A_SLOT; // dummy DMAs land there
+    static constexpr int LDS_BYTES = SCRATCH + 1024;
+    static_assert(BM * NPW % 64 == 0 && (BN * 8) % 64 == 0 || BN * 8 < 64, "whole DMA instructions");
     static_assert(LDS_BYTES <= LDS_MAX, "LDS budget");
-    static_assert(2 * MAXI <= 63, "vmcnt range");
+    static_assert((NAS - 2) * NA + NW <= 63, "vmcnt range");
 };
 
 // ---------------------------------------------------------------------------------------
-// A fragments of one stage for one 16-row group: frag[s] = the 8 weights (fragment element
-// order) of k-step s for this lane's row and k-group g.  pc(j) = the row's piece j in LDS.
-template <int F, class PC>
-__device__ __forceinline__ void stage_frags(PC pc, int g, int64_t c, f16x8 (&frag)[2]);
+// A fragments of sub-stage s4 for this lane's row: frag[s] = the 8 weights (fragment element
+// order) of k-step s, k-group g.  wr = the row's stage bytes in LDS (block byte 0).
+template <int F>
+__device__ __forceinline__ void stage_frags(const uint8_t *wr, int g, int s4, f16x8 (&frag)[2]);
 
-template <int F, class PC>
-__device__ __forceinline__ typename std::enable_if<F == Q4_K>::type
-stage_frags_impl(PC pc, int g, int64_t c, f16x8 (&frag)[2])
+// Q4_K sub-stage q: sub-blocks 2q (low nibbles) and 2q+1 (high nibbles) of qs bytes 32q..+32.
+template <>
+__device__ __forceinline__ void stage_frags<Q4_K>(const uint8_t *wr, int g, int q, f16x8 (&frag)[2])
 {
-    const int q = (int)c & 3;
-    const u32x4 hdr = *(const u32x4 *)pc(0);
+    const u32x4 hdr = *(const u32x4 *)wr;
     const float d = h2f(hdr.x & 0xffffu), dmin = h2f(hdr.x >> 16);
     // 6-bit scales / mins of sub-blocks 2q, 2q+1, one per byte (get_scale_min_k4)
     const uint32_t sc = q < 2 ? (hdr.y & 0x3f3f3f3fu) : ((hdr.w & 0x0f0f0f0fu) | ((hdr.y >> 2) & 0x30303030u));
     const uint32_t mn = q < 2 ? (hdr.z & 0x3f3f3f3fu) : (((hdr.w >> 4) & 0x0f0f0f0fu) | ((hdr.z >> 2) & 0x30303030u));
     const int sh = 16 * (q & 1);
-    const u32x2 w = *(const u32x2 *)(pc(1 + (g >> 1)) + 8 * (g & 1));
+    const u32x2 w = *(const u32x2 *)(wr + 16 + 32 * q + 8 * g);
     const h2 bias = splat(-1024.f);
 #pragma unroll
     for (int n = 0; n < 2; ++n) { // n = 0: low nibbles (sub-block 2q), 1: high (2q+1)
@@ -158,20 +138,20 @@ stage_frags_impl(PC pc, int g, int64_t c, f16x8 (&frag)[2])
     }
 }
 
-template <int F, class PC>
-__device__ __forceinline__ typename std::enable_if<F == Q6_K>::type
-stage_frags_impl(PC pc, int g, int64_t c, f16x8 (&frag)[2])
+// Q6_K sub-stage s4 = (h, v): k-step 0 = elements 128h+32v+[0,32) (ql[64h+32v..] low nibbles,
+// qh bits 2v), k-step 1 = 128h+64+32v+[0,32) (same ql bytes, high nibbles; qh bits 4+2v).
+template <>
+__device__ __forceinline__ void stage_frags<Q6_K>(const uint8_t *wr, int g, int s4, f16x8 (&frag)[2])
 {
-    const int h = (int)(c >> 1) & 1, v = (int)c & 1;
-    const float d = h2f(*(const uint16_t *)(pc(5) + 14));
-    const u32x2 ql = *(const u32x2 *)(pc(g >> 1) + 8 * (g & 1));
-    const u32x2 qh = *(const u32x2 *)(pc(2 + (g >> 1)) + 8 * (g & 1));
-    const uint8_t *scp = pc(4);
+    const int h = s4 >> 1, v = s4 & 1;
+    const float d = h2f(*(const uint16_t *)(wr + 208));
+    const u32x2 ql = *(const u32x2 *)(wr + 64 * h + 32 * v + 8 * g);
+    const u32x2 qh = *(const u32x2 *)(wr + 128 + 32 * h + 8 * g);
     const h2 bias = splat(-1056.f); // 1024 + 32
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
         // sub-block of elements 128h + 64n + 32v + 8g..: 8h + 4n + 2v + (g >> 1)
-        const float scv = (float)*(const int8_t *)(scp + 8 * h + 4 * n + 2 * v + (g >> 1));
+        const float scv = (float)*(const int8_t *)(wr + 192 + 8 * h + 4 * n + 2 * v + (g >> 1));
         const h2 dsc = splat(d * scv);
         const int sq = 4 * n + 2 * v;
         const uint32_t c0 = ((ql.x >> (4 * n)) & 0x0f0f0f0fu) | (((qh.x >> sq) & 0x03030303u) << 4);
@@ -181,28 +161,20 @@ stage_frags_impl(PC pc, int g, int64_t c, f16x8 (&frag)[2])
     }
 }
 
-template <int F, class PC>
-__device__ __forceinline__ typename std::enable_if<F == Q8_0>::type
-stage_frags_impl(PC pc, int g, int64_t /*c*/, f16x8 (&frag)[2])
+// Q8_0 sub-stage u: blocks 2u, 2u+1 of the stage's 8.
+template <>
+__device__ __forceinline__ void stage_frags<Q8_0>(const uint8_t *wr, int g, int u, f16x8 (&frag)[2])
 {
-    const uint8_t *wr = pc(0); // row-major: the row's 80 bytes
     const h2 bias = splat(-1152.f); // codes biased by +128 (xor 0x80)
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
-        const h2 d = splat(h2f(*(const uint16_t *)(wr + 34 * b)));
-        int x = 34 * b + 2 + 8 * g;
-        if (b == 1) x = x + 8 > 64 ? x + 12 : x;
-        const u32x2 q = *(const u32x2 *)(wr + x); // 2-byte aligned: gfx950 LDS runs unaligned
+        const uint8_t *blk = wr + 34 * (2 * u + b);
+        const h2 d = splat(h2f(*(const uint16_t *)blk));
+        const u32x2 q = *(const u32x2 *)(blk + 2 + 8 * g); // 2-byte aligned: gfx950 LDS runs unaligned
         const uint32_t c0 = q.x ^ 0x80808080u, c1 = q.y ^ 0x80808080u;
         frag[b] = frag4((pair02(c0) + bias) * d, (pair13(c0) + bias) * d, (pair02(c1) + bias) * d,
                         (pair13(c1) + bias) * d);
     }
-}
-
-template <int F, class PC>
-__device__ __forceinline__ void stage_frags(PC pc, int g, int64_t c, f16x8 (&frag)[2])
-{
-    stage_frags_impl<F>(pc, g, c, frag);
 }
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, uint8_t *lds_dst, uint32_t voff, uint32_t soff)
@@ -212,15 +184,29 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, uint8_t *lds_
 
 __device__ __forceinline__ int act_swz(int r) { return (r >> 1) & 7; }
 
+// Source of the padding DMAs that keep every wave's instruction count equal: the tensor's first
+// bytes (an L2 hit), written to a scratch slot.  (Out-of-range buffer offsets would return
+// zeros without a memory access, but they were measured to stall the issuing wave's vmcnt.)
+constexpr uint32_t DUMMY = 0u;
+
 // ---------------------------------------------------------------------------------------
+// Pipeline (per wave; a = activation sub-stage, w = a >> 2 = weight stage, NAS activation
+// slots, 3 weight slots):
+//   prologue  W(0) W(1) A(0) .. A(NAS-2)
+//   iteration a: wait until A(a) (and so W(a>>2)) landed -> barrier -> A(a+NAS-1) ->
+//                [a&3 == 0: W(w+2)] -> multiply sub-stage a from W slot w%3, A slot a%NAS.
+// vmcnt counts in issue order, so "A(a) landed" = all but the ops issued after it: the NAS-2
+// younger activation sub-stages and the W(.) issued in iterations a-NAS+1 .. a-1 with
+// index % 4 == 0 (after their A).  Past the end the indices are clamped (re-loads of identical
+// bytes into the same slot) so every wave issues the same sequence.
 // ABL: ablation bitmask for performance diagnosis (diagnostic build -DGQ_ABLATION only; 0 in
 // production): 1 = no MFMA, 2 = no weight DMA, 4 = no activation DMA, 8 = no dequantization.
-template <int F, int NB, int RG, int ABL = 0>
+template <int F, int NB, int ABL = 0>
 __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
                                                    uint16_t *__restrict__ C, float *__restrict__ P, int64_t M,
-                                                   int64_t N, int64_t K, int64_t ldc, int stages_per_split)
+                                                   int64_t N, int64_t K, int64_t ldc, int wstages_per_split)
 {
-    using G = Cfg<F, NB, RG>;
+    using G = Cfg<F, NB>;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[G::LDS_BYTES];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -228,144 +214,155 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
     const int g = lane >> 4, l16 = lane & 15;
     const int64_t m0 = (int64_t)blockIdx.x * G::BM;
     const int64_t n0 = (int64_t)blockIdx.y * G::BN;
-    const int64_t nstages = K / KC;
-    const int64_t c0 = (int64_t)blockIdx.z * stages_per_split;
-    const int64_t c1 = c0 + stages_per_split < nstages ? c0 + stages_per_split : nstages;
+    const int64_t nw_total = K / 256;
+    const int64_t w0 = (int64_t)blockIdx.z * wstages_per_split;
+    const int64_t w1 = w0 + wstages_per_split < nw_total ? w0 + wstages_per_split : nw_total;
     const int64_t row_bytes = (K / Layout<F>::QK) * Layout<F>::BYTES;
 
-    // buffer descriptors (byte offsets are 32-bit: tensors < 4 GiB, checked on the host)
-    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, (int)(uint32_t)(M * row_bytes),
-                                                                         0x00020000);
+    // buffer descriptors (byte offsets are 32-bit: tensors < 4 GiB, checked on the host).  The
+    // range check zeroes a whole 16-byte piece that crosses num_records, so the weight range is
+    // rounded up to 16 B: a Q6_K window's last piece may run past the tensor's last byte, but
+    // never past the 16-byte granule (hence never the page) that byte lives in.
+    const __amdgpu_buffer_rsrc_t wrs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, (int)(uint32_t)((M * row_bytes + 15) & ~(int64_t)15), 0x00020000);
     const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, (int)(uint32_t)(N * K * 2),
                                                                          0x00020000);
 
-    // this wave's DMA instructions k = wave + 8i: weights for k < W_INS, activations after;
-    // per instruction a fixed per-lane voffset, the stage part goes to soffset
-    uint32_t voff[G::MAXI];
-    int kj[G::MAXI]; // weight piece index j (K-quants) of the instruction
+    // weight DMA: instruction k = wave + 8i moves pieces p = 64k + lane: row p / NPW, piece p % NPW
+    uint32_t wv[G::NW];
+    int wpc[G::NW];
 #pragma unroll
-    for (int i = 0; i < G::MAXI; ++i) {
-        const int k = wave + NWAVE * i;
-        kj[i] = 0;
-        voff[i] = 0;
-        if (k < G::W_INS) {
-            if constexpr (F == Q8_0) {
-                const int p = 64 * k + lane, r = p / 5, j = p - 5 * r; // row-major pieces
-                const int64_t row = m0 + r < M ? m0 + r : M - 1;
-                voff[i] = (uint32_t)(row * row_bytes) + Stage<F>::piece_base(j);
-            } else {
-                constexpr int RBLK = G::BM / 64;
-                kj[i] = k / RBLK;
-                const int64_t r = m0 + 64 * (k - kj[i] * RBLK) + lane;
-                voff[i] = (uint32_t)((r < M ? r : M - 1) * row_bytes);
-            }
-        } else if (k < G::NI) {
-            const int p = 64 * (k - G::W_INS) + lane, r = p >> 3, q = p & 7;
-            const int64_t tok = n0 + r < N ? n0 + r : N - 1;
-            voff[i] = (uint32_t)(tok * K * 2) + Stage<F>::act_voff(q ^ act_swz(r));
-        }
+    for (int i = 0; i < G::NW; ++i) {
+        const int p = 64 * (wave + NWAVE * i) + lane, r = p / G::NPW;
+        wpc[i] = p - r * G::NPW;
+        const int64_t row = m0 + r < M ? m0 + r : M - 1;
+        wv[i] = r < G::BM ? (uint32_t)(row * row_bytes) : DUMMY;
     }
-    const int my_ins = G::MINI + (wave < G::NI % NWAVE ? 1 : 0);
-
-    auto issue = [&](int64_t c, int buf) {
-        uint8_t *base = lds + buf * G::STAGE_BYTES;
+    // activation DMA: instruction k moves pieces p = 64k + lane: token p >> 3, slot p & 7
+    uint32_t av[G::NA];
 #pragma unroll
-        for (int i = 0; i < G::MAXI; ++i) {
+    for (int i = 0; i < G::NA; ++i) {
+        const int p = 64 * (wave + NWAVE * i) + lane, r = p >> 3, q = p & 7;
+        const int64_t tok = n0 + r < N ? n0 + r : N - 1;
+        av[i] = r < G::BN ? (uint32_t)(tok * K * 2) + act_voff<F>(q ^ act_swz(r)) : DUMMY;
+    }
+    // the row this lane multiplies (for Q6_K's per-row window misalignment)
+    const int myrow = 16 * wave + l16;
+    const uint32_t myrow_off = (uint32_t)((m0 + myrow < M ? m0 + myrow : M - 1) * row_bytes);
+
+    auto issue_w = [&](int64_t w) {
+        if constexpr (ABL & 2) return;
+        uint8_t *dst = lds + (int)(w % NWS) * G::W_SLOT;
+#pragma unroll
+        for (int i = 0; i < G::NW; ++i) {
             const int k = wave + NWAVE * i;
-            if (k < G::W_INS) {
-                if constexpr (!(ABL & 2)) {
-                    uint32_t so;
-                    if constexpr (F == Q8_0) so = (uint32_t)(68 * c);
-                    else so = Stage<F>::soff(c, kj[i]);
-                    dma16(wrs, base + 1024 * k, voff[i], so);
-                }
-            } else if (k < G::NI) {
-                if constexpr (!(ABL & 4)) dma16(ars, base + 1024 * k, voff[i], Stage<F>::act_soff(c));
+            uint32_t vo, so;
+            if constexpr (F == Q6_K) { // 16-byte aligned window over the row's 210 bytes
+                vo = ((wv[i] + 210u * (uint32_t)w) & ~15u) + 16u * wpc[i];
+                so = 0;
+            } else {
+                vo = wv[i] + 16u * wpc[i];
+                so = (uint32_t)(WStage<F>::SB * w);
             }
+            dma16(wrs, k < G::W_REAL ? dst + 1024 * k : lds + G::SCRATCH, vo, so);
         }
     };
-    auto wait_stage = [&]() { // all but this wave's two youngest stages landed, then barrier
-        if constexpr (ABL & 6) {
-            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        } else if (my_ins == G::MAXI) {
-            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * G::MAXI) : "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * G::MINI) : "memory");
+    auto issue_a = [&](int64_t a) {
+        if constexpr (ABL & 4) return;
+        uint8_t *dst = lds + G::A_BASE + (int)(a % G::NAS) * G::A_SLOT;
+#pragma unroll
+        for (int i = 0; i < G::NA; ++i) {
+            const int k = wave + NWAVE * i;
+            dma16(ars, k < G::A_REAL ? dst + 1024 * k : lds + G::SCRATCH, av[i], act_soff<F>(a));
         }
     };
+    // vmcnt for "A(a) landed": (NAS-2) younger A's + the W's issued after A(a)
+    auto wait_a = [&](int s4) {
+        constexpr int na = ABL & 4 ? 0 : G::NA, nw = ABL & 2 ? 0 : G::NW; // (ablated streams issue nothing)
+        constexpr int base = (G::NAS - 2) * na;
+        bool w_after;
+        if constexpr (G::NAS == 4) w_after = s4 != 0;
+        else w_after = s4 == 1 || s4 == 2;
+        if constexpr ((ABL & 6) == 6) asm volatile("s_barrier" ::: "memory");
+        else if constexpr (ABL & 4) { // weights only: W(w) must land by sub-stage 4w
+            if (s4 == 0) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(nw) : "memory");
+            else asm volatile("s_barrier" ::: "memory");
+        } else if (w_after) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(base + nw) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(base) : "memory");
+    };
 
-    f32x4 acc[RG][NB];
+    f32x4 acc[NB];
 #pragma unroll
-    for (int rg = 0; rg < RG; ++rg)
-#pragma unroll
-        for (int t = 0; t < NB; ++t) acc[rg][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < NB; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-    if (c0 < c1) {
+    if (w0 < w1) {
+        const int64_t a0 = 4 * w0, a1 = 4 * w1;
+        issue_w(w0);
+        issue_w(w0 + 1 < w1 ? w0 + 1 : w1 - 1);
 #pragma unroll
-        for (int i = 0; i < NSTAGE - 1; ++i) issue(c0 + i < c1 ? c0 + i : c1 - 1, i);
-        int buf = 0;
-        for (int64_t c = c0; c < c1; ++c) {
-            // stage c landed (stages c+1, c+2 may still be in flight); all waves done with c-1
-            wait_stage();
-            issue(c + NSTAGE - 1 < c1 ? c + NSTAGE - 1 : c1 - 1, buf == 0 ? NSTAGE - 1 : buf - 1);
-            const uint8_t *ws = lds + buf * G::STAGE_BYTES;
-            const uint8_t *xs = ws + 1024 * G::W_INS;
-            f16x8 af[RG][2];
+        for (int i = 0; i < G::NAS - 1; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
+        for (int64_t a = a0; a < a1; ++a) {
+            const int s4 = (int)(a & 3);
+            wait_a(s4);
+            const int64_t w = a >> 2;
+            issue_a(a + G::NAS - 1 < a1 ? a + G::NAS - 1 : a1 - 1);
+            if (s4 == 0) issue_w(w + 2 < w1 ? w + 2 : w1 - 1);
+
+            const uint8_t *wr = lds + (int)(w % NWS) * G::W_SLOT + G::RBW * myrow;
+            if constexpr (F == Q6_K) wr += (myrow_off + 210u * (uint32_t)w) & 15u;
+            const uint8_t *xs = lds + G::A_BASE + (int)(a % G::NAS) * G::A_SLOT;
+            // all of the sub-stage's activation fragments first (one LDS round trip), the
+            // dequantization beside them, then the MFMAs
+            f16x8 bfr[2][NB];
 #pragma unroll
-            for (int rg = 0; rg < RG; ++rg) {
-                const int row = 16 * (RG * wave + rg) + l16;
-                if constexpr (ABL & 8) {
-                    af[rg][0] = *(const f16x8 *)(ws + 16 * row);
-                    af[rg][1] = *(const f16x8 *)(ws + 16 * row + 16 * G::BM);
-                } else if constexpr (F == Q8_0) {
-                    stage_frags<F>([&](int) { return ws + 80 * row; }, g, c, af[rg]);
-                } else {
-                    stage_frags<F>([&](int j) { return ws + 16 * (j * G::BM + row); }, g, c, af[rg]);
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int t = 0; t < NB; ++t) {
+                    const int r = 16 * t + l16;
+                    bfr[s][t] = *(const f16x8 *)(xs + 128 * r + 16 * ((4 * s + g) ^ act_swz(r)));
                 }
+            f16x8 af[2];
+            if constexpr (ABL & 8) {
+                af[0] = *(const f16x8 *)(wr + 0);
+                af[1] = *(const f16x8 *)(wr + 16);
+            } else {
+                stage_frags<F>(wr, g, s4, af);
             }
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
 #pragma unroll
                 for (int t = 0; t < NB; ++t) {
-                    const int r = 16 * t + l16;
-                    const f16x8 b = *(const f16x8 *)(xs + 128 * r + 16 * ((4 * s + g) ^ act_swz(r)));
-#pragma unroll
-                    for (int rg = 0; rg < RG; ++rg) {
-                        if constexpr (ABL & 1) acc[rg][t][0] += (float)af[rg][s][t & 7] * (float)b[rg & 7];
-                        else acc[rg][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[rg][s], b, acc[rg][t], 0, 0, 0);
-                    }
+                    if constexpr (ABL & 1) acc[t][0] += (float)af[s][t & 7] * (float)bfr[s][t][0];
+                    else acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s], bfr[s][t], acc[t], 0, 0, 0);
                 }
             }
-            buf = buf == NSTAGE - 1 ? 0 : buf + 1;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // no DMA may land after the workgroup exits
     }
 
-    // epilogue: acc[rg][t][i] = D[row 16(RG*wave+rg) + 4g + i][token 16t + l16]
+    // epilogue: acc[t][i] = D[row 16*wave + 4g + i][token 16t + l16]
+    const int64_t row = m0 + 16 * wave + 4 * g;
+    if (row >= M) return;
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
         const int64_t tok = n0 + 16 * t + l16;
         if (tok >= N) continue;
-#pragma unroll
-        for (int rg = 0; rg < RG; ++rg) {
-            const int64_t row = m0 + 16 * (RG * wave + rg) + 4 * g;
-            if (row >= M) continue;
-            const f32x4 v = acc[rg][t];
-            if (P == nullptr) {
-                uint16_t *dst = C + tok * ldc + row;
-                if (row + 4 <= M) {
-                    const u32x2 o = {(uint32_t)f2h_bits(v[0]) | ((uint32_t)f2h_bits(v[1]) << 16),
-                                     (uint32_t)f2h_bits(v[2]) | ((uint32_t)f2h_bits(v[3]) << 16)};
-                    *(u32x2 *)dst = o; // 2-byte aligned when ldc or M is odd: unaligned store
-                } else {
-                    for (int i = 0; i < 4 && row + i < M; ++i) dst[i] = f2h_bits(v[i]);
-                }
+        const f32x4 v = acc[t];
+        if (P == nullptr) {
+            uint16_t *dst = C + tok * ldc + row;
+            if (row + 4 <= M) {
+                const u32x2 o = {(uint32_t)f2h_bits(v[0]) | ((uint32_t)f2h_bits(v[1]) << 16),
+                                 (uint32_t)f2h_bits(v[2]) | ((uint32_t)f2h_bits(v[3]) << 16)};
+                *(u32x2 *)dst = o; // 2-byte aligned when ldc or M is odd: unaligned store
             } else {
-                float *dst = P + ((int64_t)blockIdx.z * N + tok) * M + row;
-                if (row + 4 <= M) *(f32x4 *)dst = v;
-                else
-                    for (int i = 0; i < 4 && row + i < M; ++i) dst[i] = v[i];
+                for (int i = 0; i < 4 && row + i < M; ++i) dst[i] = f2h_bits(v[i]);
             }
+        } else {
+            float *dst = P + ((int64_t)blockIdx.z * N + tok) * M + row;
+            if (row + 4 <= M) *(f32x4 *)dst = v;
+            else
+                for (int i = 0; i < 4 && row + i < M; ++i) dst[i] = v[i];
         }
     }
 }
@@ -382,27 +379,31 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restric
     C[tok * ldc + m] = f2h_bits(acc);
 }
 
-template <int F, int NB, int RG>
+template <int F, int NB>
 hipError_t launch_cfg(const uint8_t *A, const uint16_t *X, uint16_t *C, float *P, const GemmPlan &pl, int64_t M,
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
-    using G = Cfg<F, NB, RG>;
+    using G = Cfg<F, NB>;
     dim3 grid((unsigned)((M + G::BM - 1) / G::BM), (unsigned)((N + G::BN - 1) / G::BN), (unsigned)pl.splits);
     float *PP = pl.splits > 1 ? P : nullptr;
+    const int cps = pl.chunks_per_split;
 #ifdef GQ_ABLATION
     const int abl = getenv("GQ_ABLATE") ? atoi(getenv("GQ_ABLATE")) : 0;
     switch (abl) {
-    case 1: gemm_kernel<F, NB, RG, 1><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, pl.chunks_per_split); break;
-    case 2: gemm_kernel<F, NB, RG, 2><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, pl.chunks_per_split); break;
-    case 4: gemm_kernel<F, NB, RG, 4><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, pl.chunks_per_split); break;
-    case 6: gemm_kernel<F, NB, RG, 6><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, pl.chunks_per_split); break;
-    case 8: gemm_kernel<F, NB, RG, 8><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, pl.chunks_per_split); break;
-    case 9: gemm_kernel<F, NB, RG, 9><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, pl.chunks_per_split); break;
-    case 14: gemm_kernel<F, NB, RG, 14><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, pl.chunks_per_split); break;
-    default: gemm_kernel<F, NB, RG><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, pl.chunks_per_split); break;
+    case 1: gemm_kernel<F, NB, 1><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+    case 2: gemm_kernel<F, NB, 2><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+    case 4: gemm_kernel<F, NB, 4><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+    case 6: gemm_kernel<F, NB, 6><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+    case 8: gemm_kernel<F, NB, 8><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+    case 9: gemm_kernel<F, NB, 9><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+    case 12: gemm_kernel<F, NB, 12><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+    case 13: gemm_kernel<F, NB, 13><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+    case 15: gemm_kernel<F, NB, 15><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+    case 14: gemm_kernel<F, NB, 14><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+    default: gemm_kernel<F, NB><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
     }
 #else
-    gemm_kernel<F, NB, RG><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, pl.chunks_per_split);
+    gemm_kernel<F, NB><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps);
 #endif
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || pl.splits == 1) return e;
@@ -411,31 +412,23 @@ hipError_t launch_cfg(const uint8_t *A, const uint16_t *X, uint16_t *C, float *P
     return hipGetLastError();
 }
 
-template <int F, int RG>
-hipError_t launch_rg(const uint8_t *A, const uint16_t *X, uint16_t *C, float *P, const GemmPlan &pl, int64_t M,
-                     int64_t N, int64_t K, int64_t ldc, hipStream_t s)
-{
-    switch (pl.nb) {
-    case 1: return launch_cfg<F, 1, RG>(A, X, C, P, pl, M, N, K, ldc, s);
-    case 2: return launch_cfg<F, 2, RG>(A, X, C, P, pl, M, N, K, ldc, s);
-    case 4: return launch_cfg<F, 4, RG>(A, X, C, P, pl, M, N, K, ldc, s);
-    default: return launch_cfg<F, 8, RG>(A, X, C, P, pl, M, N, K, ldc, s);
-    }
-}
-
 template <int F>
 hipError_t launch_fmt(const uint8_t *A, const uint16_t *X, uint16_t *C, float *P, const GemmPlan &pl, int64_t M,
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
-    if (pl.rg == 1) return launch_rg<F, 1>(A, X, C, P, pl, M, N, K, ldc, s);
-    return launch_rg<F, 2>(A, X, C, P, pl, M, N, K, ldc, s);
+    switch (pl.nb) {
+    case 1: return launch_cfg<F, 1>(A, X, C, P, pl, M, N, K, ldc, s);
+    case 2: return launch_cfg<F, 2>(A, X, C, P, pl, M, N, K, ldc, s);
+    case 4: return launch_cfg<F, 4>(A, X, C, P, pl, M, N, K, ldc, s);
+    default: return launch_cfg<F, 8>(A, X, C, P, pl, M, N, K, ldc, s);
+    }
 }
 
 int pick_nb(int64_t N) { return N > 64 ? 8 : (N > 32 ? 4 : (N > 16 ? 2 : 1)); }
 
 } // namespace
 
-bool gemm_supported(int /*fmt*/, int64_t K) { return K > 0 && K % KC == 0; }
+bool gemm_supported(int /*fmt*/, int64_t K) { return K > 0 && K % 256 == 0; }
 
 GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K)
 {
@@ -443,21 +436,17 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K)
     GemmPlan p;
     p.nb = pick_nb(N);
     if (const char *env = getenv("GQ_GEMM_NB")) p.nb = atoi(env);
-    const int64_t nstages = K / KC;
-    const int64_t tn = (N + 16 * p.nb - 1) / (16 * p.nb);
+    p.rg = 1;
+    const int64_t nws = K / 256; // weight stages (super-blocks)
+    const int64_t tiles = ((M + 127) / 128) * ((N + 16 * p.nb - 1) / (16 * p.nb));
     const int64_t target = 256; // one workgroup per CU
-    // rows per workgroup: 256 (the activation tile is re-read once per 256 weight rows);
-    // 128 only when even split-K cannot fill the chip
-    const int64_t max_split = nstages / 16 > 0 ? nstages / 16 : 1; // >= 16 stages per split
-    p.rg = ((M + 255) / 256) * tn * max_split < target ? 1 : 2;
-    if (const char *env = getenv("GQ_GEMM_RG")) p.rg = atoi(env) == 1 ? 1 : 2;
-    const int64_t tiles = ((M + 128 * p.rg - 1) / (128 * p.rg)) * tn;
     int64_t S = tiles >= target ? 1 : (target + tiles / 2) / tiles;
     if (const char *env = getenv("GQ_GEMM_SPLITS")) S = atoll(env); // tuning / test override
+    const int64_t max_split = nws / 2 > 0 ? nws / 2 : 1;            // >= 2 super-blocks per split
     if (S > max_split) S = max_split;
     if (S < 1) S = 1;
-    int64_t sps = (nstages + S - 1) / S;
-    S = (nstages + sps - 1) / sps;
+    int64_t sps = (nws + S - 1) / S;
+    S = (nws + sps - 1) / sps;
     p.splits = (int)S;
     p.chunks_per_split = (int)sps;
     p.partial_bytes = S > 1 ? (size_t)S * N * M * sizeof(float) : 0;

@@ -2,6 +2,7 @@
 activations prepared once) for bench.py configs under env overrides.
 
 Usage: python tools/gemm_tune.py [--abl] CONFIG[:ENV=V,ENV=V...] ...
+  CONFIG: a bench.py config name or fmt_MxK_mN (e.g. q4_k_28672x8192_m128)
   --abl   load build/abl/libgguf_mmq_abl.so (make -C gguf-triton-kernel_amd abl) so that
           GQ_ABLATE=<mask> selects the ablation variants of mmq_gemm.hip.
 """
@@ -29,7 +30,13 @@ for spec in args:
     for kv in filter(None, envs.split(",")):
         k, v = kv.split("=")
         os.environ[k] = v
-    fmt, M, K, N = bench.CONFIGS[cfg]
+    if cfg in bench.CONFIGS:
+        fmt, M, K, N = bench.CONFIGS[cfg]
+    else:  # fmt_MxK_mN, e.g. q4_k_28672x8192_m128
+        fmt = cfg[:4]
+        mk, n = cfg[5:].split("_m")
+        M, K = map(int, mk.split("x"))
+        N = int(n)
     r = bench.Runner(fmt, M, K, N, dev, 40)
     r.prepare()
     g = r.capture(r.kernel, 40)
