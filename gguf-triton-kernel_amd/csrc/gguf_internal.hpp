@@ -16,9 +16,9 @@ hipError_t launch_act_quant(int mode, const uint16_t *X, int64_t ldx, int64_t ro
 hipError_t launch_gemv(int fmt, const uint8_t *A, const int8_t *xq, const float *xd, const float *xs, uint16_t *C,
                        int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
 
-// Fused decode (mmq_gemv.hip): q8_1 quantization of the N <= 8 tokens in LDS + GEMV, one
-// launch.  decode_fused_ok() says whether the LDS image fits (else: act_quant + launch_gemv).
-size_t decode_lds_bytes(int fmt, int nt, int64_t K);
+// Streaming decode (mmq_decode.hip): q8_1 quantization of the N <= 8 tokens in LDS + the
+// weight stream, one launch.  decode_fused_ok() says whether the LDS image fits (else:
+// act_quant + launch_gemv).
 bool decode_fused_ok(int fmt, int64_t N, int64_t K);
 hipError_t launch_decode_fused(int fmt, const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, int64_t M,
                                int64_t N, int64_t K, int64_t ldc, hipStream_t s);

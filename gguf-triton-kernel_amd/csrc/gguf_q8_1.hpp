@@ -15,6 +15,7 @@ struct Q81Lane {
     uint32_t codes; // this lane's 4 int8 codes, little endian
     float d;        // block scale (fp16 value)
     uint16_t dbits, sbits;
+    int s4;         // (decode quantizer only) sum of the codes of this lane's quad
 };
 
 __device__ __forceinline__ Q81Lane q8_1_lane(uint32_t w0, uint32_t w1)

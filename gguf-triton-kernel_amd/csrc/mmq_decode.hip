@@ -1,0 +1,551 @@
+// mmq_decode.hip -- the decode-shaped MMQ (N_tok <= 8): one launch that streams the weight
+// matrix once from HBM at the stream rate.
+//
+// C[t][m] = sum_k W[m][k] * q8_1(x)[t][k] for the NT tokens of blockIdx.y, with the reference's
+// per-block arithmetic (gguf_dot.hpp; kernels/cpu_impls/mmq_*_q8_1_cpu.py) and exact int32
+// dot products.
+//
+// Weight stream.  Every wave owns a contiguous range of weight rows, i.e. a contiguous byte
+// range of the packed tensor, cut into "tasks" of at most NI KiB: G whole rows when a row fits,
+// else a row segment of whole 64-element units.  A task is moved HBM -> LDS by NI LDS-DMA
+// instructions (buffer_load_dwordx4 ... lds: one 1 KiB fully coalesced line run per wave
+// instruction, nothing through VGPRs) from the 16-byte aligned window around it, into the
+// wave's private ring of S slots; S-1 tasks are in flight while one is multiplied.  The ring is
+// private, so a wave waits only on its own counted vmcnt -- no workgroup barrier in the loop.
+//
+// Activations.  The NT tokens are quantized to q8_1 (gguf_q8_1.hpp, bit-exact with
+// utils/quantize/q8_1.py) straight into LDS: the fp16 rows are LDS-DMA'd into each wave's
+// last ring slot FIRST (so waiting for them does not wait for the weight DMAs issued behind
+// them), quantized by the wave that staged them, and shared by one barrier.
+//
+// Multiply.  Lane l takes unit u = l % P + P*i of a row (P = 64, or the power of two >= the
+// units per row for short rows, several rows per wave pass); it reads the unit's packed bytes
+// and its activation block pair from LDS, dots them with v_dot4_i32_i8, and P-lane xor
+// shuffles reduce the row.
+#include <cstdlib>
+
+#include "gguf_blocks.hpp"
+#include "gguf_dot.hpp"
+#include "gguf_internal.hpp"
+#include "gguf_q8_1.hpp"
+#include "gguf_units.hpp"
+
+#ifndef GQ_DECODE_NT
+#define GQ_DECODE_NT 1 // weight DMAs with the non-temporal policy (bytes read exactly once)
+#endif
+
+namespace gq {
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int DW = 8; // waves per workgroup (two per SIMD)
+#ifndef GQ_DECODE_NI
+#define GQ_DECODE_NI 7
+#endif
+#ifndef GQ_DECODE_NS
+#define GQ_DECODE_NS 2
+#endif
+constexpr int NI = GQ_DECODE_NI; // KiB (DMA instructions) per task
+constexpr int NS = GQ_DECODE_NS; // ring slots per wave: NS-1 tasks in flight while one is multiplied
+constexpr int SLOT = NI * 1024;
+constexpr int RING = DW * NS * SLOT;
+constexpr int LDS_CAP = 160 * 1024;
+
+struct DecodeGeom {
+    int ngroups; // row groups (nseg == 1) or rows (nseg > 1)
+    int G;       // rows per group (nseg == 1)
+    int nseg;    // segments per row
+    int segu;    // units per segment (nseg > 1; a multiple of 64)
+    int lp2;     // log2(P): lanes per row
+};
+
+// byte offset of unit u (64 elements) within a row
+template <int F>
+__device__ __forceinline__ uint32_t unit_byte(int u, int nb32)
+{
+    if constexpr (F == Q8_0) return 34u * (uint32_t)(2 * u < nb32 ? 2 * u : nb32);
+    return (uint32_t)Layout<F>::BYTES * (uint32_t)(u >> 2);
+}
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, uint8_t *lds, uint32_t voff)
+{
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void *)lds, 16, voff, 0, 0, GQ_DECODE_NT ? 2 : 0);
+}
+__device__ __forceinline__ void dma16x(__amdgpu_buffer_rsrc_t r, uint8_t *lds, uint32_t voff)
+{
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void *)lds, 16, voff, 0, 0, 0);
+}
+
+#define GQ_DPP(v, ctrl) __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), ctrl, 0xf, 0xf, false))
+#define GQ_DPPI(v, ctrl) __builtin_amdgcn_mov_dpp(v, ctrl, 0xf, 0xf, false)
+__device__ __forceinline__ float wave_sum_dpp(float v)
+{
+    v += GQ_DPP(v, 0xb1);  // quad_perm [1,0,3,2]
+    v += GQ_DPP(v, 0x4e);  // quad_perm [2,3,0,1]
+    v += GQ_DPP(v, 0x124); // row_ror:4
+    v += GQ_DPP(v, 0x128); // row_ror:8
+    const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+    const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
+    const float c = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+    const float d = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+    return (a + b) + (c + d);
+}
+
+// The unit's activations for NT tokens from the LDS image (codes swizzled as swz_piece<F>;
+// d, Q4_K s and Q6_K per-16 code sums precomputed by the quantizer).
+template <int F, int NT>
+__device__ __forceinline__ void act_from_lds(Act<F, NT> &a, const uint8_t *codes, const float *sd, const float *sx,
+                                             int kp, int nb, int u)
+{
+    int b0, b1;
+    act_blocks<F>(u, b0, b1);
+    const bool has1 = b1 < nb;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const uint8_t *row = codes + t * kp;
+        const u32x4 c0 = *(const u32x4 *)(row + 16 * swz_piece<F>(2 * b0));
+        const u32x4 c1 = *(const u32x4 *)(row + 16 * swz_piece<F>(2 * b0 + 1));
+        u32x4 c2 = {0, 0, 0, 0}, c3 = {0, 0, 0, 0};
+        if (has1) {
+            c2 = *(const u32x4 *)(row + 16 * swz_piece<F>(2 * b1));
+            c3 = *(const u32x4 *)(row + 16 * swz_piece<F>(2 * b1 + 1));
+        }
+        a.q[t][0] = c0.x; a.q[t][1] = c0.y; a.q[t][2] = c0.z; a.q[t][3] = c0.w;
+        a.q[t][4] = c1.x; a.q[t][5] = c1.y; a.q[t][6] = c1.z; a.q[t][7] = c1.w;
+        a.q[t][8] = c2.x; a.q[t][9] = c2.y; a.q[t][10] = c2.z; a.q[t][11] = c2.w;
+        a.q[t][12] = c3.x; a.q[t][13] = c3.y; a.q[t][14] = c3.z; a.q[t][15] = c3.w;
+        a.d[t][0] = sd[t * nb + b0];
+        a.d[t][1] = has1 ? sd[t * nb + b1] : 0.f;
+        if constexpr (F == Q4_K) {
+            a.s[t][0] = sx[t * nb + b0];
+            a.s[t][1] = has1 ? sx[t * nb + b1] : 0.f;
+        }
+        if constexpr (F == Q6_K) { // int32 code sums of the 16-element halves: [t][2*b + h]
+            const int *sm = (const int *)sx + t * 2 * nb;
+            const u32x2 s0 = *(const u32x2 *)(sm + 2 * b0);
+            const u32x2 s1 = has1 ? *(const u32x2 *)(sm + 2 * b1) : (u32x2){0, 0};
+            a.sum[t][0] = (int)s0.x; a.sum[t][1] = (int)s0.y;
+            a.sum[t][2] = (int)s1.x; a.sum[t][3] = (int)s1.y;
+        }
+    }
+}
+
+// q8_1 of one 32-element block held by an aligned group of 8 lanes (4 elements each): the
+// arithmetic of gguf_q8_1.hpp (bit-exact with utils/quantize/q8_1.py), with the group
+// reductions on DPP quad permutes + one ds_swizzle (xor 4) instead of LDS permutes.
+__device__ __forceinline__ Q81Lane q8_1_lane_dpp(uint32_t w0, uint32_t w1)
+{
+    const float x[4] = {h2f(w0 & 0xffff), h2f(w0 >> 16), h2f(w1 & 0xffff), h2f(w1 >> 16)};
+    float amax = fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3])));
+    amax = fmaxf(amax, GQ_DPP(amax, 0xb1));
+    amax = fmaxf(amax, GQ_DPP(amax, 0x4e));
+    amax = fmaxf(amax, __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, amax), 0x101f)));
+    Q81Lane r;
+    r.dbits = amax != 0.f ? f2h_bits(amax / 127.0f) : (uint16_t)0;
+    r.d = h2f(r.dbits);
+    const float div = r.d == 0.f ? 1.0f : r.d;
+    int sum = 0;
+    r.codes = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float q = __builtin_rintf(h2f(f2h_bits(x[i] / div)));
+        q = fminf(127.f, fmaxf(-127.f, q));
+        const int qi = (int)q;
+        sum += qi;
+        r.codes |= (uint32_t)(qi & 0xff) << (8 * i);
+    }
+    sum += GQ_DPPI(sum, 0xb1);
+    sum += GQ_DPPI(sum, 0x4e);
+    r.s4 = sum; // sum over this lane's quad (Q6_K: quads 0 and 1 = the 16-element halves)
+    sum += __builtin_amdgcn_ds_swizzle(sum, 0x101f);
+    r.sbits = f2h_bits(r.d * h2f(f2h_bits((float)sum)));
+    return r;
+}
+
+// ITC > 0: the lane's activations for its units u = (lane % P) + P*i, i < ITC, are loaded from
+// the LDS image once and kept in registers (every row multiplies the same units); ITC == 0:
+// read from LDS per unit.
+template <int F, int NT, int ITC>
+__global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *__restrict__ A,
+                                                                const uint16_t *__restrict__ X, int64_t ldx,
+                                                                uint16_t *__restrict__ C, int M, int64_t N, int K,
+                                                                int64_t ldc, DecodeGeom geo)
+{
+    using L = Layout<F>;
+    extern __shared__ __attribute__((aligned(1024))) uint8_t smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t tok0 = (int64_t)blockIdx.y * NT;
+    const int nb = K / 32;
+    const int kp = (K + 63) / 64 * 64;
+    const uint32_t RB = (uint32_t)(K / L::QK) * L::BYTES;
+    const int upr = (K + 63) / 64;
+    uint8_t *ring = smem + wave * (NS * SLOT);
+    uint8_t *codes = smem + RING;
+    float *sd = (float *)(codes + NT * kp);
+    float *sx = sd + NT * nb; // Q4_K: s [NT][nb] (float); Q6_K: code sums [NT][2*nb] (int)
+
+    const __amdgpu_buffer_rsrc_t wrs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, (int)(((uint32_t)M * RB + 15u) & ~15u), 0x00020000);
+
+    // this wave's contiguous range of row groups, and its task count
+    const int W = (int)gridDim.x * DW;
+    const int gw = (int)blockIdx.x * DW + wave;
+    const int per = geo.ngroups / W, rem = geo.ngroups % W;
+    const int g_begin = gw * per + (gw < rem ? gw : rem);
+    const int ntask = (per + (gw < rem ? 1 : 0)) * geo.nseg;
+
+    // task = (row group g, segment s); cursors advance without divisions
+    auto window = [&](int g, int s, uint32_t &start, uint32_t &len) {
+        if (geo.nseg == 1) {
+            const int r0 = g * geo.G;
+            const int rows = M - r0 < geo.G ? M - r0 : geo.G;
+            start = (uint32_t)r0 * RB;
+            len = (uint32_t)rows * RB;
+        } else {
+            const int u0 = s * geo.segu;
+            const int u1 = u0 + geo.segu < upr ? u0 + geo.segu : upr;
+            start = (uint32_t)g * RB + unit_byte<F>(u0, nb);
+            len = unit_byte<F>(u1, nb) - unit_byte<F>(u0, nb);
+        }
+    };
+    auto next = [&](int &g, int &s) {
+        if (++s == geo.nseg) {
+            s = 0;
+            ++g;
+        }
+    };
+    int gi = g_begin, si = 0; // next task to issue
+    auto issue = [&](int j) {
+        uint32_t st, len;
+        window(gi, si, st, len);
+        next(gi, si);
+        const uint32_t ws = st & ~15u, we = st + len;
+        uint8_t *dst = ring + (j % NS) * SLOT;
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            uint32_t o = ws + 1024u * k + 16u * lane;
+            if (o >= we) o = ws; // past the window: re-read its first line (L2 hit), never past the tensor
+            dma16(wrs, dst + 1024 * k, o);
+        }
+    };
+
+    // ---- prologue: stage the fp16 activations (round 0) first, then the first NS-1 tasks ----
+    // Activation blocks (32 elements of one token) are dealt to waves round-robin; a wave stages
+    // NI*16 blocks per round in its last ring slot (4 lanes x 16 B per block) and quantizes them
+    // with 8 lanes per block, two blocks per lane group in flight.
+    const int xblocks = NT * nb;
+    constexpr int WBLK = NI * 16; // blocks per wave per round
+    const int rounds = (xblocks + DW * WBLK - 1) / (DW * WBLK);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, 0x7fffffff, 0x00020000);
+    uint8_t *xslot = ring + (NS - 1) * SLOT;
+    auto xblock = [&](int r, int lb) { return (r * WBLK + lb) * DW + wave; }; // global block of local block lb
+    auto issue_x = [&](int r) {
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            const int lb = 16 * k + (lane >> 2);
+            int b = xblock(r, lb);
+            if (b >= xblocks) b = 0;
+            const int t = b / nb, j = b - t * nb;
+            const int64_t tok = tok0 + t < N ? tok0 + t : N - 1;
+            dma16x(xrs, xslot + 1024 * k, (uint32_t)((tok * ldx + 32 * j + 8 * (lane & 3)) * 2));
+        }
+    };
+    auto store_q = [&](int r, int lb, const Q81Lane &qq) {
+        const int b = xblock(r, lb), t = b / nb, j = b - t * nb;
+        const int k = 32 * j + 4 * (lane & 7);
+        *(uint32_t *)(codes + t * kp + 16 * swz_piece<F>(k >> 4) + (k & 15)) = qq.codes;
+        if constexpr (F == Q6_K)
+            if ((lane & 3) == 0) ((int *)sx)[t * 2 * nb + 2 * j + ((lane >> 2) & 1)] = qq.s4;
+        if ((lane & 7) == 0) {
+            sd[t * nb + j] = qq.d;
+            if constexpr (F == Q4_K) sx[t * nb + j] = h2f(qq.sbits);
+        }
+    };
+    auto quantize = [&](int r) {
+        int nblk = xblocks - r * WBLK * DW - wave; // blocks of this wave in this round
+        nblk = nblk > 0 ? (nblk + DW - 1) / DW : 0;
+        if (nblk > WBLK) nblk = WBLK;
+        for (int lb0 = 0; lb0 < nblk; lb0 += 16) { // two passes of 8 blocks (8 lanes per block)
+            const int lb1 = lb0 + (lane >> 3), lb2 = lb1 + 8;
+            const u32x2 v1 = *(const u32x2 *)(xslot + 64 * lb1 + 8 * (lane & 7));
+            const u32x2 v2 = *(const u32x2 *)(xslot + 64 * (lb2 < WBLK ? lb2 : lb1) + 8 * (lane & 7));
+            const Q81Lane q1 = q8_1_lane_dpp(v1.x, v1.y);
+            const Q81Lane q2 = q8_1_lane_dpp(v2.x, v2.y);
+            if (lb1 < nblk) store_q(r, lb1, q1);
+            if (lb2 < nblk) store_q(r, lb2, q2);
+        }
+    };
+
+    issue_x(0);
+#pragma unroll
+    for (int j = 0; j < NS - 1; ++j)
+        if (j < ntask) issue(j);
+    int gc = g_begin, sc = 0; // task being multiplied
+    // X round 0 = the oldest NI DMAs; the younger ones are the weight tasks just issued
+    if (ntask >= NS - 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 1) * NI) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifndef GQ_ABL_NOQUANT
+    quantize(0);
+#endif
+    for (int r = 1; r < rounds; ++r) { // long activations: further rounds, full waits
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        issue_x(r);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        quantize(r);
+    }
+    __syncthreads();
+
+    // ---- main loop ----
+    const int P = 1 << geo.lp2;
+    const int lrow = lane >> geo.lp2, lunit = lane & (P - 1);
+    const int ntok = N - tok0 < NT ? (int)(N - tok0) : NT;
+    Act<F, NT> ca[ITC > 0 ? ITC : 1];
+    if constexpr (ITC > 0) {
+#pragma unroll
+        for (int i = 0; i < ITC; ++i) {
+            const int u = lunit + P * i;
+            act_from_lds<F, NT>(ca[i], codes, sd, sx, kp, nb, u < upr ? u : upr - 1);
+        }
+    }
+    float acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = 0.f;
+
+    // the contribution of unit u (activation slot i when cached) of the row at rowp
+    auto unit = [&](const uint8_t *rowp, int u, int i) {
+        UnitLoad<F> l;
+#ifdef GQ_ABL_NOWLDS
+        __builtin_memset(&l, 0, sizeof(l));
+        ((uint32_t *)&l)[0] = (uint32_t)(uintptr_t)rowp + u;
+        ((uint32_t *)&l)[3] = (uint32_t)u * 77u;
+#else
+        l.load(rowp, u, nb);
+#endif
+#ifdef GQ_ABL_NODOT
+        const uint32_t *w = (const uint32_t *)&l;
+        uint32_t x = 0;
+        for (int q = 0; q < (int)(sizeof(l) / 4); ++q) x ^= w[q];
+        acc[0] += (float)x;
+        return;
+#endif
+        if constexpr (ITC > 0) {
+            dot_unit<F, NT>(UnitRaw<F>::from(l, u, nb), ca[i], acc);
+        } else {
+            Act<F, NT> a;
+            act_from_lds<F, NT>(a, codes, sd, sx, kp, nb, u);
+            dot_unit<F, NT>(UnitRaw<F>::from(l, u, nb), a, acc);
+        }
+    };
+
+    for (int j = 0; j < ntask; ++j) {
+        if (j + NS - 2 < ntask) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * NI) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (j + NS - 1 < ntask) issue(j + NS - 1);
+
+        uint32_t st, len;
+        const int g = gc, s = sc;
+        window(g, s, st, len);
+        next(gc, sc);
+        const uint8_t *base = ring + (j % NS) * SLOT + (st & 15u);
+#ifdef GQ_ABL_NOCOMP
+        acc[0] += (float)base[lane];
+        if (j == ntask - 1 && acc[0] == 1234.5f) C[0] = 0;
+        continue;
+#endif
+        if (geo.nseg == 1) {
+            const int r0 = g * geo.G;
+            const int nr = M - r0 < geo.G ? M - r0 : geo.G;
+            for (int rp = 0; rp < nr; rp += 64 >> geo.lp2) {
+                const int r = rp + lrow;
+                const bool valid = r < nr;
+                const uint8_t *rowp = base + (uint32_t)(valid ? r : 0) * RB;
+                if constexpr (ITC > 0) {
+#pragma unroll
+                    for (int i = 0; i < ITC; ++i) {
+                        const int u = lunit + P * i;
+                        if (valid && u < upr) unit(rowp, u, i);
+                    }
+                } else {
+                    for (int u = lunit; u < upr; u += P)
+                        if (valid) unit(rowp, u, 0);
+                }
+                if (P == 64) {
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) {
+                        const float v = wave_sum_dpp(acc[t]);
+                        acc[t] = 0.f;
+                        if (lane == 0 && t < ntok) C[(tok0 + t) * ldc + r0 + r] = f2h_bits(v);
+                    }
+                } else {
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) {
+                        float v = acc[t];
+                        for (int off = P >> 1; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+                        acc[t] = 0.f;
+                        if (lunit == 0 && valid && t < ntok) C[(tok0 + t) * ldc + r0 + r] = f2h_bits(v);
+                    }
+                }
+            }
+        } else {
+            const int u0 = s * geo.segu, u1 = u0 + geo.segu;
+            const uint8_t *rowp = base - unit_byte<F>(u0, nb);
+            if constexpr (ITC > 0) {
+#pragma unroll
+                for (int i = 0; i < ITC; ++i) {
+                    const int u = lane + 64 * i;
+                    if (u >= u0 && u < u1 && u < upr) unit(rowp, u, i);
+                }
+            } else {
+                for (int u = u0 + lane; u < u1; u += 64)
+                    if (u < upr) unit(rowp, u, 0);
+            }
+            if (s == geo.nseg - 1) {
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    const float v = wave_sum_dpp(acc[t]);
+                    acc[t] = 0.f;
+                    if (lane == 0 && t < ntok) C[(tok0 + t) * ldc + g] = f2h_bits(v);
+                }
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // no DMA may land after the wave exits
+}
+
+struct Pick {
+    int nt, itc;
+    size_t lds;
+    DecodeGeom geo;
+    int grid;
+};
+
+size_t act_lds(int fmt, int nt, int64_t K)
+{
+    const int64_t kp = (K + 63) / 64 * 64, nb = K / 32;
+    return (size_t)nt * kp + (size_t)nt * nb * 4 * (fmt == Q8_0 ? 1 : (fmt == Q4_K ? 2 : 3));
+}
+
+int64_t row_bytes(int fmt, int64_t K)
+{
+    return fmt == Q8_0 ? K / 32 * 34 : (fmt == Q4_K ? K / 256 * 144 : K / 256 * 210);
+}
+
+bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p)
+{
+    const int nts[4] = {1, 2, 4, 8};
+    p.nt = 8;
+    for (int i = 0; i < 4; ++i)
+        if (nts[i] >= N) { p.nt = nts[i]; break; }
+    while ((size_t)RING + act_lds(fmt, p.nt, K) > (size_t)LDS_CAP) {
+        if (p.nt == 1) return false;
+        p.nt >>= 1;
+    }
+    p.lds = (size_t)RING + act_lds(fmt, p.nt, K);
+    const int64_t RB = row_bytes(fmt, K);
+    const int64_t upr = (K + 63) / 64;
+    const int64_t cap = NI * 1024 - 16;
+    const int per_cu = (int)(LDS_CAP / p.lds) > 0 ? (int)(LDS_CAP / p.lds) : 1;
+    const int64_t W = (int64_t)256 * per_cu * DW; // waves the chip holds
+    DecodeGeom &g = p.geo;
+    if (RB <= cap) {
+        const int64_t gmax = cap / RB;
+        const int64_t groups_min = (M + gmax - 1) / gmax;
+        const int64_t tpw = (groups_min + W - 1) / W;     // tasks per wave at the largest groups
+        int64_t G = (M + W * tpw - 1) / (W * tpw);       // smallest groups with that many tasks
+        if (G < 1) G = 1;
+        if (G > gmax) G = gmax;
+        g.G = (int)G;
+        g.nseg = 1;
+        g.segu = (int)upr;
+        g.ngroups = (int)((M + G - 1) / G);
+        int lp2 = 0;
+        while ((1 << lp2) < upr && lp2 < 6) ++lp2;
+        g.lp2 = lp2;
+    } else {
+        const int64_t unit64 = fmt == Q8_0 ? 64 * 68 : (fmt == Q4_K ? 64 * 36 : 64 * 210 / 4);
+        g.G = 1;
+        g.segu = (int)(64 * (cap / unit64));
+        g.nseg = (int)((upr + g.segu - 1) / g.segu);
+        g.ngroups = (int)M;
+        g.lp2 = 6;
+    }
+    // activations cached in registers: at most 4 units per lane and 2 tokens
+    const int64_t itc = (upr + (1 << g.lp2) - 1) >> g.lp2;
+    p.itc = (p.nt <= 2 && itc <= 4) ? (int)itc : 0;
+    const int64_t waves = g.ngroups < W ? g.ngroups : W;
+    p.grid = (int)((waves + DW - 1) / DW);
+    return true;
+}
+
+template <int F, int NT, int ITC>
+hipError_t launch_t(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, int64_t M, int64_t N, int64_t K,
+                    int64_t ldc, const Pick &p, hipStream_t s)
+{
+    static bool attr = false; // raise the dynamic LDS limit once per instantiation
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void *)stream_decode_kernel<F, NT, ITC>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, LDS_CAP);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    dim3 grid((unsigned)p.grid, (unsigned)((N + NT - 1) / NT)), block(DW * 64);
+    stream_decode_kernel<F, NT, ITC><<<grid, block, p.lds, s>>>(A, X, ldx, C, (int)M, N, (int)K, ldc, p.geo);
+    return hipGetLastError();
+}
+
+template <int F>
+hipError_t launch_f(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, int64_t M, int64_t N, int64_t K,
+                    int64_t ldc, const Pick &p, hipStream_t s)
+{
+#define GQ_LT(nt, itc) launch_t<F, nt, itc>(A, X, ldx, C, M, N, K, ldc, p, s)
+    switch (p.nt * 8 + p.itc) {
+    case 8: return GQ_LT(1, 0);
+    case 9: return GQ_LT(1, 1);
+    case 10: return GQ_LT(1, 2);
+    case 11: return GQ_LT(1, 3);
+    case 12: return GQ_LT(1, 4);
+    case 16: return GQ_LT(2, 0);
+    case 17: return GQ_LT(2, 1);
+    case 18: return GQ_LT(2, 2);
+    case 19: return GQ_LT(2, 3);
+    case 20: return GQ_LT(2, 4);
+    case 32: return GQ_LT(4, 0);
+    default: return GQ_LT(8, 0);
+    }
+#undef GQ_LT
+    return hipErrorInvalidValue;
+}
+
+} // namespace
+
+bool decode_fused_ok(int fmt, int64_t N, int64_t K)
+{
+    Pick p;
+    // 32-bit buffer offsets: the packed tensor must stay below 2 GiB (the C ABI splits larger ones)
+    return N <= 8 && pick(fmt, 1, N, K, p);
+}
+
+hipError_t launch_decode_fused(int fmt, const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, int64_t M,
+                               int64_t N, int64_t K, int64_t ldc, hipStream_t s)
+{
+    const int64_t RB = row_bytes(fmt, K);
+    const int64_t max_rows = ((int64_t)1 << 31) / RB - 1; // rows per launch under 2 GiB
+    for (int64_t m0 = 0; m0 < M; m0 += max_rows) {
+        const int64_t m = M - m0 < max_rows ? M - m0 : max_rows;
+        Pick p;
+        if (!pick(fmt, m, N, K, p)) return hipErrorInvalidValue;
+        hipError_t e;
+        switch (fmt) {
+        case Q8_0: e = launch_f<Q8_0>(A + m0 * RB, X, ldx, C + m0, m, N, K, ldc, p, s); break;
+        case Q4_K: e = launch_f<Q4_K>(A + m0 * RB, X, ldx, C + m0, m, N, K, ldc, p, s); break;
+        default: e = launch_f<Q6_K>(A + m0 * RB, X, ldx, C + m0, m, N, K, ldc, p, s); break;
+        }
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+} // namespace gq

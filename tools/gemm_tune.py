@@ -14,6 +14,12 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "gguf-triton-kernel_amd")]
 import kernels._lib as kl  # noqa: E402
 
 args = sys.argv[1:]
+STEP = "--step" in args  # time the whole drop-in step (gq_mmq: fused decode / act quant + GEMM)
+args = [a for a in args if a != "--step"]
+for a in list(args):
+    if a.startswith("--lib="):  # a diagnostic build of libgguf_mmq.so (never the product)
+        kl.LIB_PATH = os.path.abspath(a[6:])
+        args.remove(a)
 if args and args[0] == "--abl":
     kl.LIB_PATH = os.path.join(ROOT, "gguf-triton-kernel_amd", "lib", "libgguf_mmq_abl.so")
     args = args[1:]
@@ -22,7 +28,7 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 
 dev = torch.device("cuda:0")
-KEYS = ("GQ_ABLATE", "GQ_GEMM_RG", "GQ_GEMM_NB", "GQ_GEMM_SPLITS")
+KEYS = ("GQ_ABLATE", "GQ_GEMM_RG", "GQ_GEMM_NB", "GQ_GEMM_SPLITS", "GQ_DECODE_CAP", "GQ_NO_FUSED_DECODE")
 for spec in args:
     cfg, _, envs = spec.partition(":")
     for k in KEYS:
@@ -39,7 +45,7 @@ for spec in args:
         N = int(n)
     r = bench.Runner(fmt, M, K, N, dev, 40)
     r.prepare()
-    g = r.capture(r.kernel, 40)
+    g = r.capture(r.step if STEP else r.kernel, 40)
     g.replay()
     t = min(bench.timed_replay(g, dev) for _ in range(5)) / 40
     _, alg_bytes, flops = bench.model(fmt, M, K, N)
