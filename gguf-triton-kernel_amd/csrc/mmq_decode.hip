@@ -296,7 +296,8 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         quantize(r);
     }
-    __syncthreads();
+    // raw barrier: __syncthreads() would also wait vmcnt(0), draining the weight DMAs in flight
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
     // ---- main loop ----
     const int P = 1 << geo.lp2;
@@ -435,9 +436,11 @@ int64_t row_bytes(int fmt, int64_t K)
 
 bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p)
 {
-    const int nts[4] = {1, 2, 4, 8};
-    p.nt = 8;
-    for (int i = 0; i < 4; ++i)
+    // at most 4 tokens per workgroup (NT = 8 spills registers); N = 5..8 runs two token groups,
+    // whose second pass over the weights is served largely by the Infinity Cache
+    const int nts[3] = {1, 2, 4};
+    p.nt = 4;
+    for (int i = 0; i < 3; ++i)
         if (nts[i] >= N) { p.nt = nts[i]; break; }
     while ((size_t)RING + act_lds(fmt, p.nt, K) > (size_t)LDS_CAP) {
         if (p.nt == 1) return false;
@@ -472,9 +475,10 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p)
         g.ngroups = (int)M;
         g.lp2 = 6;
     }
-    // activations cached in registers: at most 4 units per lane and 2 tokens
+    // activations cached in registers: at most 4 units per lane and 2 tokens, or 7 units and 1
+    // token (K <= 28672: the 70B ffn_down rows)
     const int64_t itc = (upr + (1 << g.lp2) - 1) >> g.lp2;
-    p.itc = (p.nt <= 2 && itc <= 4) ? (int)itc : 0;
+    p.itc = ((p.nt <= 2 && itc <= 4) || (p.nt == 1 && itc <= 7)) ? (int)itc : 0;
     const int64_t waves = g.ngroups < W ? g.ngroups : W;
     p.grid = (int)((waves + DW - 1) / DW);
     return true;
@@ -507,13 +511,16 @@ hipError_t launch_f(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *
     case 10: return GQ_LT(1, 2);
     case 11: return GQ_LT(1, 3);
     case 12: return GQ_LT(1, 4);
+    case 13: return GQ_LT(1, 5);
+    case 14: return GQ_LT(1, 6);
+    case 15: return GQ_LT(1, 7);
+
     case 16: return GQ_LT(2, 0);
     case 17: return GQ_LT(2, 1);
     case 18: return GQ_LT(2, 2);
     case 19: return GQ_LT(2, 3);
     case 20: return GQ_LT(2, 4);
-    case 32: return GQ_LT(4, 0);
-    default: return GQ_LT(8, 0);
+    default: return GQ_LT(4, 0);
     }
 #undef GQ_LT
     return hipErrorInvalidValue;
