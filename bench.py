@@ -233,11 +233,18 @@ def bench_config(name, steps, warmup, dev, dist_on, world, rank):
         g.replay()  # first replay pays lazy init
         t = min(timed_replay(g, dev, dist_on) for _ in range(3))
         t_compute = t
-    # dominant kernel alone: activations prepared once, K mmq launches in a graph
-    r.prepare()
-    gk = r.capture(r.kernel, steps)
-    gk.replay()
-    t_k = min(timed_replay(gk, dev, dist_on) for _ in range(3)) / steps
+    # dominant kernel: decode (N <= 8) -- the step IS one launch (fused quantizer + weight
+    # stream), so its time is the step's; GEMM -- the MMQ call alone (gemm_kernel [+ split-K
+    # reduce]) with the activations prepared once, K launches in a graph
+    if N <= 8:
+        t_k = (t_compute if dist_on and world > 1 else t) / steps
+        kname = "stream_decode_kernel (fused q8_1 + decode)"
+    else:
+        r.prepare()
+        gk = r.capture(r.kernel, steps)
+        gk.replay()
+        t_k = min(timed_replay(gk, dev, dist_on) for _ in range(3)) / steps
+        kname = "gemm_kernel (+ gemm_reduce_kernel when split-K)"
     wbytes, alg_bytes, flops = model(fmt, M, K, N)
     per_step = t / steps
     out = {
@@ -246,7 +253,7 @@ def bench_config(name, steps, warmup, dev, dist_on, world, rank):
         "tflops": world * flops / per_step / 1e12,
         "weight_GBps": world * wbytes / per_step / 1e9,
         "compute_only_tflops": world * flops / (t_compute / steps) / 1e12,
-        "roofline": roofline(fmt, M, K, N, t_k, load_traffic(name)),
+        "roofline": dict(roofline(fmt, M, K, N, t_k, load_traffic(name)), kernel=kname),
         "weight_copies": r.ncopies,
     }
     del r
