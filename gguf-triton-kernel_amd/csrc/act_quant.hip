@@ -7,7 +7,7 @@
 // x*127/amax, no fp16 rounding); this build keeps the oracle's exact q8_1 semantics so the
 // GPU path and kernels/cpu_impls see identical integer activations.
 //
-// Eight lanes own one 32-element block (4 fp16 each): gguf_q8_1.hpp.
+// Eight lanes own one 32-element block (4 fp16 each): gguf_q8_1.hpp (DPP group reductions).
 //
 // Output forms (one kernel template, chosen by the caller):
 //   AOS  : the q8_1 byte layout itself (36 B per block) -- gq_quantize_q8_1 / tests
@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256) void act_quant_kernel(const uint16_t *__restri
         w0 = v.x;
         w1 = v.y;
     }
-    const Q81Lane q = q8_1_lane(w0, w1);
+    const Q81Lane q = q8_1_lane_dpp(w0, w1);
     if (!live) return;
 
     if constexpr (MODE == ACT_AOS) {

@@ -44,7 +44,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int KC = 64;     // K elements per stage
-constexpr int NSTAGE = 4;  // ring depth (3 stages in flight)
 constexpr int LDS_MAX = 160 * 1024;
 
 __device__ __forceinline__ h2 as_h2(uint32_t v) { return __builtin_bit_cast(h2, v); }
@@ -144,7 +143,7 @@ template <>
 __device__ __forceinline__ void stage_frags<Q6_K>(const uint8_t *wr, int g, int s4, f16x8 (&frag)[2])
 {
     const int h = s4 >> 1, v = s4 & 1;
-    const float d = h2f(*(const uint16_t *)(wr + 208));
+    const float d = h2f(*(const uint16_t *)(wr + 222)); // image: d at 222 (see issue_w)
     const u32x2 ql = *(const u32x2 *)(wr + 64 * h + 32 * v + 8 * g);
     const u32x2 qh = *(const u32x2 *)(wr + 128 + 32 * h + 8 * g);
     const h2 bias = splat(-1056.f); // 1024 + 32
@@ -246,9 +245,7 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
         const int64_t tok = n0 + r < N ? n0 + r : N - 1;
         av[i] = r < G::BN ? (uint32_t)(tok * K * 2) + act_voff<F>(q ^ act_swz(r)) : DUMMY;
     }
-    // the row this lane multiplies (for Q6_K's per-row window misalignment)
-    const int myrow = 16 * wave + l16;
-    const uint32_t myrow_off = (uint32_t)((m0 + myrow < M ? m0 + myrow : M - 1) * row_bytes);
+    const int myrow = 16 * wave + l16; // the row this lane multiplies
 
     auto issue_w = [&](int64_t w) {
         if constexpr (ABL & 2) return;
@@ -257,8 +254,8 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
         for (int i = 0; i < G::NW; ++i) {
             const int k = wave + NWAVE * i;
             uint32_t vo, so;
-            if constexpr (F == Q6_K) { // 16-byte aligned window over the row's 210 bytes
-                vo = ((wv[i] + 210u * (uint32_t)w) & ~15u) + 16u * wpc[i];
+            if constexpr (F == Q6_K) { // super-block image: pieces +16i (i < 13) and +194 (d at 222)
+                vo = wv[i] + 210u * (uint32_t)w + (wpc[i] < 13 ? 16u * wpc[i] : 194u);
                 so = 0;
             } else {
                 vo = wv[i] + 16u * wpc[i];
@@ -309,7 +306,6 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
             if (s4 == 0) issue_w(w + 2 < w1 ? w + 2 : w1 - 1);
 
             const uint8_t *wr = lds + (int)(w % NWS) * G::W_SLOT + G::RBW * myrow;
-            if constexpr (F == Q6_K) wr += (myrow_off + 210u * (uint32_t)w) & 15u;
             const uint8_t *xs = lds + G::A_BASE + (int)(a % G::NAS) * G::A_SLOT;
             // all of the sub-stage's activation fragments first (one LDS round trip), the
             // dequantization beside them, then the MFMAs
@@ -342,6 +338,15 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
     }
 
     // epilogue: acc[t][i] = D[row 16*wave + 4g + i][token 16t + l16]
+    if (P != nullptr) {
+        // split-K partial: the tile's accumulators in register order, one contiguous BM*BN-float
+        // block per (tile, split): every store instruction writes 1 KiB contiguous
+        const int64_t tile = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+        f32x4 *blk = (f32x4 *)(P + (tile * gridDim.z + blockIdx.z) * (int64_t)(G::BM * G::BN));
+#pragma unroll
+        for (int t = 0; t < NB; ++t) blk[(wave * NB + t) * 64 + lane] = acc[t];
+        return;
+    }
     const int64_t row = m0 + 16 * wave + 4 * g;
     if (row >= M) return;
 #pragma unroll
@@ -358,25 +363,39 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
             } else {
                 for (int i = 0; i < 4 && row + i < M; ++i) dst[i] = f2h_bits(v[i]);
             }
-        } else {
-            float *dst = P + ((int64_t)blockIdx.z * N + tok) * M + row;
-            if (row + 4 <= M) *(f32x4 *)dst = v;
-            else
-                for (int i = 0; i < 4 && row + i < M; ++i) dst[i] = v[i];
         }
     }
 }
 
-// C[t][m] = fp16(sum_s P[s][t][m]), summed in split order (deterministic).
+// C = fp16(sum_s partial_s), summed in split order (deterministic).  Partials are blocked as the
+// GEMM epilogue stores them: per (tile, split) a BM*BN-float block in accumulator register order,
+// element (q = (wave*NB + t)*64 + lane, i) = D[row 16*wave + 4*(lane>>4) + i][token 16t + (lane&15)].
+// One thread per (tile, q): S coalesced 16-byte loads, one 8-byte fp16 store.
+template <int NB>
 __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restrict__ P, uint16_t *__restrict__ C,
-                                                          int64_t M, int64_t N, int64_t ldc, int S)
+                                                          int64_t M, int64_t N, int64_t ldc, int S, int tiles_x,
+                                                          int64_t nq)
 {
+    constexpr int QPT = NWAVE * NB * 64; // float4s per tile block
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (idx >= N * M) return;
-    const int64_t tok = idx / M, m = idx - tok * M;
-    float acc = 0.f;
-    for (int s = 0; s < S; ++s) acc += P[((int64_t)s * N + tok) * M + m];
-    C[tok * ldc + m] = f2h_bits(acc);
+    if (idx >= nq) return;
+    const int64_t tile = idx / QPT;
+    const int q = (int)(idx - tile * QPT);
+    const int lane = q & 63, t = (q >> 6) % NB, wave = (q >> 6) / NB;
+    const int64_t m0 = (tile % tiles_x) * (16 * NWAVE), n0 = (tile / tiles_x) * (16 * NB);
+    const f32x4 *src = (const f32x4 *)P + tile * S * QPT + q;
+    f32x4 acc = src[0];
+    for (int s = 1; s < S; ++s) acc += src[(int64_t)s * QPT];
+    const int64_t row = m0 + 16 * wave + 4 * (lane >> 4), tok = n0 + 16 * t + (lane & 15);
+    if (tok >= N || row >= M) return;
+    uint16_t *dst = C + tok * ldc + row;
+    if (row + 4 <= M) {
+        const u32x2 o = {(uint32_t)f2h_bits(acc[0]) | ((uint32_t)f2h_bits(acc[1]) << 16),
+                         (uint32_t)f2h_bits(acc[2]) | ((uint32_t)f2h_bits(acc[3]) << 16)};
+        *(u32x2 *)dst = o;
+    } else {
+        for (int i = 0; i < 4 && row + i < M; ++i) dst[i] = f2h_bits(acc[i]);
+    }
 }
 
 template <int F, int NB>
@@ -407,8 +426,9 @@ hipError_t launch_cfg(const uint8_t *A, const uint16_t *X, uint16_t *C, float *P
 #endif
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || pl.splits == 1) return e;
-    const int64_t work = N * M;
-    gemm_reduce_kernel<<<dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s>>>(P, C, M, N, ldc, pl.splits);
+    const int64_t nq = (int64_t)grid.x * grid.y * (NWAVE * NB * 64);
+    gemm_reduce_kernel<NB><<<dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s>>>(P, C, M, N, ldc, pl.splits,
+                                                                                     (int)grid.x, nq);
     return hipGetLastError();
 }
 
@@ -449,7 +469,9 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K)
     S = (nws + sps - 1) / sps;
     p.splits = (int)S;
     p.chunks_per_split = (int)sps;
-    p.partial_bytes = S > 1 ? (size_t)S * N * M * sizeof(float) : 0;
+    // blocked partials: S x (tiles) x 128 rows x 16*nb tokens (padded tiles)
+    const int64_t tiles_all = ((M + 127) / 128) * ((N + 16 * p.nb - 1) / (16 * p.nb));
+    p.partial_bytes = S > 1 ? (size_t)S * tiles_all * 128 * 16 * p.nb * sizeof(float) : 0;
     return p;
 }
 
