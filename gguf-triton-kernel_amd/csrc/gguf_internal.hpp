@@ -37,4 +37,12 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K);
 hipError_t launch_gemm(int fmt, const uint8_t *A, const uint16_t *xdeq, uint16_t *C, float *partials,
                        const GemmPlan &plan, int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
 
+// Dequantization and the library GEMM (mmq_dequant.hip).  perm: store 4-groups as (0,2,1,3),
+// matching act_quant's DEQ form.  blas_gemm returns 0 or a negative code.
+hipError_t launch_dequant(int fmt, const uint8_t *A, uint16_t *W, int64_t M, int64_t K, int64_t ldw, bool perm,
+                          hipStream_t s);
+size_t blas_workspace_bytes();
+int blas_gemm(const uint16_t *W, const uint16_t *X, uint16_t *C, int64_t M, int64_t N, int64_t K, int64_t ldc,
+              void *ws, size_t ws_bytes, hipStream_t s);
+
 } // namespace gq

@@ -1,5 +1,6 @@
 // gq_capi.hip -- the C ABI (include/gguf_mmq.h): argument checks, workspace carving,
 // path selection (decode GEMV vs MFMA GEMM) and launches.  Stateless and re-entrant.
+#include <climits>
 #include <cstdio>
 #include <cstdarg>
 #include <cstdlib>
@@ -36,6 +37,19 @@ constexpr int64_t kGemvMaxTokens = 8;
 // gq_act_prepare, which does not know the weight type, makes the same one.)
 bool use_gemv(int64_t N, int64_t K) { return N <= kGemvMaxTokens || !gq::gemm_supported(gq::Q8_0, K); }
 
+// Library-GEMM path (dequantize W to fp16 + hipBLASLt) from this many tokens on; the
+// override GQ_BLAS_MIN_TOKENS (0 = never) is for tuning and tests.
+int64_t blas_min_tokens()
+{
+    const char *e = getenv("GQ_BLAS_MIN_TOKENS");
+    if (e) {
+        const long long v = atoll(e);
+        return v <= 0 ? INT64_MAX : (int64_t)v;
+    }
+    return 768; // measured crossover: 11008x4096 Q4_K 512 tokens 90 vs 121 us, 4096^2 1024 tokens
+}
+bool use_blas(int64_t N, int64_t K) { return !use_gemv(N, K) && N >= blas_min_tokens(); }
+
 // Activation part of the workspace (what gq_act_prepare writes); depends on N, K only.
 size_t act_bytes(int64_t N, int64_t K)
 {
@@ -50,7 +64,8 @@ size_t act_bytes(int64_t N, int64_t K)
 size_t ws_bytes(int t, int64_t M, int64_t N, int64_t K)
 {
     size_t b = act_bytes(N, K);
-    if (!use_gemv(N, K)) b += align_up(gq::plan_gemm(t, M, N, K).partial_bytes);
+    if (use_blas(N, K)) b += align_up((size_t)M * K * 2) + gq::blas_workspace_bytes(); // fp16 W + hipBLASLt
+    else if (!use_gemv(N, K)) b += align_up(gq::plan_gemm(t, M, N, K).partial_bytes);
     return b;
 }
 
@@ -125,6 +140,15 @@ static int compute(gq_type t, const void *A, void *workspace, size_t workspace_b
     const size_t need = ws_bytes(t, M, N, K);
     if (workspace_bytes < need) return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace_bytes, need);
     Carved c = carve(workspace, N, K);
+    if (use_blas(N, K)) {
+        uint16_t *W = (uint16_t *)c.partials; // after the activations: fp16 W, then the BLAS workspace
+        uint8_t *bws = (uint8_t *)W + align_up((size_t)M * K * 2);
+        hipError_t e = gq::launch_dequant(t, (const uint8_t *)A, W, M, K, K, true, s);
+        if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (dequant): %s", hipGetErrorString(e));
+        const int rc = gq::blas_gemm(W, c.xdeq, (uint16_t *)C, M, N, K, ldc, bws, gq::blas_workspace_bytes(), s);
+        if (rc != 0) return fail(GQ_EHIP, "hipBLASLt GEMM failed (code %d)", rc);
+        return GQ_OK;
+    }
     hipError_t e = use_gemv(N, K) ? gq::launch_gemv(t, (const uint8_t *)A, c.xq, c.xd, c.xs, (uint16_t *)C, M, N, K, ldc, s)
                                : gq::launch_gemm(t, (const uint8_t *)A, c.xdeq, (uint16_t *)C, c.partials,
                                                  gq::plan_gemm(t, M, N, K), M, N, K, ldc, s);
@@ -177,6 +201,19 @@ int gq_mmq_prepared(gq_type t, const void *A, void *workspace, size_t workspace_
     if (M == 0 || N == 0) return GQ_OK;
     if (K == 0) return fail(GQ_EINVAL, "K must be positive");
     return compute(t, A, workspace, workspace_bytes, C, M, N, K, ldc, (hipStream_t)stream);
+}
+
+int gq_dequantize(gq_type t, const void *A, void *W, int64_t M, int64_t K, int64_t ldw, void *stream)
+{
+    g_err.clear();
+    int rc = check_common(t, M, 1, K);
+    if (rc != GQ_OK) return rc;
+    if (M == 0 || K == 0) return GQ_OK;
+    if (!A || !W) return fail(GQ_EINVAL, "null pointer");
+    if (ldw < K) return fail(GQ_EINVAL, "ldw=%lld < K=%lld", (long long)ldw, (long long)K);
+    hipError_t e = gq::launch_dequant(t, (const uint8_t *)A, (uint16_t *)W, M, K, ldw, false, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed: %s", hipGetErrorString(e));
+    return GQ_OK;
 }
 
 int gq_quantize_q8_1(const void *X, void *Y, int64_t rows, int64_t K, int64_t ldx, void *stream)

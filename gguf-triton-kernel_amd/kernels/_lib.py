@@ -30,6 +30,7 @@ SIGNATURES = {
     "gq_act_prepare": ([_P, _I64, _I64, _I64, _P, _SZ, _P], _I),
     "gq_mmq_prepared": ([_I, _P, _P, _SZ, _P, _I64, _I64, _I64, _I64, _P], _I),
     "gq_quantize_q8_1": ([_P, _P, _I64, _I64, _I64, _P], _I),
+    "gq_dequantize": ([_I, _P, _P, _I64, _I64, _I64, _P], _I),
     "gq_last_error": ([], ctypes.c_char_p),
     "gq_version": ([], _I),
 }
@@ -121,3 +122,16 @@ def quantize_q8_1_device(X: torch.Tensor) -> torch.Tensor:
         stream = torch.cuda.current_stream(X.device).cuda_stream
         _check(lib().gq_quantize_q8_1(X2.data_ptr(), Y.data_ptr(), rows, K, X2.stride(0), stream))
     return Y
+
+
+def dequantize_device(gtype: int, A: torch.Tensor, M: int, K: int) -> torch.Tensor:
+    """fp16 (M, K) weights from packed blocks on the device (gq_dequantize)."""
+    _require_device(A, "A")
+    qk, bb = BLOCK_ELEMS[gtype], BLOCK_BYTES[gtype]
+    if A.numel() != M * (K // qk) * bb:
+        raise RuntimeError(f"A has {A.numel()} bytes, expected {M * (K // qk) * bb}")
+    W = torch.empty((M, K), dtype=torch.float16, device=A.device)
+    with torch.cuda.device(A.device):
+        stream = torch.cuda.current_stream(A.device).cuda_stream
+        _check(lib().gq_dequantize(gtype, A.data_ptr(), W.data_ptr(), M, K, K, stream))
+    return W

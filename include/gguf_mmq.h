@@ -14,6 +14,7 @@
  *   gq_mmq(GQ_Q4_K, ...)  <- kernels/mmq_q4_k.py:240  mmq_q4_k(A, B, M, N, K)
  *   gq_mmq(GQ_Q6_K, ...)  <- kernels/mmq_q6_k.py:197  mmq_q6_k(A, B, M, N, K)
  *   gq_quantize_q8_1      <- utils/quantize/q8_1.py:18 quantize_to_q8_1 (on the device)
+ *   gq_dequantize         <- utils/quantize/q4_k.py:125, q6_k.py:117, q8_0.py:52 dequantize (device)
  */
 #ifndef GGUF_MMQ_H
 #define GGUF_MMQ_H
@@ -66,6 +67,14 @@ int gq_act_prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *works
                    void *stream);
 int gq_mmq_prepared(gq_type t, const void *A, void *workspace, size_t workspace_bytes, void *C, int64_t M, int64_t N,
                     int64_t K, int64_t ldc, void *stream);
+
+/*
+ * Dequantize packed `t` weights to fp16: W[m * ldw + k] = w (the reference's block formulas,
+ * utils/quantize/{q8_0,q4_k,q6_k}.py dequantize, evaluated in fp32, rounded once to fp16).
+ * M rows of K (a multiple of the block) elements.  gq_mmq uses the same kernel for its
+ * library-GEMM path (N >= a few hundred tokens: fp16 W + hipBLASLt).
+ */
+int gq_dequantize(gq_type t, const void *A, void *W, int64_t M, int64_t K, int64_t ldw, void *stream);
 
 /*
  * q8_1 quantization of fp16 rows on the device, byte-identical to utils/quantize/q8_1.py:

@@ -213,3 +213,34 @@ def test_baseline_configs_full_size(fmt, M, K, Ns):
         finally:
             os.environ.pop("GQ_GEMM_SPLITS")
         assert np.array_equal(Cs.cpu().numpy().view(np.uint16), Cf.cpu().numpy()[:, rows].view(np.uint16))
+
+
+# ---- dequantization (gq_dequantize) and the library-GEMM path (fp16 W + hipBLASLt) ----
+
+@pytest.mark.parametrize("fmt", FMTS)
+def test_device_dequantize_matches_oracle(fmt):
+    """gq_dequantize == the oracle's fp32 dequantization rounded once to fp16 (bit-exact up to
+    the sign of zero: Q6_K's (q - 32) = 0 under a negative scale)."""
+    import kernels._lib as kl
+    M, K = 37, 768 if fmt != "q8_0" else 800
+    qA = random_blocks(fmt, M, K, seed=11)
+    A_t = torch.from_numpy(qA.view(np.int8)).to(_dev())
+    W = kl.dequantize_device(kl.TYPES[fmt], A_t, M, K).cpu().numpy()
+    ref = O.dequant(fmt, qA).reshape(M, K).astype(np.float16)
+    assert np.array_equal(W, ref)
+
+
+@pytest.mark.parametrize("fmt", FMTS)
+@pytest.mark.parametrize("M,N,K,force", [(300, 800, 512, False), (65, 24, 1024, True), (130, 33, 256, True)])
+def test_blas_path(fmt, M, N, K, force, monkeypatch):
+    """N_tok >= 768 (or any N with GQ_BLAS_MIN_TOKENS forced): dequantized fp16 W (same
+    k-permutation as x~) on hipBLASLt; same tolerance as the MFMA path."""
+    if force:
+        monkeypatch.setenv("GQ_BLAS_MIN_TOKENS", "9")
+    qA = random_blocks(fmt, M, K, seed=M + N)
+    B = random_activations(N, K, seed=K)
+    got = run(fmt, qA, B, M, N, K)
+    ideal = O.mmq_from_fp16(fmt, qA, B, M, N, K, O.IDEAL)
+    assert O.max_rel_err(got, ideal) <= TIGHT_GEMM, O.max_rel_err(got, ideal)
+    exact = O.mmq_from_fp16(fmt, qA, B, M, N, K, O.EXACT)
+    assert O.allclose(exact, got, 0.01)
