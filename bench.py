@@ -261,6 +261,61 @@ def bench_config(name, steps, warmup, dev, dist_on, world, rank):
     return out
 
 
+def bench_layer(N, steps, warmup, dev):
+    """BASELINE configs[4]: the seven projections of a Llama-7B block under GGUF Q4_K_M (layer 0:
+    attn_v and ffn_down in Q6_K, the rest Q4_K), shared inputs quantized once per group
+    (kernels.layer_mix.LayerMix).  Weights rotate over >= 1 GiB of copies."""
+    from gguf import LLAMA_LAYER_SHAPES, q4_k_m_layer_types
+    from kernels.layer_mix import GGUFLinear, LayerMix
+    types = q4_k_m_layer_types(0, 32)
+    one = {n: device_random_blocks(types[n], M, K, dev, seed=i) for i, (n, (M, K)) in enumerate(LLAMA_LAYER_SHAPES.items())}
+    layer_bytes = sum(t.numel() for t in one.values())
+    ncopies = max(2, math.ceil(ROTATE_BYTES / layer_bytes))
+    layers = [LayerMix({n: GGUFLinear(types[n], one[n] if c == 0 else one[n].clone(), *LLAMA_LAYER_SHAPES[n])
+                        for n in LLAMA_LAYER_SHAPES}) for c in range(ncopies)]
+    g = torch.Generator(device=dev).manual_seed(7)
+    x = torch.randn(N, 4096, device=dev, generator=g).to(torch.float16)
+    h = torch.randn(N, 11008, device=dev, generator=g).to(torch.float16)
+    outs = {n: torch.empty(N, M, dtype=torch.float16, device=dev) for n, (M, K) in LLAMA_LAYER_SHAPES.items()}
+    flops = sum(2.0 * N * M * K for M, K in LLAMA_LAYER_SHAPES.values())
+    for i in range(max(1, warmup)):  # also creates any library handles outside capture
+        layers[i % ncopies].forward(x, h, outs)
+    torch.cuda.synchronize(dev)
+    gr = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        layers[0].forward(x, h, outs)
+    torch.cuda.current_stream(dev).wait_stream(s)
+    torch.cuda.synchronize(dev)
+    with torch.cuda.graph(gr):
+        for i in range(steps):
+            layers[i % ncopies].forward(x, h, outs)
+    gr.replay()
+    t = min(timed_replay(gr, dev) for _ in range(3)) / steps
+    return {"config": f"q4_k_m_llama7b_layer_m{N}", "fmt": "q4_k+q6_k", "M_tok": N, "ms_per_step": t * 1e3,
+            "tflops": flops / t / 1e12, "weight_GBps": layer_bytes / t / 1e9, "weight_bytes": layer_bytes,
+            "types": types, "weight_copies": ncopies}
+
+
+def bench_msweep(steps, warmup, dev, fmt="q4_k", M=4096, K=4096):
+    """configs[4]'s M sweep: tokens 1..512 on one Q4_K 4096x4096 matrix (the step: gq_mmq)."""
+    res = []
+    for N in (1, 2, 4, 8, 16, 32, 64, 128, 256, 512):
+        r = Runner(fmt, M, K, N, dev, steps)
+        gw = r.capture(r.step, max(1, warmup))
+        gw.replay()
+        gs = r.capture(r.step, steps)
+        gs.replay()
+        t = min(timed_replay(gs, dev) for _ in range(3)) / steps
+        wbytes, alg_bytes, flops = model(fmt, M, K, N)
+        res.append({"M_tok": N, "us_per_step": round(t * 1e6, 2), "tflops": round(flops / t / 1e12, 3),
+                    "weight_GBps": round(wbytes / t / 1e9, 1), "alg_GBps": round(alg_bytes / t / 1e9, 1)})
+        del r, gw, gs
+        torch.cuda.empty_cache()
+    return {"config": f"{fmt}_{M}x{K}_msweep", "points": res}
+
+
 def bench_dist(r, steps, dev, world):
     """Each step: MMQ on the local row shard, then all_gather of the (N, N_out) fp16 shards
     into (world, N, N_out) on a side stream (RCCL), overlapped with the next step."""
@@ -323,6 +378,10 @@ def main():
         for name in CONFIGS:
             if name != args.config:
                 sweep.append(bench_config(name, max(20, args.steps // 4), args.warmup, dev, dist_on, world, rank))
+        if not dist_on:
+            for n in (1, 128):
+                sweep.append(bench_layer(n, max(20, args.steps // 4), args.warmup, dev))
+            sweep.append(bench_msweep(max(20, args.steps // 4), args.warmup, dev))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         fmt, M, K, N = CONFIGS[args.config]

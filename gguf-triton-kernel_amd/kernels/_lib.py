@@ -135,3 +135,27 @@ def dequantize_device(gtype: int, A: torch.Tensor, M: int, K: int) -> torch.Tens
         stream = torch.cuda.current_stream(A.device).cuda_stream
         _check(lib().gq_dequantize(gtype, A.data_ptr(), W.data_ptr(), M, K, K, stream))
     return W
+
+
+def act_prepare(B: torch.Tensor, N: int, K: int, workspace: torch.Tensor):
+    """Quantize the activations once into the front of `workspace` (gq_act_prepare); any number
+    of mmq_prepared calls with the same (N, K) then reuse them."""
+    _require_device(B, "B")
+    if B.dtype != torch.float16 or B.stride(-1) != 1:
+        B = B.to(torch.float16).contiguous()
+    with torch.cuda.device(B.device):
+        stream = torch.cuda.current_stream(B.device).cuda_stream
+        _check(lib().gq_act_prepare(B.data_ptr(), N, K, B.stride(0), workspace.data_ptr(), workspace.numel(),
+                                    stream))
+
+
+def mmq_prepared(gtype: int, A: torch.Tensor, workspace: torch.Tensor, M: int, N: int, K: int,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+    """C (N, M) fp16 from packed A and the activations act_prepare left in `workspace`."""
+    _require_device(A, "A")
+    C = out if out is not None else torch.empty((N, M), dtype=torch.float16, device=A.device)
+    with torch.cuda.device(A.device):
+        stream = torch.cuda.current_stream(A.device).cuda_stream
+        _check(lib().gq_mmq_prepared(gtype, A.data_ptr(), workspace.data_ptr(), workspace.numel(), C.data_ptr(),
+                                     M, N, K, C.stride(0), stream))
+    return C

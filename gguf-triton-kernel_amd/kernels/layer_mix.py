@@ -1,0 +1,65 @@
+"""Mixed-format (GGUF Q4_K_M) projection stack of a Llama block on the MMQ kernels.
+
+BASELINE.json configs[4] / SURVEY.md 8(f)4 (no reference counterpart).  Each projection is a
+packed GGUF weight of its own type (gguf.mix.q4_k_m_layer_types); projections that share an
+input (q/k/v/o here, gate/up) quantize it once (gq_act_prepare) and run gq_mmq_prepared per
+weight -- the dispatch is by type, per matrix, with no repacking.  At decode sizes (N <= 8)
+every call is the one-launch fused decode kernel instead (its quantizer is in-kernel).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+class GGUFLinear:
+    """y = x @ W^T for a packed GGUF weight W (M rows of K elements) on the device."""
+
+    def __init__(self, type_name: str, A: torch.Tensor, M: int, K: int):
+        self.type_name, self.gtype = type_name, _lib.TYPES[type_name]
+        self.A, self.M, self.K = A, M, K
+
+    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        return _lib.mmq(self.gtype, self.A, x, self.M, x.shape[0], self.K)
+
+    def workspace_bytes(self, N: int) -> int:
+        return _lib.workspace_size(self.gtype, self.M, N, self.K)
+
+
+class LayerMix:
+    """The seven projections of one Llama block: attn_q/k/v/output and ffn_gate/up read x
+    (K = 4096), ffn_down reads h (K = 11008).  forward(x, h) -> {name: (N, M) fp16}."""
+
+    GROUPS = (("attn_q", "attn_k", "attn_v", "attn_output", "ffn_gate", "ffn_up"), ("ffn_down",))
+
+    def __init__(self, linears: dict):
+        self.lin = linears
+
+    @classmethod
+    def from_gguf(cls, tensors: dict, layer: int, device="cuda"):
+        """From read_gguf() tensors named blk.<layer>.<proj>.weight."""
+        lins = {}
+        for group in cls.GROUPS:
+            for name in group:
+                t = tensors[f"blk.{layer}.{name}.weight"]
+                M, K = t.shape
+                lins[name] = GGUFLinear(t.type_name, t.to_device(device), M, K)
+        return cls(lins)
+
+    def forward(self, x: torch.Tensor, h: torch.Tensor, out: dict | None = None) -> dict:
+        res = {}
+        for group, inp in zip(self.GROUPS, (x, h)):
+            N, K = inp.shape
+            if N <= 8:  # decode: each call's kernel quantizes its tokens in LDS (one launch per weight)
+                for n in group:
+                    L = self.lin[n]
+                    res[n] = _lib.mmq(L.gtype, L.A, inp, L.M, N, K, out=None if out is None else out[n])
+                continue
+            ws_bytes = max(self.lin[n].workspace_bytes(N) for n in group)
+            ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=inp.device)
+            _lib.act_prepare(inp, N, K, ws)
+            for n in group:
+                L = self.lin[n]
+                res[n] = _lib.mmq_prepared(L.gtype, L.A, ws, L.M, N, K, None if out is None else out[n])
+        return res

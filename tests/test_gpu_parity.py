@@ -244,3 +244,25 @@ def test_blas_path(fmt, M, N, K, force, monkeypatch):
     assert O.max_rel_err(got, ideal) <= TIGHT_GEMM, O.max_rel_err(got, ideal)
     exact = O.mmq_from_fp16(fmt, qA, B, M, N, K, O.EXACT)
     assert O.allclose(exact, got, 0.01)
+
+
+def test_layer_mix_from_gguf(tmp_path):
+    """Q4_K_M-typed layer read from a GGUF file, shared-input groups quantized once."""
+    from gguf import q4_k_m_layer_types, read_gguf, write_gguf
+    from kernels.layer_mix import LayerMix
+    types = q4_k_m_layer_types(0, 32)  # layer 0: attn_v / ffn_down in Q6_K
+    shapes = {n: (96, 512) for n in LayerMix.GROUPS[0]}
+    shapes["ffn_down"] = (64, 768)
+    raw = {n: random_blocks(types[n], *shapes[n], seed=i) for i, n in enumerate(shapes)}
+    p = tmp_path / "l.gguf"
+    write_gguf(p, {f"blk.0.{n}.weight": (types[n], shapes[n], raw[n]) for n in shapes})
+    _, tens = read_gguf(p)
+    layer = LayerMix.from_gguf(tens, 0, device=_dev())
+    for N in (1, 20):
+        x = random_activations(N, 512, seed=N)
+        h = random_activations(N, 768, seed=N + 1)
+        out = layer.forward(torch.from_numpy(x).to(_dev()), torch.from_numpy(h).to(_dev()))
+        torch.cuda.synchronize()
+        for n, (M, K) in shapes.items():
+            ideal = O.mmq_from_fp16(types[n], raw[n], x if K == 512 else h, M, N, K, O.IDEAL)
+            assert O.max_rel_err(out[n].cpu().numpy(), ideal) <= tight(N), (n, N)
