@@ -233,10 +233,10 @@ def bench_config(name, steps, warmup, dev, dist_on, world, rank):
         g.replay()  # first replay pays lazy init
         t = min(timed_replay(g, dev, dist_on) for _ in range(3))
         t_compute = t
-    # dominant kernel: decode (N <= 8) -- the step IS one launch (fused quantizer + weight
+    # dominant kernel: decode (N <= 4) -- the step IS one launch (fused quantizer + weight
     # stream), so its time is the step's; GEMM -- the MMQ call alone (gemm_kernel [+ split-K
     # reduce]) with the activations prepared once, K launches in a graph
-    if N <= 8:
+    if N <= 4:
         t_k = (t_compute if dist_on and world > 1 else t) / steps
         kname = "stream_decode_kernel (fused q8_1 + decode)"
     else:
@@ -400,8 +400,9 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int8-act q8_1 x gguf-weights -> fp16 MFMA (f32 acc)" if N > 8 else
-                     "int8-act q8_1 x gguf-weights -> int32 dot4 (f32 acc)",
+            "dtype": "f16" if N > 4 else "i8",
+            "arith": "q8_1 activations x dequantized GGUF weights on fp16 MFMA, fp32 accumulate" if N > 4 else
+                     "q8_1 int8 activations x GGUF int codes on v_dot4_i32_i8, fp32 block scaling",
             "data": "synthetic (random packed blocks, N(0,1) fp16 activations)",
             "config": {"workload": args.config, "gguf_type": fmt, "N_out": M, "K": K, "M_tok": N,
                        "global_N_out": M * world, "parallelism": f"rowshard{world}" if world > 1 else "single",

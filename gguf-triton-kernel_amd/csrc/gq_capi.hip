@@ -31,7 +31,7 @@ int block_bytes(int t) { return t == GQ_Q8_0 ? 34 : (t == GQ_Q4_K ? 144 : 210); 
 size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
 
 // Decode path up to this many tokens; beyond it the fp16-MFMA GEMM.
-constexpr int64_t kGemvMaxTokens = 8;
+constexpr int64_t kGemvMaxTokens = 4; // 5..8 tokens: the MFMA GEMM (15.9 us at 16 tokens vs 22.3 us decode at 8, Q4_K 4096^2)
 
 // (K % 128 != 0 is only possible for Q8_0, so the choice depends on N and K alone and
 // gq_act_prepare, which does not know the weight type, makes the same one.)

@@ -3,7 +3,7 @@
 BASELINE.json configs[4] / SURVEY.md 8(f)4 (no reference counterpart).  Each projection is a
 packed GGUF weight of its own type (gguf.mix.q4_k_m_layer_types); projections that share an
 input (q/k/v/o here, gate/up) quantize it once (gq_act_prepare) and run gq_mmq_prepared per
-weight -- the dispatch is by type, per matrix, with no repacking.  At decode sizes (N <= 8)
+weight -- the dispatch is by type, per matrix, with no repacking.  At decode sizes (N <= 4)
 every call is the one-launch fused decode kernel instead (its quantizer is in-kernel).
 """
 from __future__ import annotations
@@ -51,7 +51,7 @@ class LayerMix:
         res = {}
         for group, inp in zip(self.GROUPS, (x, h)):
             N, K = inp.shape
-            if N <= 8:  # decode: each call's kernel quantizes its tokens in LDS (one launch per weight)
+            if N <= 4:  # decode: each call's kernel quantizes its tokens in LDS (one launch per weight)
                 for n in group:
                     L = self.lin[n]
                     res[n] = _lib.mmq(L.gtype, L.A, inp, L.M, N, K, out=None if out is None else out[n])

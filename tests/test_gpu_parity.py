@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 
 TIGHT_GEMV = 1.5e-3
 TIGHT_GEMM = 4e-3
-GEMV_MAX_N = 8
+GEMV_MAX_N = 4
 FMTS = ("q8_0", "q4_k", "q6_k")
 
 

@@ -39,7 +39,7 @@ def run(cfg):
                 continue
             vals.setdefault(k, []).append(float(r["Counter_Value"]))
     fmt, M, K, N = bench.CONFIGS[cfg]
-    key = "stream_decode_kernel" if N <= 8 else "gemm_kernel"
+    key = "stream_decode_kernel" if N <= 4 else "gemm_kernel"
     dom = [k for k in vals if key in k]
     if not dom:
         raise SystemExit(f"{cfg}: no {key} dispatch in the PMC output")
