@@ -88,7 +88,6 @@ __device__ __forceinline__ uint32_t act_voff(int p) // byte offset of piece p (8
 }
 
 constexpr int NWAVE = 8; // 512 threads: two waves per SIMD
-constexpr int NWS = 3;   // weight-stage ring: two super-blocks in flight (HBM latency ~1.5 us)
 
 template <int F, int NB>
 struct Cfg {
@@ -99,12 +98,18 @@ struct Cfg {
     static constexpr int NW = (W_REAL + NWAVE - 1) / NWAVE, NA = (A_REAL + NWAVE - 1) / NWAVE; // per wave
     static constexpr int W_SLOT = W_REAL * 1024, A_SLOT = A_REAL * 1024;
     // activation sub-stage ring: 4 slots (3 in flight) unless the LDS budget says 3
-    static constexpr int NAS = NWS * W_SLOT + 4 * A_SLOT + 1024 <= LDS_MAX ? 4 : 3;
+    // weight-stage ring: NWS-1 super-blocks ahead (3, or 2 for Q8_0's 34 KiB stages so that
+    // the activation ring can be deeper); activation ring: as deep as the LDS allows, at most
+    // 4*NWS-4 slots (W(w) must be issued before A(4w): see the pipeline note below)
+    static constexpr int NWS = F == Q8_0 ? 2 : 3;
+    static constexpr int NAS_FIT = (LDS_MAX - 1024 - NWS * W_SLOT) / A_SLOT;
+    static constexpr int NAS = NAS_FIT < 4 * NWS - 4 ? NAS_FIT : 4 * NWS - 4;
     static constexpr int A_BASE = NWS * W_SLOT, SCRATCH = A_BASE + NAS * A_SLOT; // dummy DMAs land there
     static constexpr int LDS_BYTES = SCRATCH + 1024;
     static_assert(BM * NPW % 64 == 0 && (BN * 8) % 64 == 0 || BN * 8 < 64, "whole DMA instructions");
     static_assert(LDS_BYTES <= LDS_MAX, "LDS budget");
-    static_assert((NAS - 2) * NA + NW <= 63, "vmcnt range");
+    static_assert(NAS >= 3, "activation ring depth");
+    static_assert((NAS - 2) * NA + 2 * NW <= 63, "vmcnt range");
 };
 
 // ---------------------------------------------------------------------------------------
@@ -190,13 +195,14 @@ constexpr uint32_t DUMMY = 0u;
 
 // ---------------------------------------------------------------------------------------
 // Pipeline (per wave; a = activation sub-stage, w = a >> 2 = weight stage, NAS activation
-// slots, 3 weight slots):
-//   prologue  W(0) W(1) A(0) .. A(NAS-2)
+// slots, NWS weight slots):
+//   prologue  W(0) .. W(NWS-2) A(0) .. A(NAS-2)
 //   iteration a: wait until A(a) (and so W(a>>2)) landed -> barrier -> A(a+NAS-1) ->
-//                [a&3 == 0: W(w+2)] -> multiply sub-stage a from W slot w%3, A slot a%NAS.
+//                [a&3 == 0: W(w+NWS-1)] -> multiply sub-stage a from W slot w%NWS, A slot a%NAS.
 // vmcnt counts in issue order, so "A(a) landed" = all but the ops issued after it: the NAS-2
 // younger activation sub-stages and the W(.) issued in iterations a-NAS+1 .. a-1 with
-// index % 4 == 0 (after their A).  Past the end the indices are clamped (re-loads of identical
+// index % 4 == 0 (after their A).  W(w) is issued in iteration 4(w-NWS+1), after
+// A(4(w-NWS+1)+NAS-1), which is older than A(4w) iff NAS <= 4*NWS-4.  Past the end the indices are clamped (re-loads of identical
 // bytes into the same slot) so every wave issues the same sequence.
 // ABL: ablation bitmask for performance diagnosis (diagnostic build -DGQ_ABLATION only; 0 in
 // production): 1 = no MFMA, 2 = no weight DMA, 4 = no activation DMA, 8 = no dequantization.
@@ -249,7 +255,7 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
 
     auto issue_w = [&](int64_t w) {
         if constexpr (ABL & 2) return;
-        uint8_t *dst = lds + (int)(w % NWS) * G::W_SLOT;
+        uint8_t *dst = lds + (int)(w % G::NWS) * G::W_SLOT;
 #pragma unroll
         for (int i = 0; i < G::NW; ++i) {
             const int k = wave + NWAVE * i;
@@ -274,17 +280,18 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
         }
     };
     // vmcnt for "A(a) landed": (NAS-2) younger A's + the W's issued after A(a)
-    auto wait_a = [&](int s4) {
+    // rel = a - a0: W issues in iterations [max(0, rel-NAS+1), rel-1] that are multiples of 4
+    auto wait_a = [&](int rel) {
         constexpr int na = ABL & 4 ? 0 : G::NA, nw = ABL & 2 ? 0 : G::NW; // (ablated streams issue nothing)
         constexpr int base = (G::NAS - 2) * na;
-        bool w_after;
-        if constexpr (G::NAS == 4) w_after = s4 != 0;
-        else w_after = s4 == 1 || s4 == 2;
+        const int lo = rel - G::NAS + 1 > 0 ? rel - G::NAS + 1 : 0, hi = rel - 1;
+        const int w_after = hi >= lo ? hi / 4 - (lo + 3) / 4 + 1 : 0;
         if constexpr ((ABL & 6) == 6) asm volatile("s_barrier" ::: "memory");
         else if constexpr (ABL & 4) { // weights only: W(w) must land by sub-stage 4w
-            if (s4 == 0) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(nw) : "memory");
+            if ((rel & 3) == 0) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(nw) : "memory");
             else asm volatile("s_barrier" ::: "memory");
-        } else if (w_after) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(base + nw) : "memory");
+        } else if (w_after >= 2) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(base + 2 * nw) : "memory");
+        else if (w_after == 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(base + nw) : "memory");
         else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(base) : "memory");
     };
 
@@ -294,18 +301,18 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
 
     if (w0 < w1) {
         const int64_t a0 = 4 * w0, a1 = 4 * w1;
-        issue_w(w0);
-        issue_w(w0 + 1 < w1 ? w0 + 1 : w1 - 1);
+#pragma unroll
+        for (int i = 0; i < G::NWS - 1; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
 #pragma unroll
         for (int i = 0; i < G::NAS - 1; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
         for (int64_t a = a0; a < a1; ++a) {
             const int s4 = (int)(a & 3);
-            wait_a(s4);
+            wait_a((int)(a - a0));
             const int64_t w = a >> 2;
             issue_a(a + G::NAS - 1 < a1 ? a + G::NAS - 1 : a1 - 1);
-            if (s4 == 0) issue_w(w + 2 < w1 ? w + 2 : w1 - 1);
+            if (s4 == 0) issue_w(w + G::NWS - 1 < w1 ? w + G::NWS - 1 : w1 - 1);
 
-            const uint8_t *wr = lds + (int)(w % NWS) * G::W_SLOT + G::RBW * myrow;
+            const uint8_t *wr = lds + (int)(w % G::NWS) * G::W_SLOT + G::RBW * myrow;
             const uint8_t *xs = lds + G::A_BASE + (int)(a % G::NAS) * G::A_SLOT;
             // all of the sub-stage's activation fragments first (one LDS round trip), the
             // dequantization beside them, then the MFMAs
@@ -338,6 +345,10 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
     }
 
     // epilogue: acc[t][i] = D[row 16*wave + 4g + i][token 16t + l16]
+    if constexpr ((ABL & 16) != 0) { // diagnostic: no epilogue stores
+        if (acc[0][0] == 1234.5f) C[0] = 0;
+        return;
+    }
     if (P != nullptr) {
         // split-K partial: the tile's accumulators in register order, one contiguous BM*BN-float
         // block per (tile, split): every store instruction writes 1 KiB contiguous
@@ -419,6 +430,8 @@ hipError_t launch_cfg(const uint8_t *A, const uint16_t *X, uint16_t *C, float *P
     case 13: gemm_kernel<F, NB, 13><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
     case 15: gemm_kernel<F, NB, 15><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
     case 14: gemm_kernel<F, NB, 14><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+    case 31: gemm_kernel<F, NB, 31><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+    case 16: gemm_kernel<F, NB, 16><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
     default: gemm_kernel<F, NB><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
     }
 #else

@@ -45,7 +45,7 @@ class GGUFTensor:
 
     def to_device(self, device="cuda"):
         import torch
-        return torch.from_numpy(np.ascontiguousarray(self.data).view(np.int8)).to(device)
+        return torch.from_numpy(np.array(self.data, dtype=np.uint8).view(np.int8)).to(device)  # host copy: memmaps are read-only
 
 
 class _Reader:
