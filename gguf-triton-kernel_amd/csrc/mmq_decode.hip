@@ -40,7 +40,10 @@ namespace {
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-constexpr int DW = 8; // waves per workgroup (two per SIMD)
+#ifndef GQ_DECODE_DW
+#define GQ_DECODE_DW 8
+#endif
+constexpr int DW = GQ_DECODE_DW; // waves per workgroup (two per SIMD)
 #ifndef GQ_DECODE_NI
 #define GQ_DECODE_NI 7
 #endif

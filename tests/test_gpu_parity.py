@@ -266,3 +266,17 @@ def test_layer_mix_from_gguf(tmp_path):
         for n, (M, K) in shapes.items():
             ideal = O.mmq_from_fp16(types[n], raw[n], x if K == 512 else h, M, N, K, O.IDEAL)
             assert O.max_rel_err(out[n].cpu().numpy(), ideal) <= tight(N), (n, N)
+
+
+@pytest.mark.parametrize("fmt", ("q4_k", "q6_k"))
+def test_gemm_256_row_tiles(fmt, monkeypatch):
+    """Two 16-row groups per wave (256-row tiles), with and without split-K, ragged edges."""
+    monkeypatch.setenv("GQ_GEMM_RG", "2")
+    for M, N, K, splits in ((600, 100, 1024, None), (300, 128, 2048, "4")):
+        if splits:
+            monkeypatch.setenv("GQ_GEMM_SPLITS", splits)
+        qA = random_blocks(fmt, M, K, seed=M)
+        B = random_activations(N, K, seed=N)
+        got = run(fmt, qA, B, M, N, K)
+        ideal = O.mmq_from_fp16(fmt, qA, B, M, N, K, O.IDEAL)
+        assert O.max_rel_err(got, ideal) <= TIGHT_GEMM, (M, N, K, O.max_rel_err(got, ideal))
