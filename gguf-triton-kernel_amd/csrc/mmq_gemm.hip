@@ -69,7 +69,10 @@ __device__ __forceinline__ h2 pair13(uint32_t c) { return as_h2(__builtin_amdgcn
 // stage's first byte and the reader adds that misalignment (delta, per row and stage).
 template <int F> struct WStage;
 template <> struct WStage<Q4_K> { static constexpr int RBW = 144, SB = 144; };
-template <> struct WStage<Q6_K> { static constexpr int RBW = 224, SB = 210; };
+// Q6_K rows are padded to 240 B (15 pieces, the last a repeat of the d piece): a 224-B stride
+// (56 dwords) put rows l and l+8 of a 16-lane fragment read on the same banks (2-way
+// conflicts, ~half of the LDS cycles measured); 60 dwords spread 16 rows over distinct banks.
+template <> struct WStage<Q6_K> { static constexpr int RBW = 240, SB = 210; };
 template <> struct WStage<Q8_0> { static constexpr int RBW = 272, SB = 272; };
 
 // Activation sub-stage c (64 elements) = sub-stage s4 = c & 3 of super-block c >> 2: the K
@@ -102,7 +105,7 @@ struct Cfg {
     // weight-stage ring: NWS-1 super-blocks ahead (3, or 2 for Q8_0's 34 KiB stages so that
     // the activation ring can be deeper); activation ring: as deep as the LDS allows, at most
     // 4*NWS-4 slots (W(w) must be issued before A(4w): see the pipeline note below)
-    static constexpr int NWS = (F == Q8_0 || (RG > 1 && F == Q6_K)) ? 2 : 3;
+    static constexpr int NWS = F == Q8_0 ? 2 : 3;
     // padding DMAs (instruction counts not a multiple of the wave count) land in a scratch KiB
     static constexpr bool PAD = W_REAL % NWAVE != 0 || A_REAL % NWAVE != 0;
     static constexpr int NAS_FIT = (LDS_MAX - (PAD ? 1024 : 0) - NWS * W_SLOT) / A_SLOT;
@@ -264,7 +267,7 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
             const int k = wave + NWAVE * i;
             uint32_t vo, so;
             if constexpr (F == Q6_K) { // super-block image: pieces +16i (i < 13) and +194 (d at 222)
-                vo = wv[i] + 210u * (uint32_t)w + (wpc[i] < 13 ? 16u * wpc[i] : 194u);
+                vo = wv[i] + 210u * (uint32_t)w + (wpc[i] < 13 ? 16u * wpc[i] : 194u); // piece 14 = 13 again
                 so = 0;
             } else {
                 vo = wv[i] + 16u * wpc[i];
@@ -467,7 +470,7 @@ template <int F>
 hipError_t launch_fmt(const uint8_t *A, const uint16_t *X, uint16_t *C, float *P, const GemmPlan &pl, int64_t M,
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
-    if constexpr (F != Q8_0)
+    if constexpr (F == Q4_K)
         if (pl.rg == 2 && pl.nb == 8) return launch_cfg<F, 8, 2>(A, X, C, P, pl, M, N, K, ldc, s);
     switch (pl.nb) {
     case 1: return launch_cfg<F, 1, 1>(A, X, C, P, pl, M, N, K, ldc, s);
@@ -490,9 +493,10 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K)
     p.nb = pick_nb(N);
     if (const char *env = getenv("GQ_GEMM_NB")) p.nb = atoi(env);
     // two 16-row groups per wave (256-row tiles: half the activation traffic per weight) for
-    // tall K-quant matrices at full token tiles; Q8_0's 34 KiB weight stages do not fit twice
-    p.rg = (fmt != Q8_0 && p.nb == 8 && M >= 8192) ? 2 : 1; // measured: 8192..28672 rows 3-6% faster
-    if (const char *env = getenv("GQ_GEMM_RG")) p.rg = (fmt != Q8_0 && p.nb == 8 && atoi(env) == 2) ? 2 : 1;
+    // tall matrices at full token tiles
+    // (Q4_K only: Q6_K's padded 240-B rows and Q8_0's 272-B rows do not fit 256 rows twice)
+    p.rg = (fmt == Q4_K && p.nb == 8 && M >= 8192) ? 2 : 1; // measured: 11008 rows 5% faster
+    if (const char *env = getenv("GQ_GEMM_RG")) p.rg = (fmt == Q4_K && p.nb == 8 && atoi(env) == 2) ? 2 : 1;
     const int64_t nws = K / 256; // weight stages (super-blocks)
     const int64_t bm = 128 * p.rg;
     const int64_t tiles = ((M + bm - 1) / bm) * ((N + 16 * p.nb - 1) / (16 * p.nb));

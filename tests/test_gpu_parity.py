@@ -268,7 +268,7 @@ def test_layer_mix_from_gguf(tmp_path):
             assert O.max_rel_err(out[n].cpu().numpy(), ideal) <= tight(N), (n, N)
 
 
-@pytest.mark.parametrize("fmt", ("q4_k", "q6_k"))
+@pytest.mark.parametrize("fmt", ("q4_k",))
 def test_gemm_256_row_tiles(fmt, monkeypatch):
     """Two 16-row groups per wave (256-row tiles), with and without split-K, ragged edges."""
     monkeypatch.setenv("GQ_GEMM_RG", "2")
