@@ -2,14 +2,28 @@
 //
 // Bit-exact with utils/quantize/q8_1.py:18-70: d = fp16(amax/127) (0 for an all-zero
 // block), q = clamp(rne(fp16(x / d')), +-127) with d' = 1 where d == 0,
-// s = fp16(d * fp16(sum q)).  fp32 division is IEEE correctly rounded (hipcc default), so
-// fp16(x/d) equals torch's CPU fp16 division.  Each of the 8 lanes of an aligned lane group
+// s = fp16(d * fp16(sum q)); fp16(x/d) equals torch's CPU fp16 division of finite inputs
+// (see Division below).  Each of the 8 lanes of an aligned lane group
 // holds 4 consecutive fp16 (two dwords); amax and sum(q) are reduced by xor shuffles inside
 // the group, so every lane of the group must reach the call together.
+//
+// Division.  fp16(x / d) for fp16 x and d is computed as q = x*r, r = v_rcp_f32(d), plus one
+// residual correction fma(fma(-q, d, x), r, q): an fp16/fp16 quotient lies more than 2^-23
+// (relative) from every fp16 rounding midpoint, and the corrected quotient is within ~2^-24
+// of it, so both round to the same fp16 value -- checked exhaustively over all fp16 pairs
+// with every r within 1 ulp of 1/d by tools/q81_div_check.cpp.  Three VALU ops per element
+// instead of the IEEE division sequence (div_scale x2, rcp, 5 fma, div_fmas, div_fixup).
 #pragma once
 #include "gguf_blocks.hpp"
 
 namespace gq {
+
+// fp16-exact x / d for fp16-valued x, d (see above); r ~ 1/d within 1 ulp
+__device__ __forceinline__ float q81_div(float x, float d, float r)
+{
+    const float q = x * r;
+    return __builtin_fmaf(__builtin_fmaf(-q, d, x), r, q);
+}
 
 struct Q81Lane {
     uint32_t codes; // this lane's 4 int8 codes, little endian
@@ -26,14 +40,15 @@ __device__ __forceinline__ Q81Lane q8_1_lane(uint32_t w0, uint32_t w1)
     amax = fmaxf(amax, __shfl_xor(amax, 2, 8));
     amax = fmaxf(amax, __shfl_xor(amax, 4, 8));
     Q81Lane r;
-    r.dbits = amax != 0.f ? f2h_bits(amax / 127.0f) : (uint16_t)0;
+    r.dbits = amax != 0.f ? f2h_bits(q81_div(amax, 127.0f, 1.0f / 127.0f)) : (uint16_t)0;
     r.d = h2f(r.dbits);
     const float div = r.d == 0.f ? 1.0f : r.d;
+    const float rdiv = __builtin_amdgcn_rcpf(div);
     int sum = 0;
     r.codes = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        float q = __builtin_rintf(h2f(f2h_bits(x[i] / div)));
+        float q = __builtin_rintf(h2f(f2h_bits(q81_div(x[i], div, rdiv))));
         q = fminf(127.f, fmaxf(-127.f, q));
         const int qi = (int)q;
         sum += qi;
@@ -57,14 +72,15 @@ __device__ __forceinline__ Q81Lane q8_1_lane_dpp(uint32_t w0, uint32_t w1)
     amax = fmaxf(amax, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax), 0x4e, 0xf, 0xf, false)));
     amax = fmaxf(amax, __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, amax), 0x101f)));
     Q81Lane r;
-    r.dbits = amax != 0.f ? f2h_bits(amax / 127.0f) : (uint16_t)0;
+    r.dbits = amax != 0.f ? f2h_bits(q81_div(amax, 127.0f, 1.0f / 127.0f)) : (uint16_t)0;
     r.d = h2f(r.dbits);
     const float div = r.d == 0.f ? 1.0f : r.d;
+    const float rdiv = __builtin_amdgcn_rcpf(div);
     int sum = 0;
     r.codes = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        float q = __builtin_rintf(h2f(f2h_bits(x[i] / div)));
+        float q = __builtin_rintf(h2f(f2h_bits(q81_div(x[i], div, rdiv))));
         q = fminf(127.f, fmaxf(-127.f, q));
         const int qi = (int)q;
         sum += qi;

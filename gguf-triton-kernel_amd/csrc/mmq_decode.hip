@@ -36,6 +36,10 @@
 
 namespace gq {
 
+#ifdef GQ_DECODE_STAMPS // diagnostic build: per-wave s_memtime breakdown (never the product)
+__device__ unsigned long long g_dstamps[65536][4];
+#endif
+
 namespace {
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -148,6 +152,10 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
     extern __shared__ __attribute__((aligned(1024))) uint8_t smem[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#ifdef GQ_DECODE_STAMPS
+    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+    unsigned long long t_wait = 0;
+#endif
     const int64_t tok0 = (int64_t)blockIdx.y * NT;
     const int nb = K / 32;
     const int kp = (K + 63) / 64 * 64;
@@ -213,19 +221,31 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, 0x7fffffff, 0x00020000);
     uint8_t *xslot = ring + (NS - 1) * SLOT;
     auto xblock = [&](int r, int lb) { return (r * WBLK + lb) * DW + wave; }; // global block of local block lb
+    auto tok_split = [&](int b, int &t, int &j) { // b = t * nb + j without an integer division
+        t = 0;
+        j = b;
+#pragma unroll
+        for (int i = 1; i < NT; ++i)
+            if (j >= nb) {
+                j -= nb;
+                ++t;
+            }
+    };
     auto issue_x = [&](int r) {
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
             const int lb = 16 * k + (lane >> 2);
             int b = xblock(r, lb);
             if (b >= xblocks) b = 0;
-            const int t = b / nb, j = b - t * nb;
+            int t, j;
+            tok_split(b, t, j);
             const int64_t tok = tok0 + t < N ? tok0 + t : N - 1;
             dma16x(xrs, xslot + 1024 * k, (uint32_t)((tok * ldx + 32 * j + 8 * (lane & 3)) * 2));
         }
     };
     auto store_q = [&](int r, int lb, const Q81Lane &qq) {
-        const int b = xblock(r, lb), t = b / nb, j = b - t * nb;
+        int t, j;
+        tok_split(xblock(r, lb), t, j);
         const int k = 32 * j + 4 * (lane & 7);
         *(uint32_t *)(codes + t * kp + 16 * swz_piece<F>(k >> 4) + (k & 15)) = qq.codes;
         if constexpr (F == Q6_K)
@@ -269,6 +289,9 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
     }
     // raw barrier: __syncthreads() would also wait vmcnt(0), draining the weight DMAs in flight
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#ifdef GQ_DECODE_STAMPS
+    const unsigned long long t_pro = __builtin_amdgcn_s_memtime();
+#endif
 
     // ---- main loop ----
     const int P = 1 << geo.lp2;
@@ -313,8 +336,14 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
     };
 
     for (int j = 0; j < ntask; ++j) {
+#ifdef GQ_DECODE_STAMPS
+        const unsigned long long ta = __builtin_amdgcn_s_memtime();
+#endif
         if (j + NS - 2 < ntask) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * NI) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef GQ_DECODE_STAMPS
+        t_wait += __builtin_amdgcn_s_memtime() - ta;
+#endif
         if (j + NS - 1 < ntask) issue(j + NS - 1);
 
         uint32_t st, len;
@@ -385,6 +414,16 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // no DMA may land after the wave exits
+#ifdef GQ_DECODE_STAMPS
+    const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+    const int gw_id = blockIdx.x * DW + wave;
+    if (lane == 0 && gw_id < 65536 && blockIdx.y == 0) {
+        g_dstamps[gw_id][0] = t_pro - t_start;
+        g_dstamps[gw_id][1] = t_wait;
+        g_dstamps[gw_id][2] = t_end - t_pro;
+        g_dstamps[gw_id][3] = (unsigned long long)ntask;
+    }
+#endif
 }
 
 struct Pick {
@@ -527,3 +566,10 @@ hipError_t launch_decode_fused(int fmt, const uint8_t *A, const uint16_t *X, int
 }
 
 } // namespace gq
+
+#ifdef GQ_DECODE_STAMPS
+extern "C" int gq_debug_decode_stamps(void *host, size_t bytes)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(gq::g_dstamps), bytes < sizeof(gq::g_dstamps) ? bytes : sizeof(gq::g_dstamps)) == hipSuccess ? 0 : 1;
+}
+#endif

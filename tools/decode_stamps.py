@@ -1,0 +1,35 @@
+"""Per-wave time breakdown of the decode kernel (diagnostic build -DGQ_DECODE_STAMPS):
+prologue (staging + quantization), waiting for weight DMAs, multiply loop.  s_memtime ticks."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gguf-triton-kernel_amd")]
+import kernels._lib as kl  # noqa: E402
+
+kl.LIB_PATH = os.path.join(ROOT, "gguf-triton-kernel_amd", "lib",
+                           "libgguf_mmq_%s.so" % os.environ.get("GQ_STAMPS_SO", "stamps"))
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+dev = torch.device("cuda:0")
+for cfg in sys.argv[1:] or ["q6_k_28672x8192_m1"]:
+    fmt, M, K, N = bench.CONFIGS[cfg]
+    r = bench.Runner(fmt, M, K, N, dev, 4)
+    for i in range(8):
+        r.step(i)
+    torch.cuda.synchronize()
+    buf = np.zeros((65536, 4), np.uint64)
+    assert kl.lib().gq_debug_decode_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes) == 0
+    used = buf[buf[:, 3] > 0].astype(np.float64)
+    pro, wait, loop, nt = used[:, 0], used[:, 1], used[:, 2], used[:, 3]
+    tot = pro + loop
+    print(f"{cfg}: waves={len(used)} tasks/wave={nt.mean():.1f}  ticks: total med={np.median(tot):.0f} "
+          f"max={tot.max():.0f}  prologue med={np.median(pro):.0f}  loop med={np.median(loop):.0f}  "
+          f"dma-wait med={np.median(wait):.0f} ({np.median(wait / loop) * 100:.0f}% of loop)  "
+          f"compute/task={np.median((loop - wait) / nt):.0f}")
+    del r
