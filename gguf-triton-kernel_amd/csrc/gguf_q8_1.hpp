@@ -94,4 +94,50 @@ __device__ __forceinline__ Q81Lane q8_1_lane_dpp(uint32_t w0, uint32_t w1)
     return r;
 }
 
+// q8_1 of one 32-element block held by an aligned group of 4 lanes (8 elements, one 16-byte
+// load, each): the same arithmetic again; the group reductions are two DPP quad permutes.
+// codes = the lane's 8 codes (2 dwords); s4 = the sum over the lane pair (a 16-element half).
+struct Q81Quad {
+    uint32_t codes[2];
+    float d;
+    uint16_t sbits;
+    int s4;
+};
+
+__device__ __forceinline__ Q81Quad q8_1_quad(u32x4 w)
+{
+    const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
+    float x[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        x[2 * i] = h2f(wd[i] & 0xffff);
+        x[2 * i + 1] = h2f(wd[i] >> 16);
+    }
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(x[i]));
+    amax = fmaxf(amax, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax), 0xb1, 0xf, 0xf, false)));
+    amax = fmaxf(amax, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax), 0x4e, 0xf, 0xf, false)));
+    Q81Quad r;
+    const uint16_t dbits = amax != 0.f ? f2h_bits(q81_div(amax, 127.0f, 1.0f / 127.0f)) : (uint16_t)0;
+    r.d = h2f(dbits);
+    const float div = r.d == 0.f ? 1.0f : r.d;
+    const float rdiv = __builtin_amdgcn_rcpf(div);
+    int sum = 0;
+    r.codes[0] = r.codes[1] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        float q = __builtin_rintf(h2f(f2h_bits(q81_div(x[i], div, rdiv))));
+        q = fminf(127.f, fmaxf(-127.f, q));
+        const int qi = (int)q;
+        sum += qi;
+        r.codes[i >> 2] |= (uint32_t)(qi & 0xff) << (8 * (i & 3));
+    }
+    sum += __builtin_amdgcn_mov_dpp(sum, 0xb1, 0xf, 0xf, false);
+    r.s4 = sum; // lanes (0,1) and (2,3) of the group: the two 16-element halves
+    sum += __builtin_amdgcn_mov_dpp(sum, 0x4e, 0xf, 0xf, false);
+    r.sbits = f2h_bits(r.d * h2f(f2h_bits((float)sum)));
+    return r;
+}
+
 } // namespace gq

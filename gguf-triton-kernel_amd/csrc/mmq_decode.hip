@@ -37,7 +37,7 @@
 namespace gq {
 
 #ifdef GQ_DECODE_STAMPS // diagnostic build: per-wave s_memtime breakdown (never the product)
-__device__ unsigned long long g_dstamps[65536][4];
+__device__ unsigned long long g_dstamps[65536][8];
 #endif
 
 namespace {
@@ -59,6 +59,10 @@ constexpr int NS = GQ_DECODE_NS; // ring slots per wave: NS-1 tasks in flight wh
 constexpr int SLOT = NI * 1024;
 constexpr int RING = DW * NS * SLOT;
 constexpr int LDS_CAP = 160 * 1024;
+// units (64 weights) per lane work item: Q6_K lanes take whole super-block halves (up to two
+// tokens: with four, two units' activations at once exceed the register file)
+template <int F, int NT> constexpr int UPC_OF = F == Q6_K && NT <= 2 ? 2 : 1;
+int upc_of(int fmt, int nt) { return fmt == Q6_K && nt <= 2 ? 2 : 1; }
 
 struct DecodeGeom {
     int ngroups; // row groups (nseg == 1) or rows (nseg > 1)
@@ -149,6 +153,7 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
                                                                 int64_t ldc, DecodeGeom geo)
 {
     using L = Layout<F>;
+    constexpr int UPC = UPC_OF<F, NT>;
     extern __shared__ __attribute__((aligned(1024))) uint8_t smem[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -161,6 +166,7 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
     const int kp = (K + 63) / 64 * 64;
     const uint32_t RB = (uint32_t)(K / L::QK) * L::BYTES;
     const int upr = (K + 63) / 64;
+    const int cpr = upr / UPC; // lane chunks per row
     uint8_t *ring = smem + wave * (NS * SLOT);
     uint8_t *codes = smem + RING;
     float *sd = (float *)(codes + NT * kp);
@@ -203,24 +209,25 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
         next(gi, si);
         const uint32_t ws = st & ~15u, we = st + len;
         uint8_t *dst = ring + (j % NS) * SLOT;
+        const bool real = j < ntask;
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
             uint32_t o = ws + 1024u * k + 16u * lane;
             if (o >= we) o = ws; // past the window: re-read its first line (L2 hit), never past the tensor
-            dma16(wrs, dst + 1024 * k, o);
+            // no task: an offset past the buffer's range (>= 2^31) -- zeros, no memory access
+            dma16(wrs, dst + 1024 * k, real ? o : 0x80000000u);
         }
     };
 
-    // ---- prologue: stage the fp16 activations (round 0) first, then the first NS-1 tasks ----
-    // Activation blocks (32 elements of one token) are dealt to waves round-robin; a wave stages
-    // NI*16 blocks per round in its last ring slot (4 lanes x 16 B per block) and quantizes them
-    // with 8 lanes per block, two blocks per lane group in flight.
+    // ---- prologue: the fp16 activations into registers, then a task into every ring slot ----
+    // Activation blocks (32 elements of one token) are dealt to waves round-robin, 16 per pass
+    // (4 lanes per block, 8 elements = one 16-byte load per lane), up to XP passes per round.
+    // 4 passes (one round) cover K <= 16384 at one token; the instantiations that cache 5+
+    // units per lane (K > 16384) take 8 -- more than needed costs redundant loads elsewhere
+    constexpr int XP = ITC * UPC >= 5 ? 8 : 4;
     const int xblocks = NT * nb;
-    constexpr int WBLK = NI * 16; // blocks per wave per round
-    const int rounds = (xblocks + DW * WBLK - 1) / (DW * WBLK);
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, 0x7fffffff, 0x00020000);
-    uint8_t *xslot = ring + (NS - 1) * SLOT;
-    auto xblock = [&](int r, int lb) { return (r * WBLK + lb) * DW + wave; }; // global block of local block lb
+    const int xrounds = (xblocks + DW * 16 * XP - 1) / (DW * 16 * XP);
+    auto xblock = [&](int r, int pass) { return ((r * XP + pass) * 16 + (lane >> 2)) * DW + wave; };
     auto tok_split = [&](int b, int &t, int &j) { // b = t * nb + j without an integer division
         t = 0;
         j = b;
@@ -231,62 +238,80 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
                 ++t;
             }
     };
-    auto issue_x = [&](int r) {
+    auto npass = [&](int r) { // passes of round r with a block for some lane group of this wave
+        const int left = xblocks - (r * XP * 16) * DW - wave;
+        const int n = left > 0 ? (left + 16 * DW - 1) / (16 * DW) : 0;
+        return n < XP ? n : XP;
+    };
+    // unconditional (clamped) loads: a load under a branch leaves a phi copy behind it that
+    // the compiler waits for (vmcnt(0)) right away, serializing the passes
+    auto load_x = [&](int r, u32x4 (&xv)[XP]) {
 #pragma unroll
-        for (int k = 0; k < NI; ++k) {
-            const int lb = 16 * k + (lane >> 2);
-            int b = xblock(r, lb);
+        for (int q = 0; q < XP; ++q) {
+            int b = xblock(r, q);
             if (b >= xblocks) b = 0;
             int t, j;
             tok_split(b, t, j);
             const int64_t tok = tok0 + t < N ? tok0 + t : N - 1;
-            dma16x(xrs, xslot + 1024 * k, (uint32_t)((tok * ldx + 32 * j + 8 * (lane & 3)) * 2));
+            xv[q] = ld16(X + tok * ldx + 32 * j + 8 * (lane & 3));
         }
     };
-    auto store_q = [&](int r, int lb, const Q81Lane &qq) {
+    auto store_q = [&](int b, const Q81Quad &qq) {
         int t, j;
-        tok_split(xblock(r, lb), t, j);
-        const int k = 32 * j + 4 * (lane & 7);
-        *(uint32_t *)(codes + t * kp + 16 * swz_piece<F>(k >> 4) + (k & 15)) = qq.codes;
+        tok_split(b, t, j);
+        const int k = 32 * j + 8 * (lane & 3);
+        *(u32x2 *)(codes + t * kp + 16 * swz_piece<F>(k >> 4) + (k & 15)) = (u32x2){qq.codes[0], qq.codes[1]};
         if constexpr (F == Q6_K)
-            if ((lane & 3) == 0) ((int *)sx)[t * 2 * nb + 2 * j + ((lane >> 2) & 1)] = qq.s4;
-        if ((lane & 7) == 0) {
+            if ((lane & 1) == 0) ((int *)sx)[t * 2 * nb + 2 * j + ((lane >> 1) & 1)] = qq.s4;
+        if ((lane & 3) == 0) {
             sd[t * nb + j] = qq.d;
             if constexpr (F == Q4_K) sx[t * nb + j] = h2f(qq.sbits);
         }
     };
-    auto quantize = [&](int r) {
-        int nblk = xblocks - r * WBLK * DW - wave; // blocks of this wave in this round
-        nblk = nblk > 0 ? (nblk + DW - 1) / DW : 0;
-        if (nblk > WBLK) nblk = WBLK;
-        for (int lb0 = 0; lb0 < nblk; lb0 += 16) { // two passes of 8 blocks (8 lanes per block)
-            const int lb1 = lb0 + (lane >> 3), lb2 = lb1 + 8;
-            const u32x2 v1 = *(const u32x2 *)(xslot + 64 * lb1 + 8 * (lane & 7));
-            const u32x2 v2 = *(const u32x2 *)(xslot + 64 * (lb2 < WBLK ? lb2 : lb1) + 8 * (lane & 7));
-            const Q81Lane q1 = q8_1_lane_dpp(v1.x, v1.y);
-            const Q81Lane q2 = q8_1_lane_dpp(v2.x, v2.y);
-            if (lb1 < nblk) store_q(r, lb1, q1);
-            if (lb2 < nblk) store_q(r, lb2, q2);
+    auto quantize = [&](int r, const u32x4 (&xv)[XP]) {
+        const int np = npass(r);
+#pragma unroll
+        for (int q = 0; q < XP; ++q) {
+            if (q < np) { // every lane of the wave computes (DPP groups); stores only real blocks
+                const Q81Quad qq = q8_1_quad(xv[q]);
+                const int b = xblock(r, q);
+                if (b < xblocks) store_q(b, qq);
+            }
         }
+        // consume every activation register on every path: a load the compiler sees as possibly
+        // unconsumed makes it wait vmcnt(0) -- all weight DMAs -- before reusing its register
+#pragma unroll
+        for (int q = 0; q < XP; ++q) asm volatile("" ::"v"(xv[q].x), "v"(xv[q].y), "v"(xv[q].z), "v"(xv[q].w));
     };
 
-    issue_x(0);
+    u32x4 xv[XP];
+    load_x(0, xv);
+    // Task 0 goes out with the activation loads; the rest of the ring once the activations are
+    // quantized (issued together, they queue the activations behind twice the weight traffic,
+    // and a small matrix waits on exactly that latency).  Task 0 always issues (past the
+    // wave's tasks: an offset beyond the buffer -- zeros, no memory access), so the wait below
+    // for the activations, the older loads, is a fixed vmcnt(NI).
+    issue(0);
 #pragma unroll
-    for (int j = 0; j < NS - 1; ++j)
-        if (j < ntask) issue(j);
-    int gc = g_begin, sc = 0; // task being multiplied
-    // X round 0 = the oldest NI DMAs; the younger ones are the weight tasks just issued
-    if (ntask >= NS - 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 1) * NI) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifndef GQ_ABL_NOQUANT
-    quantize(0);
+    for (int q = 0; q < XP; ++q) asm volatile("" ::"v"(xv[q].x), "v"(xv[q].y), "v"(xv[q].z), "v"(xv[q].w)); // waits vmcnt(NI)
+#ifdef GQ_DECODE_STAMPS
+    const unsigned long long t_xw = __builtin_amdgcn_s_memtime();
 #endif
-    for (int r = 1; r < rounds; ++r) { // long activations: further rounds, full waits
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        issue_x(r);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        quantize(r);
+    quantize(0, xv);
+    for (int r = 1; r < xrounds; ++r) { // long activations: further rounds (their loads wait behind the DMAs)
+        u32x4 xr[XP];
+        load_x(r, xr);
+        quantize(r, xr);
     }
+#pragma unroll
+    for (int j = 1; j < NS; ++j)
+        if (j < ntask) issue(j);
+    int issued = NS < ntask ? NS : ntask;
+    int gc = g_begin, sc = 0; // task being multiplied
+#ifdef GQ_DECODE_STAMPS
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const unsigned long long t_q = __builtin_amdgcn_s_memtime();
+#endif
     // raw barrier: __syncthreads() would also wait vmcnt(0), draining the weight DMAs in flight
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #ifdef GQ_DECODE_STAMPS
@@ -297,12 +322,13 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
     const int P = 1 << geo.lp2;
     const int lrow = lane >> geo.lp2, lunit = lane & (P - 1);
     const int ntok = N - tok0 < NT ? (int)(N - tok0) : NT;
-    Act<F, NT> ca[ITC > 0 ? ITC : 1];
+    Act<F, NT> ca[ITC > 0 ? ITC * UPC : 1];
     if constexpr (ITC > 0) {
 #pragma unroll
         for (int i = 0; i < ITC; ++i) {
-            const int u = lunit + P * i;
-            act_from_lds<F, NT>(ca[i], codes, sd, sx, kp, nb, u < upr ? u : upr - 1);
+            const int c = lunit + P * i < cpr ? lunit + P * i : cpr - 1;
+#pragma unroll
+            for (int e = 0; e < UPC; ++e) act_from_lds<F, NT>(ca[UPC * i + e], codes, sd, sx, kp, nb, UPC * c + e);
         }
     }
     float acc[NT];
@@ -310,7 +336,32 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
     for (int t = 0; t < NT; ++t) acc[t] = 0.f;
 
     // the contribution of unit u (activation slot i when cached) of the row at rowp
-    auto unit = [&](const uint8_t *rowp, int u, int i) {
+    auto unit = [&](const UnitLoad<F> &l, int u, int i, float (&acc)[NT]) {
+        if constexpr (ITC > 0) {
+            dot_unit<F, NT>(UnitRaw<F>::from(l, u, nb), ca[i], acc);
+        } else {
+            Act<F, NT> a;
+            act_from_lds<F, NT>(a, codes, sd, sx, kp, nb, u);
+            dot_unit<F, NT>(UnitRaw<F>::from(l, u, nb), a, acc);
+        }
+    };
+    // lane chunk c of the row at rowp (activation slots UPC*i.. when cached).  Q6_K: the half
+    // super-block c -- units 2c (v = 0) and 2c+1 (v = 1) share its qh, scale and d bytes, so
+    // they are read once (8 LDS reads per 128 weights instead of 12) and the unit's shifts
+    // are compile-time constants
+    auto chunk = [&](const uint8_t *rowp, int c, int i, float (&acc)[NT]) {
+        if constexpr (UPC == 2) {
+            // (the shared fields' loads are merged by the compiler; written as two unit loads
+            // because direct reads here made the waitcnt pass add a vmcnt(0) before them, i.e.
+            // wait for the task DMA just issued -- tools/check_waits.py)
+            UnitLoad<Q6_K> l0, l1;
+            l0.load(rowp, 2 * c, nb);
+            l1.load(rowp, 2 * c + 1, nb);
+            unit(l0, 2 * c, 2 * i, acc);
+            unit(l1, 2 * c + 1, 2 * i + 1, acc);
+            return;
+        }
+        const int u = c;
         UnitLoad<F> l;
 #ifdef GQ_ABL_NOWLDS
         __builtin_memset(&l, 0, sizeof(l));
@@ -326,25 +377,28 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
         acc[0] += (float)x;
         return;
 #endif
-        if constexpr (ITC > 0) {
-            dot_unit<F, NT>(UnitRaw<F>::from(l, u, nb), ca[i], acc);
-        } else {
-            Act<F, NT> a;
-            act_from_lds<F, NT>(a, codes, sd, sx, kp, nb, u);
-            dot_unit<F, NT>(UnitRaw<F>::from(l, u, nb), a, acc);
-        }
+        unit(l, u, i, acc);
     };
 
     for (int j = 0; j < ntask; ++j) {
 #ifdef GQ_DECODE_STAMPS
         const unsigned long long ta = __builtin_amdgcn_s_memtime();
 #endif
-        if (j + NS - 2 < ntask) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * NI) : "memory");
+        // slot (j - 1) % NS was freed by the previous multiply: refill it, then wait for task j
+        // with the tasks issued after it still in flight (counted vmcnt; stores only add to it)
+        if (j > 0 && issued < ntask) {
+            issue(issued);
+            ++issued;
+        }
+        const int ahead = issued - j - 1;
+        static_assert(NS >= 2 && NS <= 4, "ring depth");
+        if (ahead >= NS - 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 1) * NI) : "memory");
+        else if (NS > 2 && ahead == NS - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS > 2 ? NS - 2 : 0) * NI) : "memory");
+        else if (NS > 3 && ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifdef GQ_DECODE_STAMPS
         t_wait += __builtin_amdgcn_s_memtime() - ta;
 #endif
-        if (j + NS - 1 < ntask) issue(j + NS - 1);
 
         uint32_t st, len;
         const int g = gc, s = sc;
@@ -359,49 +413,59 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
         if (geo.nseg == 1) {
             const int r0 = g * geo.G;
             const int nr = M - r0 < geo.G ? M - r0 : geo.G;
-            for (int rp = 0; rp < nr; rp += 64 >> geo.lp2) {
+            // row pass rp: lane row rp + lrow into a[]; out: reduce over the P lanes and store
+            auto pass = [&](int rp, float (&a)[NT]) {
                 const int r = rp + lrow;
                 const bool valid = r < nr;
                 const uint8_t *rowp = base + (uint32_t)(valid ? r : 0) * RB;
                 if constexpr (ITC > 0) {
 #pragma unroll
                     for (int i = 0; i < ITC; ++i) {
-                        const int u = lunit + P * i;
-                        if (valid && u < upr) unit(rowp, u, i);
+                        const int c = lunit + P * i;
+                        if (valid && c < cpr) chunk(rowp, c, i, a);
                     }
                 } else {
-                    for (int u = lunit; u < upr; u += P)
-                        if (valid) unit(rowp, u, 0);
+                    for (int c = lunit; c < cpr; c += P)
+                        if (valid) chunk(rowp, c, 0, a);
                 }
+            };
+            auto out = [&](int rp, float (&a)[NT]) {
+                const int r = rp + lrow;
                 if (P == 64) {
 #pragma unroll
                     for (int t = 0; t < NT; ++t) {
-                        const float v = wave_sum_dpp(acc[t]);
-                        acc[t] = 0.f;
+                        const float v = wave_sum_dpp(a[t]);
+                        a[t] = 0.f;
                         if (lane == 0 && t < ntok) C[(tok0 + t) * ldc + r0 + r] = f2h_bits(v);
                     }
                 } else {
 #pragma unroll
                     for (int t = 0; t < NT; ++t) {
-                        float v = acc[t];
+                        float v = a[t];
                         for (int off = P >> 1; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-                        acc[t] = 0.f;
-                        if (lunit == 0 && valid && t < ntok) C[(tok0 + t) * ldc + r0 + r] = f2h_bits(v);
+                        a[t] = 0.f;
+                        if (lunit == 0 && r < nr && t < ntok) C[(tok0 + t) * ldc + r0 + r] = f2h_bits(v);
                     }
                 }
+            };
+            const int RS = 64 >> geo.lp2; // rows per pass
+            int rp = 0;
+            for (; rp < nr; rp += RS) {
+                pass(rp, acc);
+                out(rp, acc);
             }
         } else {
-            const int u0 = s * geo.segu, u1 = u0 + geo.segu;
+            const int u0 = s * geo.segu, c0 = u0 / UPC, c1 = c0 + geo.segu / UPC;
             const uint8_t *rowp = base - unit_byte<F>(u0, nb);
             if constexpr (ITC > 0) {
 #pragma unroll
                 for (int i = 0; i < ITC; ++i) {
-                    const int u = lane + 64 * i;
-                    if (u >= u0 && u < u1 && u < upr) unit(rowp, u, i);
+                    const int c = lane + 64 * i;
+                    if (c >= c0 && c < c1 && c < cpr) chunk(rowp, c, i, acc);
                 }
             } else {
-                for (int u = u0 + lane; u < u1; u += 64)
-                    if (u < upr) unit(rowp, u, 0);
+                for (int c = c0 + lane; c < c1; c += 64)
+                    if (c < cpr) chunk(rowp, c, 0, acc);
             }
             if (s == geo.nseg - 1) {
 #pragma unroll
@@ -422,6 +486,10 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
         g_dstamps[gw_id][1] = t_wait;
         g_dstamps[gw_id][2] = t_end - t_pro;
         g_dstamps[gw_id][3] = (unsigned long long)ntask;
+        g_dstamps[gw_id][4] = t_xw - t_start;
+        g_dstamps[gw_id][5] = t_q - t_start;
+        g_dstamps[gw_id][6] = t_start;
+        g_dstamps[gw_id][7] = t_end;
     }
 #endif
 }
@@ -459,6 +527,7 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p)
     p.lds = (size_t)RING + act_lds(fmt, p.nt, K);
     const int64_t RB = row_bytes(fmt, K);
     const int64_t upr = (K + 63) / 64;
+    const int64_t cpr = upr / upc_of(fmt, p.nt); // lane chunks per row
     const int64_t cap = NI * 1024 - 16;
     const int per_cu = (int)(LDS_CAP / p.lds) > 0 ? (int)(LDS_CAP / p.lds) : 1;
     const int64_t W = (int64_t)256 * per_cu * DW; // waves the chip holds
@@ -475,7 +544,7 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p)
         g.segu = (int)upr;
         g.ngroups = (int)((M + G - 1) / G);
         int lp2 = 0;
-        while ((1 << lp2) < upr && lp2 < 6) ++lp2;
+        while ((1 << lp2) < cpr && lp2 < 6) ++lp2;
         g.lp2 = lp2;
     } else {
         const int64_t unit64 = fmt == Q8_0 ? 64 * 68 : (fmt == Q4_K ? 64 * 36 : 64 * 210 / 4);
@@ -485,10 +554,10 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p)
         g.ngroups = (int)M;
         g.lp2 = 6;
     }
-    // activations cached in registers: at most 4 units per lane and 2 tokens, or 7 units and 1
-    // token (K <= 28672: the 70B ffn_down rows)
-    const int64_t itc = (upr + (1 << g.lp2) - 1) >> g.lp2;
-    p.itc = ((p.nt <= 2 && itc <= 4) || (p.nt == 1 && itc <= 7)) ? (int)itc : 0;
+    // activations cached in registers: at most 4 units per lane (Q6_K: 2) and 2 tokens, or 8
+    // units and 1 token (K <= 28672: the 70B ffn_down rows) -- no spills (kernel-resource-usage)
+    const int64_t itc = (cpr + (1 << g.lp2) - 1) >> g.lp2, units = itc * (upr / cpr);
+    p.itc = ((p.nt <= 2 && units <= (fmt == Q6_K ? 2 : 4)) || (p.nt == 1 && units <= 8)) ? (int)itc : 0;
     const int64_t waves = g.ngroups < W ? g.ngroups : W;
     p.grid = (int)((waves + DW - 1) / DW);
     return true;
@@ -515,22 +584,36 @@ hipError_t launch_f(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *
                     int64_t ldc, const Pick &p, hipStream_t s)
 {
 #define GQ_LT(nt, itc) launch_t<F, nt, itc>(A, X, ldx, C, M, N, K, ldc, p, s)
-    switch (p.nt * 8 + p.itc) {
-    case 8: return GQ_LT(1, 0);
-    case 9: return GQ_LT(1, 1);
-    case 10: return GQ_LT(1, 2);
-    case 11: return GQ_LT(1, 3);
-    case 12: return GQ_LT(1, 4);
-    case 13: return GQ_LT(1, 5);
-    case 14: return GQ_LT(1, 6);
-    case 15: return GQ_LT(1, 7);
+    if constexpr (F == Q6_K) { // pick(): at most 8 cached units (4 chunks), 2 with two tokens
+        switch (p.nt * 8 + p.itc) {
+        case 8: return GQ_LT(1, 0);
+        case 9: return GQ_LT(1, 1);
+        case 10: return GQ_LT(1, 2);
+        case 11: return GQ_LT(1, 3);
+        case 12: return GQ_LT(1, 4);
+        case 16: return GQ_LT(2, 0);
+        case 17: return GQ_LT(2, 1);
+        case 32: return GQ_LT(4, 0);
+        default: return hipErrorInvalidValue;
+        }
+    } else {
+        switch (p.nt * 8 + p.itc) {
+        case 8: return GQ_LT(1, 0);
+        case 9: return GQ_LT(1, 1);
+        case 10: return GQ_LT(1, 2);
+        case 11: return GQ_LT(1, 3);
+        case 12: return GQ_LT(1, 4);
+        case 13: return GQ_LT(1, 5);
+        case 14: return GQ_LT(1, 6);
+        case 15: return GQ_LT(1, 7);
 
-    case 16: return GQ_LT(2, 0);
-    case 17: return GQ_LT(2, 1);
-    case 18: return GQ_LT(2, 2);
-    case 19: return GQ_LT(2, 3);
-    case 20: return GQ_LT(2, 4);
-    default: return GQ_LT(4, 0);
+        case 16: return GQ_LT(2, 0);
+        case 17: return GQ_LT(2, 1);
+        case 18: return GQ_LT(2, 2);
+        case 19: return GQ_LT(2, 3);
+        case 20: return GQ_LT(2, 4);
+        default: return GQ_LT(4, 0);
+        }
     }
 #undef GQ_LT
     return hipErrorInvalidValue;

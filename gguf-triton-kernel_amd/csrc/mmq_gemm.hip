@@ -112,7 +112,7 @@ struct Cfg {
     static constexpr int NAS = NAS_FIT < 4 * NWS - 4 ? NAS_FIT : 4 * NWS - 4;
     static constexpr int A_BASE = NWS * W_SLOT, SCRATCH = A_BASE + NAS * A_SLOT; // dummy DMAs land there
     static constexpr int LDS_BYTES = SCRATCH + (PAD ? 1024 : 0);
-    static_assert(BM * NPW % 64 == 0 && (BN * 8) % 64 == 0 || BN * 8 < 64, "whole DMA instructions");
+    static_assert((BM * NPW % 64 == 0 && (BN * 8) % 64 == 0) || BN * 8 < 64, "whole DMA instructions");
     static_assert(LDS_BYTES <= LDS_MAX, "LDS budget");
     static_assert(NAS >= 3, "activation ring depth");
     static_assert((NAS - 2) * NA + 2 * NW <= 63, "vmcnt range");
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
             const int k = wave + NWAVE * i;
             uint32_t vo, so;
             if constexpr (F == Q6_K) { // super-block image: pieces +16i (i < 13) and +194 (d at 222)
-                vo = wv[i] + 210u * (uint32_t)w + (wpc[i] < 13 ? 16u * wpc[i] : 194u); // piece 14 = 13 again
+                vo = wv[i] + (uint32_t)WStage<F>::SB * (uint32_t)w + (wpc[i] < 13 ? 16u * wpc[i] : 194u); // piece 14 = 13 again
                 so = 0;
             } else {
                 vo = wv[i] + 16u * wpc[i];

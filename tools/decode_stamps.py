@@ -23,13 +23,16 @@ for cfg in sys.argv[1:] or ["q6_k_28672x8192_m1"]:
     for i in range(8):
         r.step(i)
     torch.cuda.synchronize()
-    buf = np.zeros((65536, 4), np.uint64)
+    buf = np.zeros((65536, 8), np.uint64)
     assert kl.lib().gq_debug_decode_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes) == 0
     used = buf[buf[:, 3] > 0].astype(np.float64)
     pro, wait, loop, nt = used[:, 0], used[:, 1], used[:, 2], used[:, 3]
+    xw, qd, t0, t1 = used[:, 4], used[:, 5], used[:, 6], used[:, 7]
     tot = pro + loop
     print(f"{cfg}: waves={len(used)} tasks/wave={nt.mean():.1f}  ticks: total med={np.median(tot):.0f} "
           f"max={tot.max():.0f}  prologue med={np.median(pro):.0f}  loop med={np.median(loop):.0f}  "
           f"dma-wait med={np.median(wait):.0f} ({np.median(wait / loop) * 100:.0f}% of loop)  "
           f"compute/task={np.median((loop - wait) / nt):.0f}")
+    print(f"   prologue: x-arrival med={np.median(xw):.0f}  quantized med={np.median(qd):.0f}  "
+          f"barrier med={np.median(pro - qd):.0f}")
     del r
