@@ -453,6 +453,7 @@ hipError_t launch_cfg(const uint8_t *A, const uint16_t *X, uint16_t *C, float *P
     case 8: gemm_kernel<F, NB, RG, 8><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
     case 15: gemm_kernel<F, NB, RG, 15><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
     case 16: gemm_kernel<F, NB, RG, 16><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+    case 31: gemm_kernel<F, NB, RG, 31><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
     default: gemm_kernel<F, NB, RG><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
     }
 #else
