@@ -122,6 +122,22 @@ def test_ragged_shapes(fmt, M, N, K):
     assert O.allclose(exact, got, 0.01)
 
 
+@pytest.mark.parametrize("fmt", FMTS)
+@pytest.mark.parametrize("N,K", [(2, 8192), (4, 8192), (3, 16384), (2, 28672), (4, 28672), (1, 16640)])
+def test_decode_long_rows(fmt, N, K):
+    """Decode path at long rows: several activation quantization rounds (N*K/32 blocks beyond
+    one round of the workgroup's register passes), Q6_K super-block-half lanes at two tokens,
+    row segments, activation caches of 1..8 units -- every row against the oracle."""
+    M = 97
+    qA = random_blocks(fmt, M, K, seed=N * 31 + K)
+    B = random_activations(N, K, seed=K - N)
+    got = run(fmt, qA, B, M, N, K)
+    ideal = O.mmq_from_fp16(fmt, qA, B, M, N, K, O.IDEAL)
+    assert O.max_rel_err(got, ideal) <= TIGHT_GEMV, O.max_rel_err(got, ideal)
+    exact = O.mmq_from_fp16(fmt, qA, B, M, N, K, O.EXACT)
+    assert O.allclose(exact, got, 0.01)
+
+
 @pytest.mark.parametrize("K", [32, 64, 96, 160, 288, 320, 384, 4000])
 def test_q8_0_any_block_count(K):
     """Q8_0 only needs K % 32 == 0.  The reference's Triton kernel is wrong for K > 256 with
