@@ -408,10 +408,23 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restric
                                                           int64_t nq)
 {
     constexpr int QPT = NWAVE * RG * NB * 64; // float4s per tile block
-    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (idx >= nq) return;
-    const int64_t tile = idx / QPT;
-    const int q = (int)(idx - tile * QPT);
+    constexpr int BPT = QPT / 256;            // reduce workgroups per tile
+    // Workgroup -> tile on the XCD that computed the tile: workgroups are dealt to the 8 XCDs
+    // round-robin by linear id, so with tiles % 8 == 0 every split of GEMM tile t ran on XCD
+    // t % 8 and its partials are in that XCD's L2; reduce workgroup b (on XCD b % 8) takes
+    // one of those tiles.  Otherwise tile-major.
+    const int64_t ntiles = nq / QPT;
+    int64_t tile, chunk;
+    if (ntiles % 8 == 0) {
+        const int64_t i = blockIdx.x / 8;
+        tile = blockIdx.x % 8 + 8 * (i / BPT);
+        chunk = i % BPT;
+    } else {
+        tile = blockIdx.x / BPT;
+        chunk = blockIdx.x % BPT;
+    }
+    const int q = (int)(chunk * 256 + threadIdx.x);
+    if (tile >= ntiles) return;
     const int lane = q & 63, t = (q >> 6) % NB, wave = (q >> 6) / NB;
     const int64_t m0 = (tile % tiles_x) * (16 * NWAVE * RG), n0 = (tile / tiles_x) * (16 * NB);
     const f32x4 *src = (const f32x4 *)P + tile * S * QPT + q;
