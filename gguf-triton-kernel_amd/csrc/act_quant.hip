@@ -7,7 +7,8 @@
 // x*127/amax, no fp16 rounding); this build keeps the oracle's exact q8_1 semantics so the
 // GPU path and kernels/cpu_impls see identical integer activations.
 //
-// Eight lanes own one 32-element block (4 fp16 each): gguf_q8_1.hpp (DPP group reductions).
+// Four lanes own one 32-element block (8 fp16, one 16-byte load each): gguf_q8_1.hpp's
+// q8_1_quad (DPP quad reductions).
 //
 // Output forms (one kernel template, chosen by the caller):
 //   AOS  : the q8_1 byte layout itself (36 B per block) -- gq_quantize_q8_1 / tests
@@ -27,44 +28,44 @@ __global__ __launch_bounds__(256) void act_quant_kernel(const uint16_t *__restri
                                                         uint16_t *__restrict__ xdeq)
 {
     const int64_t nb = K / 32;
-    const int64_t blk = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
-    const int sub = threadIdx.x & 7;
+    const int64_t blk = (int64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
+    const int sub = threadIdx.x & 3; // elements 8*sub .. 8*sub+7 of the block
     const bool live = blk < rows * nb;
     const int64_t row = live ? blk / nb : 0;
     const int64_t j = live ? blk - row * nb : 0;
 
-    uint32_t w0 = 0, w1 = 0;
-    if (live) {
-        u32x2 v = ld8(X + row * ldx + 32 * j + 4 * sub);
-        w0 = v.x;
-        w1 = v.y;
-    }
-    const Q81Lane q = q8_1_lane_dpp(w0, w1);
+    u32x4 v = {0, 0, 0, 0};
+    if (live) v = ld16(X + row * ldx + 32 * j + 8 * sub);
+    const Q81Quad q = q8_1_quad(v);
     if (!live) return;
 
     if constexpr (MODE == ACT_AOS) {
         uint8_t *o = out + blk * 36;
-        __builtin_memcpy(o + 4 + 4 * sub, &q.codes, 4);
+        __builtin_memcpy(o + 4 + 8 * sub, q.codes, 8);
         if (sub == 0) {
-            uint32_t ds = (uint32_t)q.dbits | ((uint32_t)q.sbits << 16);
+            const uint32_t ds = (uint32_t)f2h_bits(q.d) | ((uint32_t)q.sbits << 16);
             __builtin_memcpy(o, &ds, 4);
         }
     } else if constexpr (MODE == ACT_SOA) {
-        *(uint32_t *)(codes + row * K + 32 * j + 4 * sub) = q.codes;
+        *(u32x2 *)(codes + row * K + 32 * j + 8 * sub) = (u32x2){q.codes[0], q.codes[1]};
         if (sub == 0) {
             dout[row * nb + j] = q.d;
             sout[row * nb + j] = h2f(q.sbits);
         }
     } else {
-        float v[4];
+        // x~ = fp16(d*q); each 4-element group in the order (0,2,1,3): the order mmq_gemm.hip's
+        // packed dequantization produces weight pairs in (its k-permutation; the MFMA k-sum is
+        // unchanged)
+        uint32_t o[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = q.d * (float)(int8_t)((q.codes >> (8 * i)) & 0xff);
-        // element order (0,2,1,3) inside each 4-group: the order mmq_gemm.hip's packed
-        // dequantization produces weight pairs in (its k-permutation; the MFMA k-sum is unchanged)
-        u32x2 o;
-        o.x = (uint32_t)f2h_bits(v[0]) | ((uint32_t)f2h_bits(v[2]) << 16);
-        o.y = (uint32_t)f2h_bits(v[1]) | ((uint32_t)f2h_bits(v[3]) << 16);
-        *(u32x2 *)(xdeq + row * K + 32 * j + 4 * sub) = o;
+        for (int h = 0; h < 2; ++h) {
+            float v4[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v4[i] = q.d * (float)(int8_t)((q.codes[h] >> (8 * i)) & 0xff);
+            o[2 * h] = (uint32_t)f2h_bits(v4[0]) | ((uint32_t)f2h_bits(v4[2]) << 16);
+            o[2 * h + 1] = (uint32_t)f2h_bits(v4[1]) | ((uint32_t)f2h_bits(v4[3]) << 16);
+        }
+        *(u32x4 *)(xdeq + row * K + 32 * j + 8 * sub) = (u32x4){o[0], o[1], o[2], o[3]};
     }
 }
 
@@ -73,7 +74,7 @@ hipError_t launch_act_quant(int mode, const uint16_t *X, int64_t ldx, int64_t ro
 {
     const int64_t nblk = rows * (K / 32);
     if (nblk == 0) return hipSuccess;
-    dim3 grid((unsigned)((nblk + 31) / 32)), block(256);
+    dim3 grid((unsigned)((nblk + 63) / 64)), block(256);
     switch (mode) {
     case ACT_AOS:
         act_quant_kernel<ACT_AOS><<<grid, block, 0, s>>>(X, ldx, rows, K, (uint8_t *)out0, nullptr, nullptr,
