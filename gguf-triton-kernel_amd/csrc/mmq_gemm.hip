@@ -36,6 +36,10 @@
 
 namespace gq {
 
+#ifdef GQ_GEMM_STAMPS // diagnostic build: per-wave s_memtime breakdown (never the product)
+__device__ unsigned long long g_gstamps[65536][8];
+#endif
+
 namespace {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -219,6 +223,10 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
 {
     using G = Cfg<F, NB, RG>;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[G::LDS_BYTES];
+#ifdef GQ_GEMM_STAMPS
+    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+    unsigned long long t_first = 0, t_wait = 0, t_loop = 0;
+#endif
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -315,7 +323,17 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
         for (int i = 0; i < G::NAS - 1; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
         for (int64_t a = a0; a < a1; ++a) {
             const int s4 = (int)(a & 3);
+#ifdef GQ_GEMM_STAMPS
+            const unsigned long long tw = __builtin_amdgcn_s_memtime();
+#endif
             wait_a((int)(a - a0));
+#ifdef GQ_GEMM_STAMPS
+            {
+                const unsigned long long tn = __builtin_amdgcn_s_memtime();
+                if (a == a0) t_first = tn - t_start;
+                else t_wait += tn - tw;
+            }
+#endif
             const int64_t w = a >> 2;
             issue_a(a + G::NAS - 1 < a1 ? a + G::NAS - 1 : a1 - 1);
             if (s4 == 0) issue_w(w + G::NWS - 1 < w1 ? w + G::NWS - 1 : w1 - 1);
@@ -359,6 +377,22 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // no DMA may land after the workgroup exits
     }
+#ifdef GQ_GEMM_STAMPS
+    t_loop = __builtin_amdgcn_s_memtime() - t_start;
+    auto stamp_out = [&]() {
+        const int64_t wg = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+        const int64_t id = wg * NWAVE + wave;
+        if (lane == 0 && id < 65536) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            g_gstamps[id][0] = t_first;
+            g_gstamps[id][1] = t_wait;
+            g_gstamps[id][2] = t_loop;
+            g_gstamps[id][3] = __builtin_amdgcn_s_memtime() - t_start;
+            g_gstamps[id][4] = (unsigned long long)(w1 - w0) * 4;
+            g_gstamps[id][5] = 1;
+        }
+    };
+#endif
 
     // epilogue: acc[rg][t][i] = D[row 16*(RG*wave + rg) + 4g + i][token 16t + l16]
     if constexpr ((ABL & 16) != 0) { // diagnostic: no epilogue stores
@@ -374,6 +408,9 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
         for (int rg = 0; rg < RG; ++rg)
 #pragma unroll
             for (int t = 0; t < NB; ++t) blk[((RG * wave + rg) * NB + t) * 64 + lane] = acc[rg][t];
+#ifdef GQ_GEMM_STAMPS
+        stamp_out();
+#endif
         return;
     }
 #pragma unroll
@@ -395,6 +432,9 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
             }
         }
     }
+#ifdef GQ_GEMM_STAMPS
+    stamp_out();
+#endif
 }
 
 // C = fp16(sum_s partial_s), summed in split order (deterministic).  Partials are blocked as the
@@ -542,3 +582,10 @@ hipError_t launch_gemm(int fmt, const uint8_t *A, const uint16_t *X, uint16_t *C
 }
 
 } // namespace gq
+
+#ifdef GQ_GEMM_STAMPS
+extern "C" int gq_debug_gemm_stamps(void *host, size_t bytes)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(gq::g_gstamps), bytes < sizeof(gq::g_gstamps) ? bytes : sizeof(gq::g_gstamps)) == hipSuccess ? 0 : 1;
+}
+#endif
