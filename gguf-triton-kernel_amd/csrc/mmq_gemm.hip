@@ -225,7 +225,7 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
     __shared__ __attribute__((aligned(1024))) uint8_t lds[G::LDS_BYTES];
 #ifdef GQ_GEMM_STAMPS
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-    unsigned long long t_first = 0, t_wait = 0, t_loop = 0;
+    unsigned long long t_first = 0, t_wait = 0, t_loop = 0, t_issued = 0;
 #endif
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -315,12 +315,18 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
 #pragma unroll
         for (int t = 0; t < NB; ++t) acc[rg][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+#ifdef GQ_GEMM_STAMPS
+    const unsigned long long t_setup = __builtin_amdgcn_s_memtime() - t_start;
+#endif
     if (w0 < w1) {
         const int64_t a0 = 4 * w0, a1 = 4 * w1;
 #pragma unroll
         for (int i = 0; i < G::NWS - 1; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
 #pragma unroll
         for (int i = 0; i < G::NAS - 1; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
+#ifdef GQ_GEMM_STAMPS
+        t_issued = __builtin_amdgcn_s_memtime() - t_start;
+#endif
         for (int64_t a = a0; a < a1; ++a) {
             const int s4 = (int)(a & 3);
 #ifdef GQ_GEMM_STAMPS
@@ -389,7 +395,9 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
             g_gstamps[id][2] = t_loop;
             g_gstamps[id][3] = __builtin_amdgcn_s_memtime() - t_start;
             g_gstamps[id][4] = (unsigned long long)(w1 - w0) * 4;
-            g_gstamps[id][5] = 1;
+            g_gstamps[id][5] = 1 + t_setup;
+            g_gstamps[id][6] = t_start;
+            g_gstamps[id][7] = t_issued;
         }
     };
 #endif

@@ -33,5 +33,13 @@ for cfg in sys.argv[1:] or ["q8_0_4096x4096_m128"]:
     med = lambda v: np.median(v)
     print(f"{cfg}: waves={len(u)} sub-stages/wave={med(subs):.0f}  ticks med: first wait={med(first):.0f} "
           f"later waits={med(wait):.0f} ({med(wait / np.maximum(loop - first, 1)) * 100:.0f}% of the rest of the loop) "
-          f"loop end={med(loop):.0f} epilogue={med(end - loop):.0f} total={med(end):.0f} max={end.max():.0f}", flush=True)
+          f"loop end={med(loop):.0f} epilogue={med(end - loop):.0f} total={med(end):.0f} max={end.max():.0f}  "
+          f"(setup done by {med(u[:, 5] - 1):.0f}, prologue DMAs issued by {med(u[:, 7]):.0f})", flush=True)
+    # launch skew inside each workgroup (8 waves, one CU, one clock): the first barrier waits
+    # for the last wave to arrive
+    t0 = buf[:len(buf) // 8 * 8, 6].reshape(-1, 8).astype(np.float64)
+    t0 = t0[(t0 > 0).all(axis=1)]
+    if len(t0):
+        print(f"   wave start spread inside a workgroup: med={np.median(t0.max(1) - t0.min(1)):.0f} "
+              f"max={(t0.max(1) - t0.min(1)).max():.0f} ticks", flush=True)
     del r
