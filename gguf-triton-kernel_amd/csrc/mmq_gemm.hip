@@ -113,7 +113,11 @@ struct Cfg {
     // padding DMAs (instruction counts not a multiple of the wave count) land in a scratch KiB
     static constexpr bool PAD = W_REAL % NWAVE != 0 || A_REAL % NWAVE != 0;
     static constexpr int NAS_FIT = (LDS_MAX - (PAD ? 1024 : 0) - NWS * W_SLOT) / A_SLOT;
-    static constexpr int NAS = NAS_FIT < 4 * NWS - 4 ? NAS_FIT : 4 * NWS - 4;
+#ifndef GQ_GEMM_NAS_CAP // activation ring depth cap: 4 measured best (Q4_K 4096^2 x128: 6 slots
+#define GQ_GEMM_NAS_CAP 4  // 19.6 us, 4 slots 18.8, 3 slots 19.4; Q6_K x128: 3 slots +15%)
+#endif
+    static constexpr int NAS_MAX = 4 * NWS - 4 < GQ_GEMM_NAS_CAP ? 4 * NWS - 4 : GQ_GEMM_NAS_CAP;
+    static constexpr int NAS = NAS_FIT < NAS_MAX ? NAS_FIT : NAS_MAX;
     static constexpr int A_BASE = NWS * W_SLOT, SCRATCH = A_BASE + NAS * A_SLOT; // dummy DMAs land there
     static constexpr int LDS_BYTES = SCRATCH + (PAD ? 1024 : 0);
     static_assert((BM * NPW % 64 == 0 && (BN * 8) % 64 == 0) || BN * 8 < 64, "whole DMA instructions");
