@@ -105,11 +105,12 @@ struct Cfg {
     static constexpr int A_REAL = BN * 8 / 64 > 0 ? BN * 8 / 64 : 1;
     static constexpr int NW = (W_REAL + NWAVE - 1) / NWAVE, NA = (A_REAL + NWAVE - 1) / NWAVE; // per wave
     static constexpr int W_SLOT = W_REAL * 1024, A_SLOT = A_REAL * 1024;
-    // activation sub-stage ring: 4 slots (3 in flight) unless the LDS budget says 3
-    // weight-stage ring: NWS-1 super-blocks ahead (3, or 2 for Q8_0's 34 KiB stages so that
-    // the activation ring can be deeper); activation ring: as deep as the LDS allows, at most
-    // 4*NWS-4 slots (W(w) must be issued before A(4w): see the pipeline note below)
-    static constexpr int NWS = F == Q8_0 ? 2 : 3;
+    // activation sub-stage ring: as deep as the LDS allows, at most 4*NWS-4 slots (W(w) must
+    // be issued before A(4w): see the pipeline note below) and GQ_GEMM_NAS_CAP.  Two weight
+    // slots (one super-block ahead): at kernel start every workgroup's prologue DMAs are issued
+    // together, and a smaller burst lands the first sub-stage sooner (three slots measured
+    // 6-9% slower on every K-quant shape; tools/gemm_stamps.py)
+    static constexpr int NWS = 2;
     // padding DMAs (instruction counts not a multiple of the wave count) land in a scratch KiB
     static constexpr bool PAD = W_REAL % NWAVE != 0 || A_REAL % NWAVE != 0;
     static constexpr int NAS_FIT = (LDS_MAX - (PAD ? 1024 : 0) - NWS * W_SLOT) / A_SLOT;
