@@ -548,6 +548,7 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p)
         g.lp2 = lp2;
     } else {
         const int64_t unit64 = fmt == Q8_0 ? 64 * 68 : (fmt == Q4_K ? 64 * 36 : 64 * 210 / 4);
+        if (cap < unit64) return false; // a 64-unit segment must fit one task (tuning builds with small NI)
         g.G = 1;
         g.segu = (int)(64 * (cap / unit64));
         g.nseg = (int)((upr + g.segu - 1) / g.segu);
