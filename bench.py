@@ -9,16 +9,23 @@ timing; the steps cycle through >= 1 GiB of distinct weight copies so the 256 MB
 Infinity Cache cannot serve them.  K steps are captured into one hipGraph and replayed;
 time = HIP events around the replay, bracketed by barrier + synchronize.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME] [--sweep] [--no-cpu]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME] [--strong] [--quick] [--no-cpu]
 
-N > 1 (torch.distributed.run, one rank per GPU, RCCL): weak scaling of the row-sharded
-layer -- every rank owns an N_out-row shard of an (N * N_out)-row weight matrix, runs the
-step on it and all-gathers the fp16 output shards over xGMI (RCCL all_gather, overlapped
-with the next step's compute).  value = all ranks' FLOPs / max-over-ranks time.
+N > 1 (torch.distributed.run, one rank per GPU, RCCL): the row-sharded matmul of
+dist/row_shard.py (RowShardedMMQ: local MMQ on the rank's rows, RCCL all_gather of the fp16
+output slabs over xGMI, overlapped with the next step's compute, assembled to (N, M)).
+  default   weak scaling: every rank owns an N_out-row shard of an (N * N_out)-row matrix;
+            value = all ranks' FLOPs / max-over-ranks time.  The line also carries
+            "strong": the Q6_K Llama-70B matrices (BASELINE configs[3]) at fixed global size,
+            split over the N ranks, compute-only and end-to-end.
+  --strong  the headline itself is the strong-scaling Q6_K 28672x8192 (M_tok 128) run.
 
 Extra JSON fields: roofline (dominant kernel = the MMQ launch, timed alone with HIP events
-in its own graph), cpu_baseline (oracle/ C restatement of kernels/cpu_impls, one thread,
-bounded row sample, rank 0 at N=1 only), sweep (other BASELINE configs with --sweep).
+in its own graph), cpu_baseline (oracle/ C restatement of kernels/cpu_impls, rank 0 at N=1
+only: all host cores (row slices), plus the 1-thread literal port and the product's own
+vectorised CPU MMQ in cpu_baseline_variants), sweep (every GGUF type at M=1 and M=128 on the
+BASELINE shapes incl. the down projections, the Q4_K_M layer and the token sweep; --quick
+skips it).
 """
 from __future__ import annotations
 
@@ -49,9 +56,14 @@ CONFIGS = {
     "q4_k_11008x4096_m1": ("q4_k", 11008, 4096, 1),
     "q4_k_11008x4096_m16": ("q4_k", 11008, 4096, 16),
     "q4_k_11008x4096_m128": ("q4_k", 11008, 4096, 128),
-    "q6_k_28672x8192_m1": ("q6_k", 28672, 8192, 1),
+    "q4_k_4096x11008_m1": ("q4_k", 4096, 11008, 1),     # Llama-7B ffn_down
+    "q4_k_4096x11008_m128": ("q4_k", 4096, 11008, 128),
+    "q6_k_28672x8192_m1": ("q6_k", 28672, 8192, 1),     # Llama-70B ffn_gate/up
     "q6_k_28672x8192_m128": ("q6_k", 28672, 8192, 128),
+    "q6_k_8192x28672_m1": ("q6_k", 8192, 28672, 1),     # Llama-70B ffn_down
+    "q6_k_8192x28672_m128": ("q6_k", 8192, 28672, 128),
 }
+STRONG = ("q6_k_28672x8192_m1", "q6_k_28672x8192_m128")  # BASELINE configs[3]: row-sharded over the ranks
 DEFAULT = "q8_0_4096x4096_m128"
 BLOCK = {"q8_0": (32, 34), "q4_k": (256, 144), "q6_k": (256, 210)}
 GTYPE = {"q8_0": 0, "q4_k": 1, "q6_k": 2}
@@ -187,72 +199,289 @@ def load_traffic(name):
     return None
 
 
-def cpu_baseline(fmt, M, K, N, target_s=12.0):
-    """oracle/ C restatement of kernels/cpu_impls (the reference's arithmetic), one thread,
-    on the first R weight rows x all N tokens; R sized for ~target_s of CPU work."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
-    from utils.synth import random_activations, random_blocks
-    qk, nbytes = BLOCK[fmt]
-    B = random_activations(N, K, seed=1)
-    Bq = O.quantize_q8_1(B)
+def host_cores() -> int:
+    """Host threads for the CPU baseline: the process's affinity set, capped at 16 (the GPU
+    box gives one GPU's job a 16-core share; OMP_NUM_THREADS says the same there)."""
+    n = len(os.sched_getaffinity(0))
+    cap = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    return max(1, min(n, cap, 16))
+
+
+# The reference's own CPU path (kernels/cpu_impls, Python loops) measured in the survey
+# container (SURVEY.md 6): ms per (weight row x token) at K = 4096.
+REF_CPU_MS_PER_ROW_TOKEN = {"q8_0": 4.29, "q4_k": 7.63, "q6_k": 18.52}
+
+
+def _timed_rows(run, M, target_s):
+    """Grow a row count until run(rows) takes ~target_s (or all M rows); -> (rows, seconds)."""
     rows = 1
     while True:
-        A = random_blocks(fmt, rows, K, seed=2)
         t0 = time.perf_counter()
-        O.mmq(fmt, A, Bq, rows, N, K, O.EXACT)
+        run(rows)
         dt = time.perf_counter() - t0
-        if dt > 0.5 or rows >= M:
+        if dt > 0.25 * target_s or rows >= M:
             break
         rows = min(M, rows * 4)
     if dt < target_s and rows < M:
         rows = min(M, max(rows, int(rows * target_s / max(dt, 1e-6))))
-        A = random_blocks(fmt, rows, K, seed=2)
         t0 = time.perf_counter()
-        O.mmq(fmt, A, Bq, rows, N, K, O.EXACT)
+        run(rows)
         dt = time.perf_counter() - t0
-    tflops = 2.0 * rows * N * K / dt / 1e12
-    return {"value": tflops, "unit": "TFLOP/s", "cores": 1, "kind": "port",
-            "sample": f"{fmt} rows 0..{rows - 1} of N_out={M} x all {N} tokens, K={K}: oracle/mmq_oracle.c "
-                      f"mode EXACT (kernels/cpu_impls arithmetic, fp16 running sum), 1 thread, {dt:.2f} s; "
-                      f"extrapolated full step {dt * M / rows:.1f} s",
-            "seconds": round(dt, 3), "rows": rows}
+    return rows, dt
 
 
-def bench_config(name, steps, warmup, dev, dist_on, world, rank):
+def cpu_baseline(fmt, M, K, N, target_s=6.0):
+    """The reference's CPU arithmetic on the host cores, on a bounded row sample of the
+    workload (all N tokens, the first R weight rows; R sized for ~target_s per leg):
+      main     oracle/mmq_oracle.c EXACT (restatement of kernels/cpu_impls), row slices
+               over host_cores() threads (ctypes drops the GIL; outputs independent);
+      variants the same oracle on 1 thread (the reference's literal loop order), and the
+               product's vectorised C++ CPU MMQ (kernels.cpu_impls drop-in, libgguf_quant)
+               on all cores -- bit-identical outputs, different speed."""
+    from concurrent.futures import ThreadPoolExecutor
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from kernels.cpu_impls._cpu import cpu_mmq
+    from utils.synth import random_activations, random_blocks
+    cores = host_cores()
+    B = random_activations(N, K, seed=1)
+    Bq = O.quantize_q8_1(B)
+    qk, nbytes = BLOCK[fmt]
+    row_bytes = (K // qk) * nbytes
+    A_all = random_blocks(fmt, min(M, 4096), K, seed=2)
+
+    def rows_of(r):
+        reps = -(-r // (A_all.size // row_bytes))
+        return np.tile(A_all, reps)[:r * row_bytes] if reps > 1 else A_all[:r * row_bytes]
+
+    def oracle_mt(r):
+        A = rows_of(r)
+        per = -(-r // cores)
+        chunks = [(i, min(r, i + per)) for i in range(0, r, per)]
+        with ThreadPoolExecutor(cores) as ex:
+            list(ex.map(lambda c: O.mmq(fmt, A[c[0] * row_bytes:c[1] * row_bytes], Bq, c[1] - c[0], N, K, O.EXACT),
+                        chunks))
+
+    def oracle_1(r):
+        O.mmq(fmt, rows_of(r), Bq, r, N, K, O.EXACT)
+
+    Bt = torch.from_numpy(Bq.view(np.int8))
+
+    def product_mt(r):
+        cpu_mmq(GTYPE[fmt], torch.from_numpy(rows_of(r).view(np.int8)), Bt, r, N, K, threads=cores)
+
+    def leg(run, kind, threads, what):
+        r, dt = _timed_rows(run, M, target_s)
+        return {"value": 2.0 * r * N * K / dt / 1e12, "unit": "TFLOP/s", "cores": threads, "kind": kind,
+                "sample": f"{fmt} rows 0..{r - 1} of N_out={M} x all {N} tokens, K={K}: {what}, {threads} "
+                          f"thread(s), {dt:.2f} s; extrapolated full step {dt * M / r:.2f} s",
+                "seconds": round(dt, 3), "rows": r, "ms_per_row_token": round(dt * 1e3 / (r * N), 5)}
+
+    main = leg(oracle_mt, "port", cores, "oracle/mmq_oracle.c mode EXACT (kernels/cpu_impls arithmetic, "
+                                         "fp16 running sum), row slices over threads")
+    one = leg(oracle_1, "port", 1, "oracle/mmq_oracle.c mode EXACT, the reference's loop order")
+    vec = leg(product_mt, "port", cores, "kernels.cpu_impls drop-in (csrc/quant/gguf_cpu_mmq.cpp: rows unpacked "
+                                         "once, vectorised int8 dots, same outputs bit for bit)")
+    ref = REF_CPU_MS_PER_ROW_TOKEN[fmt] * K / 4096.0
+    main["reference_python_ms_per_row_token"] = round(ref, 3)
+    main["reference_python_source"] = ("kernels/cpu_impls Python loops measured in the survey container "
+                                       "(SURVEY.md 6), scaled to this K; 1 thread")
+    main["speedup_1thread_port_vs_reference_python"] = round(ref / one["ms_per_row_token"], 1)
+    return main, [one, vec]
+
+
+class ShardedRunner:
+    """One rank's part of a row-sharded step: RowShardedMMQ over rotating copies of this rank's
+    packed rows (>= 1 GiB), the local MMQ through the C ABI into a padded slab (graph-capturable:
+    preallocated workspace, torch's current stream), then the RCCL all_gather + assemble."""
+
+    def __init__(self, fmt, M_global, K, N, dev, world, rank, seed=0):
+        import kernels._lib as kl
+        from dist.row_shard import RowShardedMMQ, shard_rows
+        self.L = kl.lib()
+        self.fmt, self.K, self.N, self.dev, self.world = fmt, K, N, dev, world
+        self.row0, self.rows, self.R = shard_rows(M_global, world, rank)
+        qk, nbytes = BLOCK[fmt]
+        wbytes = max(1, self.rows * (K // qk) * nbytes)
+        self.ncopies = max(2, math.ceil(ROTATE_BYTES / wbytes))
+        base = device_random_blocks(fmt, max(self.rows, 1), K, dev, seed + rank)[:self.rows * (K // qk) * nbytes]
+        self.ws_bytes = max(1, kl.workspace_size(GTYPE[fmt], max(self.rows, 1), N, K))
+        self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=dev)
+        self.parts = [RowShardedMMQ(fmt, base if c == 0 else base.clone(), M_global, K, align=64,
+                                    compute=self._compute, world=world, rank=rank) for c in range(self.ncopies)]
+        g = torch.Generator(device=dev).manual_seed(seed + 1)
+        self.B = torch.randn(N, K, device=dev, generator=g).to(torch.float16)
+        self.slab = [torch.zeros(N, self.R, dtype=torch.float16, device=dev) for _ in range(2)]
+        self.gathered = [torch.empty(world, N, self.R, dtype=torch.float16, device=dev) for _ in range(2)]
+        self.gtype = GTYPE[fmt]
+
+    def _compute(self, A_shard, B, rows, N, K, out):
+        rc = self.L.gq_mmq(self.gtype, A_shard.data_ptr(), B.data_ptr(), out.data_ptr(), rows, N, K, K,
+                           out.stride(0), self.ws.data_ptr(), self.ws_bytes,
+                           torch.cuda.current_stream(self.dev).cuda_stream)
+        if rc:
+            raise RuntimeError(self.L.gq_last_error().decode())
+
+    def local(self, i):
+        self.parts[i % self.ncopies].local(self.B, self.N, self.slab[i & 1])
+
+    def capture(self, n, first=0):
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(s):
+            self.local(first)
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        torch.cuda.synchronize(self.dev)
+        with torch.cuda.graph(g):
+            for i in range(n):
+                self.local(first + i)
+        return g
+
+    def capture_e2e(self, n):
+        """One graph of n whole steps: local MMQ on the compute stream; the all_gather (RCCL,
+        captured) and the assemble on a side stream, so step i's exchange overlaps step i+1's
+        compute; slab j is rewritten only after the exchange that read it (events)."""
+        part = self.parts[0]
+        side = torch.cuda.Stream(self.dev)
+        done = [torch.cuda.Event() for _ in range(2)]
+        out = [None, None]
+
+        def body(i):
+            if i >= 2:
+                torch.cuda.current_stream(self.dev).wait_event(done[i & 1])
+            self.local(i)
+            side.wait_stream(torch.cuda.current_stream(self.dev))
+            with torch.cuda.stream(side):
+                part.gather(self.slab[i & 1], self.gathered[i & 1])
+                out[i & 1] = part.assemble(self.gathered[i & 1])
+                done[i & 1].record(side)
+
+        s = torch.cuda.Stream(self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(s):  # warm every op outside capture (RCCL communicator included)
+            for i in range(2):
+                body(i)
+            s.wait_stream(side)
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        torch.cuda.synchronize(self.dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for i in range(n):
+                body(i)
+            torch.cuda.current_stream(self.dev).wait_stream(side)
+        return g
+
+    def end_to_end(self, steps):
+        """(seconds for `steps` whole steps -- local MMQ + all_gather + assemble -- max over
+        ranks, how it ran).  The steps are one captured graph (RCCL collectives captured);
+        for a backend that cannot be captured (gloo rehearsals), an eager loop: per step a one-step graph replay and an async
+        all_gather on RCCL's stream, one exchange in flight behind the next step's compute."""
+        import torch.distributed as dist
+        if dist.is_initialized() and dist.get_backend() == "nccl":  # RCCL collectives are capturable
+            g = self.capture_e2e(steps)
+            g.replay()
+            t = min(timed_replay(g, self.dev, True) for _ in range(3))
+            return t, "graph"
+        # (a failed capture leaves the stream poisoned, so no try: other backends run eagerly)
+        how = f"eager ({dist.get_backend() if dist.is_initialized() else 'no'} backend: not capturable)"
+        one = [self.capture(1, j) for j in range(2)]
+        part = self.parts[0]
+
+        def run(n):
+            works = []
+            for i in range(n):
+                one[i & 1].replay()
+                _, w = part.gather(self.slab[i & 1], self.gathered[i & 1], async_op=True)
+                works.append((w, i & 1))
+                if len(works) > 1:
+                    w0, j = works.pop(0)
+                    if w0 is not None:
+                        w0.wait()
+                    part.assemble(self.gathered[j])
+            for w0, j in works:
+                if w0 is not None:
+                    w0.wait()
+                part.assemble(self.gathered[j])
+
+        run(4)
+        if dist.is_initialized():
+            dist.barrier()
+        torch.cuda.synchronize(self.dev)
+        t0 = time.perf_counter()
+        run(steps)
+        torch.cuda.synchronize(self.dev)
+        t = time.perf_counter() - t0
+        if dist.is_initialized():
+            tt = torch.tensor([t], device=self.dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dist.barrier()
+            t = float(tt.item())
+        return t, how
+
+
+def dist_backend():
+    import torch.distributed as dist
+    b = dist.get_backend() if dist.is_initialized() else "none"
+    return "nccl = RCCL over xGMI" if b == "nccl" else b
+
+
+def bench_sharded(name, steps, warmup, dev, dist_on, world, rank, M_global=None):
+    """Row-sharded run of config `name` over the ranks: M_global rows in total (default: the
+    config's N_out, i.e. strong scaling; weak scaling passes world * N_out)."""
     fmt, M, K, N = CONFIGS[name]
-    r = Runner(fmt, M, K, N, dev, steps, seed=rank)
-    # full step graph (act quant + mmq); warmup graph separately sized
+    Mg = M_global or M
+    r = ShardedRunner(fmt, Mg, K, N, dev, world, rank, seed=0)
+    gw = r.capture(max(1, warmup))
+    gw.replay()
+    g = r.capture(steps)
+    g.replay()
+    t_c = min(timed_replay(g, dev, dist_on) for _ in range(3))
+    t_e, how = r.end_to_end(steps) if dist_on else (t_c, "graph (1 rank: no exchange)")
+    _, _, flops = model(fmt, Mg, K, N)
+    qk, nbytes = BLOCK[fmt]
+    wbytes = Mg * (K // qk) * nbytes
+    out = {"config": name, "fmt": fmt, "N_out_global": Mg, "K": K, "M_tok": N, "ranks": world,
+           "rows_per_rank": r.R, "ms_per_step": t_e / steps * 1e3, "compute_ms_per_step": t_c / steps * 1e3,
+           "tflops": flops / (t_e / steps) / 1e12, "compute_only_tflops": flops / (t_c / steps) / 1e12,
+           "weight_GBps": wbytes / (t_e / steps) / 1e9, "weight_copies": r.ncopies,
+           "collective": (f"all_gather_into_tensor (backend {dist_backend()}) + assemble" if dist_on
+                          else "none (1 rank)"), "timed_as": how}
+    del r, g, gw
+    torch.cuda.empty_cache()
+    return out
+
+
+def bench_config(name, steps, warmup, dev):
+    """One config on this GPU: the drop-in step (gq_mmq) timed over a graph of `steps` calls,
+    and the dominant kernel for the roofline."""
+    fmt, M, K, N = CONFIGS[name]
+    r = Runner(fmt, M, K, N, dev, steps)
     gw = r.capture(r.step, max(1, warmup))
     gw.replay()
     torch.cuda.synchronize(dev)
-    if dist_on and world > 1:
-        t, t_compute = bench_dist(r, steps, dev, world)
-    else:
-        g = r.capture(r.step, steps)
-        g.replay()  # first replay pays lazy init
-        t = min(timed_replay(g, dev, dist_on) for _ in range(3))
-        t_compute = t
+    g = r.capture(r.step, steps)
+    g.replay()  # first replay pays lazy init
+    t = min(timed_replay(g, dev) for _ in range(3))
     # dominant kernel: decode (N <= 4) -- the step IS one launch (fused quantizer + weight
     # stream), so its time is the step's; GEMM -- the MMQ call alone (gemm_kernel [+ split-K
     # reduce]) with the activations prepared once, K launches in a graph
     if N <= 4:
-        t_k = (t_compute if dist_on and world > 1 else t) / steps
+        t_k = t / steps
         kname = "stream_decode_kernel (fused q8_1 + decode)"
     else:
         r.prepare()
         gk = r.capture(r.kernel, steps)
         gk.replay()
-        t_k = min(timed_replay(gk, dev, dist_on) for _ in range(3)) / steps
+        t_k = min(timed_replay(gk, dev) for _ in range(3)) / steps
         kname = "gemm_kernel (+ gemm_reduce_kernel when split-K)"
     wbytes, alg_bytes, flops = model(fmt, M, K, N)
     per_step = t / steps
     out = {
         "config": name, "fmt": fmt, "N_out": M, "K": K, "M_tok": N,
         "ms_per_step": per_step * 1e3,
-        "tflops": world * flops / per_step / 1e12,
-        "weight_GBps": world * wbytes / per_step / 1e9,
-        "compute_only_tflops": world * flops / (t_compute / steps) / 1e12,
+        "tflops": flops / per_step / 1e12,
+        "weight_GBps": wbytes / per_step / 1e9,
         "roofline": dict(roofline(fmt, M, K, N, t_k, load_traffic(name)), kernel=kname),
         "weight_copies": r.ncopies,
     }
@@ -316,39 +545,14 @@ def bench_msweep(steps, warmup, dev, fmt="q4_k", M=4096, K=4096):
     return {"config": f"{fmt}_{M}x{K}_msweep", "points": res}
 
 
-def bench_dist(r, steps, dev, world):
-    """Each step: MMQ on the local row shard, then all_gather of the (N, N_out) fp16 shards
-    into (world, N, N_out) on a side stream (RCCL), overlapped with the next step."""
-    import torch.distributed as dist
-    gathered = [torch.empty(world, r.N, r.M, dtype=torch.float16, device=dev) for _ in range(2)]
-    gstep = [r.capture(lambda i, j=j: r.step(j), 1) for j in range(2)]
-
-    def run(n):
-        works = []
-        for i in range(n):
-            gstep[i & 1].replay()
-            works.append(dist.all_gather_into_tensor(gathered[i & 1].view(world * r.N, r.M), r.C[i & 1],
-                                                     async_op=True))
-            if len(works) > 1:
-                works.pop(0).wait()
-        for w in works:
-            w.wait()
-
-    run(4)
-    dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    run(steps)
-    torch.cuda.synchronize(dev)
-    t = time.perf_counter() - t0
-    # compute only
-    g = r.capture(r.step, steps)
-    g.replay()
-    tc = timed_replay(g, dev, True)
-    tt = torch.tensor([t], device=dev)
-    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    dist.barrier()
-    return float(tt.item()), tc
+def compact(e):
+    """A sweep entry with the roofline reduced to its fraction and kernel time."""
+    o = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in e.items() if k != "roofline"}
+    if e.get("roofline"):
+        rf = e["roofline"]
+        o["roofline"] = {"bound": rf["bound"], "frac": rf["frac"], "achieved": rf["achieved"], "unit": rf["unit"],
+                         "kernel_us": rf["kernel_us"]}
+    return o
 
 
 def main():
@@ -357,38 +561,63 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default=DEFAULT, choices=sorted(CONFIGS))
-    ap.add_argument("--sweep", action="store_true", help="also measure the other BASELINE configs")
+    ap.add_argument("--strong", action="store_true", help="headline = strong scaling of Q6_K 28672x8192 x128")
+    ap.add_argument("--quick", action="store_true", help="headline only: no per-type sweep")
+    ap.add_argument("--sweep", action="store_true", help="(the default; kept for old command lines)")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist_on = world > 1
+    # BENCH_FORCE_DIST=1: the distributed code path even at world 1 (exercises RCCL graph
+    # capture on a 1-GPU box)
+    dist_on = world > 1 or os.environ.get("BENCH_FORCE_DIST") == "1"
+    # BENCH_BACKEND=gloo: rehearsal of the N > 1 path with every rank on the visible GPUs
+    # round-robin (e.g. 2 ranks on a 1-GPU box); the product path is "nccl" = RCCL over xGMI
+    backend = os.environ.get("BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
+    dev = torch.device("cuda", local)
     if dist_on:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(dev)
+    name = STRONG[1] if args.strong else args.config
+    fmt, M, K, N = CONFIGS[name]
+    sweep_steps = max(20, args.steps // 4)
 
-    head = bench_config(args.config, args.steps, args.warmup, dev, dist_on, world, rank)
+    if args.strong:
+        head = bench_sharded(name, args.steps, args.warmup, dev, dist_on, world, rank)
+        R = head["rows_per_rank"]
+        head["roofline"] = dict(roofline(fmt, R, K, N, head["compute_ms_per_step"] / 1e3),
+                                kernel="per-rank local step on its R rows (act quant + MMQ), compute only")
+    elif dist_on:
+        head = bench_sharded(name, args.steps, args.warmup, dev, dist_on, world, rank, M_global=world * M)
+        head["roofline"] = dict(roofline(fmt, M, K, N, head["compute_ms_per_step"] / 1e3),
+                                kernel="per-rank local step (act quant + MMQ), compute only")
+    else:
+        head = bench_config(name, args.steps, args.warmup, dev)
+    strong = []
+    if dist_on and not args.strong:
+        for sname in STRONG:
+            strong.append(bench_sharded(sname, sweep_steps, args.warmup, dev, dist_on, world, rank))
     sweep = []
-    if args.sweep:
-        for name in CONFIGS:
-            if name != args.config:
-                sweep.append(bench_config(name, max(20, args.steps // 4), args.warmup, dev, dist_on, world, rank))
-        if not dist_on:
-            for n in (1, 128):
-                sweep.append(bench_layer(n, max(20, args.steps // 4), args.warmup, dev))
-            sweep.append(bench_msweep(max(20, args.steps // 4), args.warmup, dev))
-    cpu = None
+    if not args.quick and not args.strong and not dist_on:
+        for sname in CONFIGS:
+            if sname != name:
+                sweep.append(bench_config(sname, sweep_steps, args.warmup, dev))
+        for n in (1, 128):
+            sweep.append(bench_layer(n, sweep_steps, args.warmup, dev))
+        sweep.append(bench_msweep(sweep_steps, args.warmup, dev))
+    cpu, cpu_var = None, None
     if rank == 0 and world == 1 and not args.no_cpu:
-        fmt, M, K, N = CONFIGS[args.config]
-        cpu = cpu_baseline(fmt, M, K, N)
+        cpu, cpu_var = cpu_baseline(fmt, M, K, N)
 
     if rank == 0:
-        fmt, M, K, N = CONFIGS[args.config]
         line = {
             "metric": "effective fp16 TFLOPS (+ quant-weight GB/s) per GGUF type",
             "value": round(head["tflops"], 3),
@@ -398,22 +627,29 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(head["ms_per_step"], 6),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "f16" if N > 4 else "i8",
             "arith": "q8_1 activations x dequantized GGUF weights on fp16 MFMA, fp32 accumulate" if N > 4 else
                      "q8_1 int8 activations x GGUF int codes on v_dot4_i32_i8, fp32 block scaling",
             "data": "synthetic (random packed blocks, N(0,1) fp16 activations)",
-            "config": {"workload": args.config, "gguf_type": fmt, "N_out": M, "K": K, "M_tok": N,
-                       "global_N_out": M * world, "parallelism": f"rowshard{world}" if world > 1 else "single",
+            "config": {"workload": name, "gguf_type": fmt, "N_out": M, "K": K, "M_tok": N,
+                       "global_N_out": M if args.strong else M * world,
+                       "parallelism": f"rowshard{world}" if world > 1 else "single",
                        "weight_copies_rotated": head["weight_copies"]},
             "weight_GBps": round(head["weight_GBps"], 1),
-            "compute_only_tflops": round(head["compute_only_tflops"], 3),
             "roofline": head["roofline"],
             "cpu_baseline": cpu,
         }
+        if "compute_only_tflops" in head:
+            line["compute_only_tflops"] = round(head["compute_only_tflops"], 3)
+            line["compute_ms_per_step"] = round(head["compute_ms_per_step"], 6)
+        if cpu_var:
+            line["cpu_baseline_variants"] = cpu_var
+        if strong:
+            line["strong"] = [compact(e) for e in strong]
         if sweep:
-            line["sweep"] = [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in s.items()} for s in sweep]
+            line["sweep"] = [compact(e) for e in sweep]
         print(json.dumps(line), flush=True)
     if dist_on:
         torch.distributed.destroy_process_group()

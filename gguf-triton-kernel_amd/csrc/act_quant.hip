@@ -15,6 +15,8 @@
 //   SOA  : codes int8 [rows][K] + d float [rows][K/32] + s float [rows][K/32] -- GEMV input
 //   DEQ  : x~ = fp16(d * q) [rows][K] -- the dequantized activation fed to the fp16 MFMA GEMM,
 //          each 4-element group stored in the order (0,2,1,3) (see mmq_gemm.hip)
+//   I8   : codes int8 [rows][K] + d float BLOCK-major [K/32][ld] (ld = rows rounded up to 4) --
+//          the int8-MFMA GEMM's input: one tile's d of a K block is one contiguous run
 #include "gguf_blocks.hpp"
 #include "gguf_internal.hpp"
 #include "gguf_q8_1.hpp"
@@ -52,6 +54,9 @@ __global__ __launch_bounds__(256) void act_quant_kernel(const uint16_t *__restri
             dout[row * nb + j] = q.d;
             sout[row * nb + j] = h2f(q.sbits);
         }
+    } else if constexpr (MODE == ACT_I8) {
+        *(u32x2 *)(codes + row * K + 32 * j + 8 * sub) = (u32x2){q.codes[0], q.codes[1]};
+        if (sub == 0) dout[j * ((rows + 3) & ~(int64_t)3) + row] = q.d;
     } else {
         // x~ = fp16(d*q); each 4-element group in the order (0,2,1,3): the order mmq_gemm.hip's
         // packed dequantization produces weight pairs in (its k-permutation; the MFMA k-sum is
@@ -83,6 +88,10 @@ hipError_t launch_act_quant(int mode, const uint16_t *X, int64_t ldx, int64_t ro
     case ACT_SOA:
         act_quant_kernel<ACT_SOA><<<grid, block, 0, s>>>(X, ldx, rows, K, nullptr, (int8_t *)out0, (float *)out1,
                                                           (float *)out2, nullptr);
+        break;
+    case ACT_I8:
+        act_quant_kernel<ACT_I8><<<grid, block, 0, s>>>(X, ldx, rows, K, nullptr, (int8_t *)out0, (float *)out1,
+                                                         nullptr, nullptr);
         break;
     default:
         act_quant_kernel<ACT_DEQ><<<grid, block, 0, s>>>(X, ldx, rows, K, nullptr, nullptr, nullptr, nullptr,

@@ -5,10 +5,11 @@
 
 namespace gq {
 
-enum ActMode : int { ACT_AOS = 0, ACT_SOA = 1, ACT_DEQ = 2 };
+enum ActMode : int { ACT_AOS = 0, ACT_SOA = 1, ACT_DEQ = 2, ACT_I8 = 3 };
 
 // Activation quantizer (act_quant.hip).  AOS: out0 = q8_1 bytes.  SOA: out0 = int8 codes
 // [rows][K], out1 = float d [rows][K/32], out2 = float s [rows][K/32].  DEQ: out0 = fp16 x~.
+// I8: out0 = int8 codes [rows][K], out1 = float d [K/32][(rows + 3) & ~3] (block-major).
 hipError_t launch_act_quant(int mode, const uint16_t *X, int64_t ldx, int64_t rows, int64_t K, void *out0,
                             void *out1, void *out2, hipStream_t s);
 
@@ -28,13 +29,22 @@ struct GemmPlan {
     int nb = 8;                // 16-token groups per workgroup (tile = 16*nb tokens)
     int rg = 2;                // 16-row groups per wave (8 waves: tile = 128*rg weight rows)
     int splits = 1;            // split-K factor (grid.z)
-    int chunks_per_split = 1;  // 128-wide K stages per split
+    int chunks_per_split = 1;  // 256-wide K stages (super-blocks) per split
+    bool i8 = false;           // Q8_0 only: int8 activations x int8 weights on v_mfma_i32_16x16x32_i8
     size_t partial_bytes = 0;  // fp32 partial slabs needed when splits > 1
 };
-// The MFMA GEMM needs K in whole 128-element stages (always true for Q4_K/Q6_K).
+// Activations as the GEMM reads them: fp16 x~ (act_quant DEQ) or, for plan.i8, int8 codes +
+// block-major fp32 d (act_quant I8).
+struct GemmAct {
+    const uint16_t *xdeq = nullptr;
+    const int8_t *xq = nullptr;
+    const float *xd = nullptr;
+};
+// The MFMA GEMM needs K in whole 256-element stages (always true for Q4_K/Q6_K).
 bool gemm_supported(int fmt, int64_t K);
-GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K);
-hipError_t launch_gemm(int fmt, const uint8_t *A, const uint16_t *xdeq, uint16_t *C, float *partials,
+// i8: request the int8-MFMA form (honoured for Q8_0 only).
+GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, bool i8 = false);
+hipError_t launch_gemm(int fmt, const uint8_t *A, const GemmAct &x, uint16_t *C, float *partials,
                        const GemmPlan &plan, int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
 
 // Dequantization and the library GEMM (mmq_dequant.hip).  perm: store 4-groups as (0,2,1,3),

@@ -50,6 +50,21 @@ int64_t blas_min_tokens()
 }
 bool use_blas(int64_t N, int64_t K) { return !use_gemv(N, K) && N >= blas_min_tokens(); }
 
+// Q8_0 on the MFMA GEMM path: int8 activations x int8 weights (v_mfma_i32_16x16x32_i8 + per-block
+// fp32 scaling) instead of fp16 x~ x dequantized weights.  GQ_GEMM_I8=0/1 overrides.
+bool use_i8(int t, int64_t N, int64_t K)
+{
+    if (t != GQ_Q8_0 || use_gemv(N, K) || use_blas(N, K)) return false;
+    const char *e = getenv("GQ_GEMM_I8");
+    return e ? atoi(e) != 0 : false;
+}
+
+// GEMM-path activation forms in the workspace: fp16 x~ [N][K], then (int8 form) codes [N][K]
+// and block-major d [K/32][(N+3)&~3].
+size_t deq_bytes(int64_t N, int64_t K) { return align_up((size_t)N * K * 2); }
+size_t i8_code_bytes(int64_t N, int64_t K) { return align_up((size_t)N * K); }
+size_t i8_d_bytes(int64_t N, int64_t K) { return align_up((size_t)(K / 32) * (size_t)((N + 3) & ~(int64_t)3) * 4); }
+
 // Activation part of the workspace (what gq_act_prepare writes); depends on N, K only.
 size_t act_bytes(int64_t N, int64_t K)
 {
@@ -57,7 +72,7 @@ size_t act_bytes(int64_t N, int64_t K)
         // SOA q8_1: codes + d + s
         return align_up((size_t)N * K) + 2 * align_up((size_t)N * (K / 32) * sizeof(float));
     }
-    return align_up((size_t)N * K * 2); // dequantized fp16 activation
+    return deq_bytes(N, K) + i8_code_bytes(N, K) + i8_d_bytes(N, K);
 }
 
 // Whole workspace: activations + (GEMM split-K) fp32 partial slabs.
@@ -65,7 +80,7 @@ size_t ws_bytes(int t, int64_t M, int64_t N, int64_t K)
 {
     size_t b = act_bytes(N, K);
     if (use_blas(N, K)) b += align_up((size_t)M * K * 2) + gq::blas_workspace_bytes(); // fp16 W + hipBLASLt
-    else if (!use_gemv(N, K)) b += align_up(gq::plan_gemm(t, M, N, K).partial_bytes);
+    else if (!use_gemv(N, K)) b += align_up(gq::plan_gemm(t, M, N, K, use_i8(t, N, K)).partial_bytes);
     return b;
 }
 
@@ -95,8 +110,8 @@ static int check_common(gq_type t, int64_t M, int64_t N, int64_t K)
 }
 
 struct Carved {
-    int8_t *xq;
-    float *xd, *xs;
+    int8_t *xq;       // SOA codes (decode) / int8-form codes (GEMM)
+    float *xd, *xs;   // SOA d, s (decode) / int8-form block-major d (GEMM)
     uint16_t *xdeq;
     float *partials;
 };
@@ -111,13 +126,16 @@ static Carved carve(void *workspace, int64_t N, int64_t K)
         c.xs = (float *)((uint8_t *)c.xd + align_up((size_t)N * (K / 32) * sizeof(float)));
     } else {
         c.xdeq = (uint16_t *)ws;
+        c.xq = (int8_t *)(ws + deq_bytes(N, K));
+        c.xd = (float *)(ws + deq_bytes(N, K) + i8_code_bytes(N, K));
         c.partials = (float *)(ws + act_bytes(N, K));
     }
     return c;
 }
 
+// forms: bit 0 = fp16 x~ (DEQ), bit 1 = int8 codes + d (I8); only the GEMM path reads them
 static int prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *workspace, size_t workspace_bytes,
-                   hipStream_t s)
+                   hipStream_t s, int forms = 1)
 {
     if (!B) return fail(GQ_EINVAL, "null activation pointer");
     if (ldb < K) return fail(GQ_EINVAL, "ldb=%lld < K=%lld", (long long)ldb, (long long)K);
@@ -125,9 +143,14 @@ static int prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *works
     if (!workspace || workspace_bytes < need)
         return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace ? workspace_bytes : (size_t)0, need);
     Carved c = carve(workspace, N, K);
-    hipError_t e = use_gemv(N, K) ? gq::launch_act_quant(gq::ACT_SOA, (const uint16_t *)B, ldb, N, K, c.xq, c.xd, c.xs, s)
-                               : gq::launch_act_quant(gq::ACT_DEQ, (const uint16_t *)B, ldb, N, K, c.xdeq, nullptr,
-                                                      nullptr, s);
+    hipError_t e = hipSuccess;
+    if (use_gemv(N, K)) {
+        e = gq::launch_act_quant(gq::ACT_SOA, (const uint16_t *)B, ldb, N, K, c.xq, c.xd, c.xs, s);
+    } else {
+        if (forms & 1) e = gq::launch_act_quant(gq::ACT_DEQ, (const uint16_t *)B, ldb, N, K, c.xdeq, nullptr, nullptr, s);
+        if (e == hipSuccess && (forms & 2))
+            e = gq::launch_act_quant(gq::ACT_I8, (const uint16_t *)B, ldb, N, K, c.xq, c.xd, nullptr, s);
+    }
     if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (act_quant): %s", hipGetErrorString(e));
     return GQ_OK;
 }
@@ -149,9 +172,17 @@ static int compute(gq_type t, const void *A, void *workspace, size_t workspace_b
         if (rc != 0) return fail(GQ_EHIP, "hipBLASLt GEMM failed (code %d)", rc);
         return GQ_OK;
     }
-    hipError_t e = use_gemv(N, K) ? gq::launch_gemv(t, (const uint8_t *)A, c.xq, c.xd, c.xs, (uint16_t *)C, M, N, K, ldc, s)
-                               : gq::launch_gemm(t, (const uint8_t *)A, c.xdeq, (uint16_t *)C, c.partials,
-                                                 gq::plan_gemm(t, M, N, K), M, N, K, ldc, s);
+    hipError_t e;
+    if (use_gemv(N, K)) {
+        e = gq::launch_gemv(t, (const uint8_t *)A, c.xq, c.xd, c.xs, (uint16_t *)C, M, N, K, ldc, s);
+    } else {
+        gq::GemmAct x;
+        x.xdeq = c.xdeq;
+        x.xq = c.xq;
+        x.xd = c.xd;
+        e = gq::launch_gemm(t, (const uint8_t *)A, x, (uint16_t *)C, c.partials,
+                            gq::plan_gemm(t, M, N, K, use_i8(t, N, K)), M, N, K, ldc, s);
+    }
     if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (mmq): %s", hipGetErrorString(e));
     return GQ_OK;
 }
@@ -177,7 +208,7 @@ int gq_mmq(gq_type t, const void *A, const void *B, void *C, int64_t M, int64_t 
         if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (decode): %s", hipGetErrorString(e));
         return GQ_OK;
     }
-    rc = prepare(B, N, K, ldb, workspace, workspace_bytes, (hipStream_t)stream);
+    rc = prepare(B, N, K, ldb, workspace, workspace_bytes, (hipStream_t)stream, use_i8(t, N, K) ? 2 : 1);
     if (rc != GQ_OK) return rc;
     return compute(t, A, workspace, workspace_bytes, C, M, N, K, ldc, (hipStream_t)stream);
 }
@@ -189,7 +220,10 @@ int gq_act_prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *works
     if (N < 0 || K < 0) return fail(GQ_EINVAL, "negative size");
     if (K % 32 != 0) return fail(GQ_EINVAL, "K=%lld is not a multiple of 32", (long long)K);
     if (N == 0 || K == 0) return GQ_OK;
-    return prepare(B, N, K, ldb, workspace, workspace_bytes, (hipStream_t)stream);
+    // the weight type is not known here: write every form a later gq_mmq_prepared may read
+    // (the int8 form only when Q8_0 would use it)
+    return prepare(B, N, K, ldb, workspace, workspace_bytes, (hipStream_t)stream,
+                   use_i8(GQ_Q8_0, N, K) ? 3 : 1);
 }
 
 int gq_mmq_prepared(gq_type t, const void *A, void *workspace, size_t workspace_bytes, void *C, int64_t M, int64_t N,

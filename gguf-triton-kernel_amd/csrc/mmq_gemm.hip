@@ -1,4 +1,4 @@
-// mmq_gemm.hip -- batched MMQ (many tokens) on the fp16 matrix cores, LDS-DMA staged.
+// mmq_gemm.hip -- batched MMQ (many tokens) on the matrix cores, LDS-DMA staged.
 //
 // C[t][m] = sum_k W[m][k] * x~[t][k]: W dequantized in registers from the packed GGUF bytes,
 // x~ = fp16(d*q) the q8_1-quantized activation (act_quant.hip, DEQ form) -- the integer
@@ -6,27 +6,35 @@
 // v_mfma_f32_16x16x32_f16 with fp32 accumulation.  fp16 rather than bf16: the reference's
 // activations are fp16 and bf16 would drop three of their mantissa bits.
 //
-// Workgroup = 4 waves = BM = 64*RG weight rows x BN = 16*NB tokens.  Wave w owns rows
+// Q8_0 has a second form (I8 = true, act_quant I8 form): the q8_1 codes and the weight codes
+// go into v_mfma_i32_16x16x32_i8 as they are (one 32-element block = one MFMA k-step, the
+// reference's int dot, mmq_q8_0.py:85-88), and every block's int32 tile is scaled by
+// dA[row]*dB[token] into the fp32 accumulators -- no weight dequantization, half the
+// activation bytes, four VALU ops per output per block.
+//
+// Workgroup = 8 waves = BM = 128*RG weight rows x BN = 16*NB tokens.  Wave w owns rows
 // 16*(RG*w + rg) + [0,16) (rg < RG) and every token of the tile: each weight is dequantized
 // once per workgroup; the activation tile is shared through LDS.  Large BM matters: every
 // stage moves 2*BN bytes of activations per K element beside BM*bytes/weight of weights, and
 // the per-CU L2->LDS rate, not the MFMA, is what a small tile runs into.
 //
-// K advances in stages of 64 elements (2 MFMA k-steps of 32).  Everything a stage needs is
-// moved HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4: no VGPRs, no ds_write):
-//   weights     : per row the stage's raw block bytes (Stage<F> below), 16-byte pieces at
+// K advances in activation sub-stages of 64 elements (2 MFMA k-steps of 32) and weight stages
+// of one super-block (256 elements, Q8_0: 8 blocks).  Everything is moved HBM/L2 -> LDS by
+// LDS-DMA (global_load_lds_dwordx4: no VGPRs, no ds_write):
+//   weights     : per row the stage's raw block bytes (WStage<F> below), 16-byte pieces at
 //                 whatever (2-byte) alignment the blocks have (gfx950 runs unaligned);
-//   activations : BN token rows x 128 B, 16-byte pieces XOR-swizzled by ((row >> 1) & 7) on
-//                 the SOURCE side (the DMA destination is lane-linear) so the MFMA
-//                 fragment ds_read_b128s of a 16-lane group hit 16 distinct bank quads.
-// A ring of 4 stage buffers keeps three stages in flight while one is multiplied; one
-// s_barrier per stage, preceded by a counted vmcnt (never vmcnt(0) inside the loop).
+//   activations : BN token rows x 128 B (I8: x 64 B of codes + the tile's d), 16-byte pieces
+//                 XOR-swizzled on the SOURCE side (the DMA destination is lane-linear) so the
+//                 MFMA fragment reads of a lane group hit distinct banks.
+// Two weight-stage slots and an activation ring of up to 4 slots (Cfg below) keep the next
+// sub-stages in flight while one is multiplied; one s_barrier per sub-stage, preceded by a
+// counted vmcnt (never vmcnt(0) inside the loop).
 //
-// MFMA 16x16x32 f16 maps (gfx950): lane l holds A[row l&15][k 8(l>>4)+j] and
+// MFMA 16x16x32 (f16 and i8) maps (gfx950): lane l holds A[row l&15][k 8(l>>4)+j] and
 // B[k 8(l>>4)+j][col l&15]; D[row 4(l>>4)+i][col l&15] in acc element i.  Weight rows are the
 // A rows and tokens the B columns, so lane l ends with 4 consecutive weight rows of one token:
 // one 8-byte store per (row group, token group) in the epilogue.
-// The 8 k of a fragment are taken in the element order (0,2,1,3,4,6,5,7) in which packed
+// The 8 k of an f16 fragment are taken in the element order (0,2,1,3,4,6,5,7) in which packed
 // dequantization produces them; act_quant's DEQ form stores x~ in the same order.
 #include <cstdlib>
 #include <type_traits>
@@ -45,6 +53,7 @@ namespace {
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int KC = 64;     // K elements per stage
@@ -96,13 +105,17 @@ __device__ __forceinline__ uint32_t act_voff(int p) // byte offset of piece p (8
 
 constexpr int NWAVE = 8; // 512 threads: two waves per SIMD
 
-template <int F, int NB, int RG = 1>
+template <int F, int NB, int RG = 1, bool I8 = false>
 struct Cfg {
     // 128*RG weight rows x 16*NB tokens; wave w owns rows 16*(RG*w + rg) + [0, 16), rg < RG
     static constexpr int BN = 16 * NB, BM = 16 * NWAVE * RG;
     static constexpr int RBW = WStage<F>::RBW, NPW = RBW / 16;
     static constexpr int W_REAL = BM * NPW / 64;                              // DMA instructions per stage
-    static constexpr int A_REAL = BN * 8 / 64 > 0 ? BN * 8 / 64 : 1;
+    // I8 activation sub-stage: BN x 64 code bytes (CI instructions), then one instruction for
+    // the tile's d of the sub-stage's two blocks (2 x BN floats)
+    static constexpr int CI = BN * 64 / 1024 > 0 ? BN * 64 / 1024 : 1;
+    static constexpr int A_REAL = I8 ? CI + 1 : (BN * 8 / 64 > 0 ? BN * 8 / 64 : 1);
+    static constexpr int D_OFF = CI * 1024; // I8: byte offset of the d floats in a slot
     static constexpr int NW = (W_REAL + NWAVE - 1) / NWAVE, NA = (A_REAL + NWAVE - 1) / NWAVE; // per wave
     static constexpr int W_SLOT = W_REAL * 1024, A_SLOT = A_REAL * 1024;
     // activation sub-stage ring: as deep as the LDS allows, at most 4*NWS-4 slots (W(w) must
@@ -122,6 +135,7 @@ struct Cfg {
     static constexpr int A_BASE = NWS * W_SLOT, SCRATCH = A_BASE + NAS * A_SLOT; // dummy DMAs land there
     static constexpr int LDS_BYTES = SCRATCH + (PAD ? 1024 : 0);
     static_assert((BM * NPW % 64 == 0 && (BN * 8) % 64 == 0) || BN * 8 < 64, "whole DMA instructions");
+    static_assert(!I8 || (F == Q8_0 && RG == 1 && BN <= 128), "int8 form: Q8_0, 128-row tiles, <= 128 tokens");
     static_assert(LDS_BYTES <= LDS_MAX, "LDS budget");
     static_assert(NAS >= 3, "activation ring depth");
     static_assert((NAS - 2) * NA + 2 * NW <= 63, "vmcnt range");
@@ -202,6 +216,9 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, uint8_t *lds_
 }
 
 __device__ __forceinline__ int act_swz(int r) { return (r >> 1) & 7; }
+// I8 code rows are 64 B (four 16-byte pieces): piece q of token r lands in piece q ^ i8_swz(r),
+// so the 8-byte fragment reads of 16 tokens x 2 k-groups cover all 64 banks once.
+__device__ __forceinline__ int i8_swz(int r) { return (r >> 2) & 3; }
 
 // Source of the padding DMAs that keep every wave's instruction count equal: the tensor's first
 // bytes (an L2 hit), written to a scratch slot.  (Out-of-range buffer offsets would return
@@ -221,12 +238,14 @@ constexpr uint32_t DUMMY = 0u;
 // bytes into the same slot) so every wave issues the same sequence.
 // ABL: ablation bitmask for performance diagnosis (diagnostic build -DGQ_ABLATION only; 0 in
 // production): 1 = no MFMA, 2 = no weight DMA, 4 = no activation DMA, 8 = no dequantization.
-template <int F, int NB, int RG, int ABL = 0>
-__global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
-                                                   uint16_t *__restrict__ C, float *__restrict__ P, int64_t M,
-                                                   int64_t N, int64_t K, int64_t ldc, int wstages_per_split)
+// I8 (Q8_0): X = int8 codes [N][K], XD = block-major d [K/32][ldd]; otherwise X = fp16 x~.
+template <int F, int NB, int RG, int ABL = 0, bool I8 = false>
+__global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A, const void *__restrict__ X,
+                                                   const float *__restrict__ XD, uint16_t *__restrict__ C,
+                                                   float *__restrict__ P, int64_t M, int64_t N, int64_t K,
+                                                   int64_t ldc, int wstages_per_split)
 {
-    using G = Cfg<F, NB, RG>;
+    using G = Cfg<F, NB, RG, I8>;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[G::LDS_BYTES];
 #ifdef GQ_GEMM_STAMPS
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
@@ -249,8 +268,11 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
     // never past the 16-byte granule (hence never the page) that byte lives in.
     const __amdgpu_buffer_rsrc_t wrs =
         __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, (int)(uint32_t)((M * row_bytes + 15) & ~(int64_t)15), 0x00020000);
-    const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, (int)(uint32_t)(N * K * 2),
-                                                                         0x00020000);
+    const __amdgpu_buffer_rsrc_t ars =
+        __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, (int)(uint32_t)(N * K * (I8 ? 1 : 2)), 0x00020000);
+    const int64_t ldd = (N + 3) & ~(int64_t)3; // I8: row length of the block-major d array
+    const __amdgpu_buffer_rsrc_t drs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)XD, 0, I8 ? (int)(uint32_t)((K / 32) * ldd * 4) : 0, 0x00020000);
 
     // weight DMA: instruction k = wave + 8i moves pieces p = 64k + lane: row p / NPW, piece p % NPW
     uint32_t wv[G::NW];
@@ -262,13 +284,28 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
         const int64_t row = m0 + r < M ? m0 + r : M - 1;
         wv[i] = r < G::BM ? (uint32_t)(row * row_bytes) : DUMMY;
     }
-    // activation DMA: instruction k moves pieces p = 64k + lane: token p >> 3, slot p & 7
+    // activation DMA: instruction k moves pieces p = 64k + lane: token p >> 3, slot p & 7.
+    // I8: code instructions k < CI move pieces p: token p >> 2, piece p & 3 (swizzle i8_swz);
+    // instruction CI moves the d of the sub-stage's two blocks: lanes [0, BN/4) block 0, the
+    // next BN/4 block 1, four tokens per lane.
     uint32_t av[G::NA];
 #pragma unroll
     for (int i = 0; i < G::NA; ++i) {
-        const int p = 64 * (wave + NWAVE * i) + lane, r = p >> 3, q = p & 7;
-        const int64_t tok = n0 + r < N ? n0 + r : N - 1;
-        av[i] = r < G::BN ? (uint32_t)(tok * K * 2) + act_voff<F>(q ^ act_swz(r)) : DUMMY;
+        const int k = wave + NWAVE * i, p = 64 * k + lane;
+        if constexpr (I8) {
+            if (k < G::CI) {
+                const int r = p >> 2, q = p & 3;
+                const int64_t tok = n0 + r < N ? n0 + r : N - 1;
+                av[i] = r < G::BN ? (uint32_t)(tok * K) + 16u * (uint32_t)(q ^ i8_swz(r)) : DUMMY;
+            } else {
+                const int b = lane / (G::BN / 4), j = lane - b * (G::BN / 4);
+                av[i] = k == G::CI && b < 2 ? (uint32_t)((b * ldd + n0 + 4 * j) * 4) : DUMMY;
+            }
+        } else {
+            const int r = p >> 3, q = p & 7;
+            const int64_t tok = n0 + r < N ? n0 + r : N - 1;
+            av[i] = r < G::BN ? (uint32_t)(tok * K * 2) + act_voff<F>(q ^ act_swz(r)) : DUMMY;
+        }
     }
     const int myrow = 16 * RG * wave + l16; // the row this lane multiplies (row group 0)
 
@@ -295,7 +332,13 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
 #pragma unroll
         for (int i = 0; i < G::NA; ++i) {
             const int k = wave + NWAVE * i;
-            dma16(ars, k < G::A_REAL ? dst + 1024 * k : lds + G::SCRATCH, av[i], act_soff<F>(a));
+            uint8_t *d = k < G::A_REAL ? dst + 1024 * k : lds + G::SCRATCH;
+            if constexpr (I8) {
+                if (k < G::CI) dma16(ars, d, av[i], (uint32_t)(64 * a));
+                else dma16(drs, d, av[i], (uint32_t)(8 * a * ldd)); // d of blocks 2a, 2a+1
+            } else {
+                dma16(ars, d, av[i], act_soff<F>(a));
+            }
         }
     };
     // vmcnt for "A(a) landed": (NAS-2) younger A's + the W's issued after A(a)
@@ -351,6 +394,37 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
 
             const uint8_t *wr = lds + (int)(w % G::NWS) * G::W_SLOT + G::RBW * myrow;
             const uint8_t *xs = lds + G::A_BASE + (int)(a % G::NAS) * G::A_SLOT;
+            if constexpr (I8) {
+                // int8 form: per block b of the sub-stage one i8 MFMA per token tile, the int32
+                // tile scaled by dA[row] * dB[token] into the fp32 accumulators
+                const uint8_t *wq = wr - G::RBW * l16 + G::RBW * 4 * g; // row 16*wave + 4g (+i)
+                long aq[2], bq[2][NB];
+                float da[2][4], db[2][NB];
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    const int boff = 34 * (2 * s4 + b);
+                    aq[b] = __builtin_bit_cast(long, *(const u32x2 *)(wr + boff + 2 + 8 * g));
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) da[b][i] = h2f(*(const uint16_t *)(wq + G::RBW * i + boff));
+#pragma unroll
+                    for (int t = 0; t < NB; ++t) {
+                        const int r = 16 * t + l16;
+                        bq[b][t] = __builtin_bit_cast(
+                            long, *(const u32x2 *)(xs + 64 * r + 16 * ((2 * b + (g >> 1)) ^ i8_swz(r)) + 8 * (g & 1)));
+                        db[b][t] = *(const float *)(xs + G::D_OFF + 4 * (G::BN * b + r));
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int t = 0; t < NB; ++t) {
+                        const i32x4 pi = __builtin_amdgcn_mfma_i32_16x16x32_i8(aq[b], bq[b][t], (i32x4){0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) acc[0][t][i] = __builtin_fmaf((float)pi[i], da[b][i] * db[b][t], acc[0][t][i]);
+                    }
+                continue;
+            }
             // all of the sub-stage's activation fragments first (one LDS round trip), the
             // dequantization beside them, then the MFMAs
             f16x8 bfr[2][NB];
@@ -503,27 +577,26 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restric
     }
 }
 
-template <int F, int NB, int RG>
-hipError_t launch_cfg(const uint8_t *A, const uint16_t *X, uint16_t *C, float *P, const GemmPlan &pl, int64_t M,
+template <int F, int NB, int RG, bool I8 = false>
+hipError_t launch_cfg(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P, const GemmPlan &pl, int64_t M,
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
-    using G = Cfg<F, NB, RG>;
+    using G = Cfg<F, NB, RG, I8>;
     dim3 grid((unsigned)((M + G::BM - 1) / G::BM), (unsigned)((N + G::BN - 1) / G::BN), (unsigned)pl.splits);
     float *PP = pl.splits > 1 ? P : nullptr;
     const int cps = pl.chunks_per_split;
+    const void *X = I8 ? (const void *)x.xq : (const void *)x.xdeq;
 #ifdef GQ_ABLATION
     const int abl = getenv("GQ_ABLATE") ? atoi(getenv("GQ_ABLATE")) : 0;
+#define GQ_ABL_CASE(v) \
+    case v: gemm_kernel<F, NB, RG, v, I8><<<grid, dim3(512), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, cps); break;
     switch (abl) {
-    case 1: gemm_kernel<F, NB, RG, 1><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
-    case 6: gemm_kernel<F, NB, RG, 6><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
-    case 8: gemm_kernel<F, NB, RG, 8><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
-    case 15: gemm_kernel<F, NB, RG, 15><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
-    case 16: gemm_kernel<F, NB, RG, 16><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
-    case 31: gemm_kernel<F, NB, RG, 31><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
-    default: gemm_kernel<F, NB, RG><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps); break;
+    GQ_ABL_CASE(1) GQ_ABL_CASE(6) GQ_ABL_CASE(8) GQ_ABL_CASE(15) GQ_ABL_CASE(16) GQ_ABL_CASE(31)
+    default: gemm_kernel<F, NB, RG, 0, I8><<<grid, dim3(512), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, cps); break;
     }
+#undef GQ_ABL_CASE
 #else
-    gemm_kernel<F, NB, RG><<<grid, dim3(512), 0, s>>>(A, X, C, PP, M, N, K, ldc, cps);
+    gemm_kernel<F, NB, RG, 0, I8><<<grid, dim3(512), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, cps);
 #endif
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || pl.splits == 1) return e;
@@ -534,16 +607,23 @@ hipError_t launch_cfg(const uint8_t *A, const uint16_t *X, uint16_t *C, float *P
 }
 
 template <int F>
-hipError_t launch_fmt(const uint8_t *A, const uint16_t *X, uint16_t *C, float *P, const GemmPlan &pl, int64_t M,
+hipError_t launch_fmt(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P, const GemmPlan &pl, int64_t M,
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
     if constexpr (F == Q4_K)
-        if (pl.rg == 2 && pl.nb == 8) return launch_cfg<F, 8, 2>(A, X, C, P, pl, M, N, K, ldc, s);
+        if (pl.rg == 2 && pl.nb == 8) return launch_cfg<F, 8, 2>(A, x, C, P, pl, M, N, K, ldc, s);
+    if constexpr (F == Q8_0)
+        if (pl.i8) switch (pl.nb) {
+            case 1: return launch_cfg<F, 1, 1, true>(A, x, C, P, pl, M, N, K, ldc, s);
+            case 2: return launch_cfg<F, 2, 1, true>(A, x, C, P, pl, M, N, K, ldc, s);
+            case 4: return launch_cfg<F, 4, 1, true>(A, x, C, P, pl, M, N, K, ldc, s);
+            default: return launch_cfg<F, 8, 1, true>(A, x, C, P, pl, M, N, K, ldc, s);
+            }
     switch (pl.nb) {
-    case 1: return launch_cfg<F, 1, 1>(A, X, C, P, pl, M, N, K, ldc, s);
-    case 2: return launch_cfg<F, 2, 1>(A, X, C, P, pl, M, N, K, ldc, s);
-    case 4: return launch_cfg<F, 4, 1>(A, X, C, P, pl, M, N, K, ldc, s);
-    default: return launch_cfg<F, 8, 1>(A, X, C, P, pl, M, N, K, ldc, s);
+    case 1: return launch_cfg<F, 1, 1>(A, x, C, P, pl, M, N, K, ldc, s);
+    case 2: return launch_cfg<F, 2, 1>(A, x, C, P, pl, M, N, K, ldc, s);
+    case 4: return launch_cfg<F, 4, 1>(A, x, C, P, pl, M, N, K, ldc, s);
+    default: return launch_cfg<F, 8, 1>(A, x, C, P, pl, M, N, K, ldc, s);
     }
 }
 
@@ -553,10 +633,10 @@ int pick_nb(int64_t N) { return N > 64 ? 8 : (N > 32 ? 4 : (N > 16 ? 2 : 1)); }
 
 bool gemm_supported(int /*fmt*/, int64_t K) { return K > 0 && K % 256 == 0; }
 
-GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K)
+GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, bool i8)
 {
-    (void)fmt;
     GemmPlan p;
+    p.i8 = i8 && fmt == Q8_0;
     p.nb = pick_nb(N);
     if (const char *env = getenv("GQ_GEMM_NB")) p.nb = atoi(env);
     // two 16-row groups per wave (256-row tiles: half the activation traffic per weight) for
@@ -584,13 +664,13 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K)
     return p;
 }
 
-hipError_t launch_gemm(int fmt, const uint8_t *A, const uint16_t *X, uint16_t *C, float *P, const GemmPlan &plan,
+hipError_t launch_gemm(int fmt, const uint8_t *A, const GemmAct &x, uint16_t *C, float *P, const GemmPlan &plan,
                        int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
     switch (fmt) {
-    case Q8_0: return launch_fmt<Q8_0>(A, X, C, P, plan, M, N, K, ldc, s);
-    case Q4_K: return launch_fmt<Q4_K>(A, X, C, P, plan, M, N, K, ldc, s);
-    default: return launch_fmt<Q6_K>(A, X, C, P, plan, M, N, K, ldc, s);
+    case Q8_0: return launch_fmt<Q8_0>(A, x, C, P, plan, M, N, K, ldc, s);
+    case Q4_K: return launch_fmt<Q4_K>(A, x, C, P, plan, M, N, K, ldc, s);
+    default: return launch_fmt<Q6_K>(A, x, C, P, plan, M, N, K, ldc, s);
     }
 }
 

@@ -54,13 +54,15 @@ class RowShardedMMQ:
     A_shard: this rank's packed rows (from shard_bytes), on this rank's device.
     compute(A_shard, B, rows, N, K, out) -> writes fp16 (N, rows) into `out`
     (default: the HIP MMQ through the C ABI).
+    world / rank: override the process group's (a shard of a G-way split driven outside a
+    group, e.g. all G shards on one device in a test); gather() needs the real group.
     """
 
     def __init__(self, fmt: str, A_shard: torch.Tensor, M: int, K: int, group=None, align: int = 64,
-                 compute: Optional[Callable] = None):
+                 compute: Optional[Callable] = None, world: Optional[int] = None, rank: Optional[int] = None):
         self.fmt, self.M, self.K, self.group = fmt, M, K, group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = world if world is not None else (dist.get_world_size(group) if dist.is_initialized() else 1)
+        self.rank = rank if rank is not None else (dist.get_rank(group) if dist.is_initialized() else 0)
         self.row0, self.rows, self.R = shard_rows(M, self.world, self.rank, align)
         qk, nbytes = BLOCK[fmt]
         assert A_shard.numel() == self.rows * (K // qk) * nbytes, "A_shard is not this rank's row range"
@@ -82,7 +84,9 @@ class RowShardedMMQ:
         N = slab.shape[0]
         if out is None:
             out = torch.empty(self.world, N, self.R, dtype=slab.dtype, device=slab.device)
-        if self.world == 1:
+        if not dist.is_initialized():
+            if self.world != 1:
+                raise RuntimeError("gather() needs an initialised process group for world > 1")
             out[0].copy_(slab)
             return out, None
         # concatenated (world*N, R) form: accepted by both RCCL and gloo

@@ -1,0 +1,125 @@
+"""GPU parity of the alternative paths behind the drop-in API, each against the oracle on the
+same inputs (run with `pytest -m gpu` on an MI355X):
+
+  * the Q8_0 int8-MFMA GEMM (GQ_GEMM_I8=1: q8_1 codes x weight codes on
+    v_mfma_i32_16x16x32_i8, per-block fp32 scaling) -- exact integer dots, so it is held to
+    the decode path's tight gate TIGHT_I8 = 1.5e-3 of max|C| against oracle IDEAL, and to the
+    reference's 1% gate against oracle EXACT (kernels/cpu_impls arithmetic);
+  * the prepared form (gq_act_prepare + gq_mmq_prepared) at every token count, including the
+    N <= 4 decode-shaped kernel the fused gq_mmq path does not use;
+  * row-sharded MMQ (dist/row_shard.py): the Q6_K Llama-70B matrices split into
+    G = 2, 4, 8 row shards, each shard run through RowShardedMMQ.local on this device,
+    assembled, compared with the oracle and bit for bit with the unsharded call.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from utils.synth import random_activations, random_blocks
+
+pytestmark = pytest.mark.gpu
+
+TIGHT_I8 = 1.5e-3
+TIGHT_GEMV = 1.5e-3
+TIGHT_GEMM = 4e-3
+
+
+def _dev():
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    return torch.device("cuda:0")
+
+
+def _run(fmt, qA, B, M, N, K):
+    from kernels._lib import TYPES, mmq
+    dev = _dev()
+    A_t = torch.from_numpy(np.ascontiguousarray(qA).view(np.int8)).to(dev)
+    B_t = torch.from_numpy(np.ascontiguousarray(B)).to(dev)
+    C = mmq(TYPES[fmt], A_t, B_t, M, N, K)
+    torch.cuda.synchronize()
+    return C.cpu().numpy()
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(128, 5, 256, None), (200, 16, 512, None), (130, 33, 768, "1"),
+                                          (64, 64, 1024, None), (300, 100, 2048, "3"), (256, 128, 4096, None),
+                                          (96, 128, 4096, "8"), (1000, 77, 1280, None)])
+def test_q8_0_int8_mfma_gemm(M, N, K, splits, monkeypatch):
+    monkeypatch.setenv("GQ_GEMM_I8", "1")
+    if splits:
+        monkeypatch.setenv("GQ_GEMM_SPLITS", splits)
+    qA = random_blocks("q8_0", M, K, seed=M + 3 * N)
+    B = random_activations(N, K, seed=K + N)
+    got = _run("q8_0", qA, B, M, N, K)
+    ideal = O.mmq_from_fp16("q8_0", qA, B, M, N, K, O.IDEAL)
+    err = O.max_rel_err(got, ideal)
+    assert err <= TIGHT_I8, (M, N, K, err)
+    exact = O.mmq_from_fp16("q8_0", qA, B, M, N, K, O.EXACT)
+    assert O.allclose(exact, got, 0.01)
+
+
+def test_q8_0_int8_mfma_golden(golden, monkeypatch):
+    """Every golden case of the reference through the int8 form (cases with N >= 5 run it)."""
+    monkeypatch.setenv("GQ_GEMM_I8", "1")
+    for c in golden["q8_0"]:
+        got = _run("q8_0", c["qA"], c["B"], c["M"], c["N"], c["K"])
+        if c["kind"] != "tiny":
+            assert O.allclose(c["C"], got, 0.01), (c["i"], c["kind"])
+        ideal = O.mmq("q8_0", c["qA"], c["qB"], c["M"], c["N"], c["K"], O.IDEAL)
+        assert O.max_rel_err(got, ideal) <= TIGHT_I8, (c["i"], c["kind"])
+
+
+@pytest.mark.parametrize("fmt", ("q8_0", "q4_k", "q6_k"))
+@pytest.mark.parametrize("N", (1, 2, 3, 4, 5, 16, 128))
+def test_prepared_matches_oracle(fmt, N):
+    """gq_act_prepare + gq_mmq_prepared (the LayerMix form) at every path's token counts."""
+    import kernels._lib as kl
+    dev = _dev()
+    M, K = 160, 1024
+    qA = random_blocks(fmt, M, K, seed=N + 5)
+    B = random_activations(N, K, seed=N + 6)
+    A_t = torch.from_numpy(qA.view(np.int8)).to(dev)
+    B_t = torch.from_numpy(B).to(dev)
+    g = kl.TYPES[fmt]
+    ws = torch.empty(kl.workspace_size(g, M, N, K), dtype=torch.uint8, device=dev)
+    kl.act_prepare(B_t, N, K, ws)
+    C = kl.mmq_prepared(g, A_t, ws, M, N, K).cpu().numpy()
+    ideal = O.mmq_from_fp16(fmt, qA, B, M, N, K, O.IDEAL)
+    assert O.max_rel_err(C, ideal) <= (TIGHT_GEMV if N <= 4 else TIGHT_GEMM), (fmt, N)
+    full = kl.mmq(g, A_t, B_t, M, N, K).cpu().numpy()
+    assert O.max_rel_err(C, full) <= 2 * TIGHT_GEMM
+
+
+@pytest.mark.parametrize("M,K", [(28672, 8192), (8192, 28672)])
+@pytest.mark.parametrize("G", (2, 4, 8))
+@pytest.mark.parametrize("N", (1, 128))
+def test_row_sharded_q6_k_70b(M, K, G, N, monkeypatch):
+    """Config 4: Q6_K Llama-70B ffn_gate/up (28672x8192) and ffn_down (8192x28672) split into G
+    row shards (zero-copy byte ranges), each run through RowShardedMMQ.local, assembled as the
+    all-gather would; vs the unsharded call (bit for bit, split-K off on both) and the oracle
+    on sampled rows."""
+    from dist.row_shard import RowShardedMMQ, shard_bytes
+    from kernels._lib import TYPES, mmq
+    monkeypatch.setenv("GQ_GEMM_SPLITS", "1")
+    dev = _dev()
+    qA = random_blocks("q6_k", M, K, seed=M + G)
+    B = random_activations(N, K, seed=N + K)
+    A_t = torch.from_numpy(qA.view(np.int8)).to(dev)
+    B_t = torch.from_numpy(B).to(dev)
+    full = mmq(TYPES["q6_k"], A_t, B_t, M, N, K)
+    slabs = []
+    for g in range(G):
+        part = RowShardedMMQ("q6_k", shard_bytes("q6_k", A_t, M, K, G, g), M, K, world=G, rank=g)
+        slabs.append(part.local(B_t, N))
+    gathered = torch.stack(slabs)  # what all_gather_into_tensor leaves: (G, N, R)
+    C = part.assemble(gathered)
+    torch.cuda.synchronize()
+    assert C.shape == (N, M)
+    assert torch.equal(C.view(torch.int16), full.view(torch.int16))
+    rows = np.sort(np.random.default_rng(G).choice(M, size=40, replace=False))
+    row_bytes = qA.size // M
+    sub = np.concatenate([qA[r * row_bytes:(r + 1) * row_bytes] for r in rows])
+    ideal = O.mmq_from_fp16("q6_k", sub, B, len(rows), N, K, O.IDEAL)
+    got = C.cpu().numpy()[:, rows]
+    assert O.max_rel_err(got, ideal) <= (TIGHT_GEMV if N <= 4 else TIGHT_GEMM)
+    exact = O.mmq_from_fp16("q6_k", sub, B, len(rows), N, K, O.EXACT)
+    assert O.allclose(exact, got, 0.01)
