@@ -508,18 +508,18 @@ def bench_layer(N, steps, warmup, dev):
     outs = {n: torch.empty(N, M, dtype=torch.float16, device=dev) for n, (M, K) in LLAMA_LAYER_SHAPES.items()}
     flops = sum(2.0 * N * M * K for M, K in LLAMA_LAYER_SHAPES.values())
     for i in range(max(1, warmup)):  # also creates any library handles outside capture
-        layers[i % ncopies].forward(x, h, outs)
+        layers[i % ncopies].forward(x, h, out=outs)
     torch.cuda.synchronize(dev)
     gr = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream(dev)
     s.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(s):
-        layers[0].forward(x, h, outs)
+        layers[0].forward(x, h, out=outs)
     torch.cuda.current_stream(dev).wait_stream(s)
     torch.cuda.synchronize(dev)
     with torch.cuda.graph(gr):
         for i in range(steps):
-            layers[i % ncopies].forward(x, h, outs)
+            layers[i % ncopies].forward(x, h, out=outs)
     gr.replay()
     t = min(timed_replay(gr, dev) for _ in range(3)) / steps
     return {"config": f"q4_k_m_llama7b_layer_m{N}", "fmt": "q4_k+q6_k", "M_tok": N, "ms_per_step": t * 1e3,

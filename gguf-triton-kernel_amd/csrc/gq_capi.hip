@@ -52,9 +52,33 @@ bool use_blas(int64_t N, int64_t K) { return !use_gemv(N, K) && N >= blas_min_to
 
 // Q8_0 on the MFMA GEMM path: int8 activations x int8 weights (v_mfma_i32_16x16x32_i8 + per-block
 // fp32 scaling) instead of fp16 x~ x dequantized weights.  GQ_GEMM_I8=0/1 overrides.
+// The MFMA GEMM addresses its operands with 32-bit buffer offsets: one launch covers at most
+// this many weight bytes and this many activation bytes; gemm_chunks() cuts larger calls into
+// row / token chunks (launched back to back on the stream, reusing the workspace).
+// (GQ_GEMM_MAX_BYTES lowers the limit: tests cut small calls into many chunks.)
+int64_t gemm_max_bytes()
+{
+    const char *e = getenv("GQ_GEMM_MAX_BYTES");
+    const int64_t lim = (int64_t)1 << 31;
+    const int64_t v = e ? atoll(e) : lim;
+    return v > 0 && v < lim ? v : lim;
+}
+int64_t row_bytes_of(int t, int64_t K) { return (K / block_elems(t)) * block_bytes(t); }
+int64_t gemm_rows_per_launch(int t, int64_t M, int64_t K)
+{
+    const int64_t r = gemm_max_bytes() / row_bytes_of(t, K) / 256 * 256; // whole 256-row tiles
+    return r < 256 ? 256 : (r < M ? r : M);
+}
+int64_t gemm_toks_per_launch(int64_t N, int64_t K)
+{
+    const int64_t n = gemm_max_bytes() / (2 * K) / 128 * 128; // whole 128-token tiles
+    return n < 16 ? 16 : (n < N ? n : N);
+}
+
 bool use_i8(int t, int64_t N, int64_t K)
 {
     if (t != GQ_Q8_0 || use_gemv(N, K) || use_blas(N, K)) return false;
+    if (gemm_toks_per_launch(N, K) < N) return false; // its block-major d is not token-chunked
     const char *e = getenv("GQ_GEMM_I8");
     return e ? atoi(e) != 0 : false;
 }
@@ -80,7 +104,18 @@ size_t ws_bytes(int t, int64_t M, int64_t N, int64_t K)
 {
     size_t b = act_bytes(N, K);
     if (use_blas(N, K)) b += align_up((size_t)M * K * 2) + gq::blas_workspace_bytes(); // fp16 W + hipBLASLt
-    else if (!use_gemv(N, K)) b += align_up(gq::plan_gemm(t, M, N, K, use_i8(t, N, K)).partial_bytes);
+    else if (!use_gemv(N, K)) {
+        // split-K partials of the largest need over the launch shapes (full and remainder chunks)
+        const int64_t mr = gemm_rows_per_launch(t, M, K), nt = gemm_toks_per_launch(N, K);
+        size_t p = 0;
+        for (int64_t mc : {mr, M % mr})
+            for (int64_t nc : {nt, N % nt})
+                if (mc > 0 && nc > 0) {
+                    const size_t q = gq::plan_gemm(t, mc, nc, K, use_i8(t, N, K)).partial_bytes;
+                    p = q > p ? q : p;
+                }
+        b += align_up(p);
+    }
     return b;
 }
 
@@ -176,12 +211,20 @@ static int compute(gq_type t, const void *A, void *workspace, size_t workspace_b
     if (use_gemv(N, K)) {
         e = gq::launch_gemv(t, (const uint8_t *)A, c.xq, c.xd, c.xs, (uint16_t *)C, M, N, K, ldc, s);
     } else {
-        gq::GemmAct x;
-        x.xdeq = c.xdeq;
-        x.xq = c.xq;
-        x.xd = c.xd;
-        e = gq::launch_gemm(t, (const uint8_t *)A, x, (uint16_t *)C, c.partials,
-                            gq::plan_gemm(t, M, N, K, use_i8(t, N, K)), M, N, K, ldc, s);
+        // chunks of < 2 GiB of weights and of activations per launch (32-bit buffer offsets)
+        const int64_t mr = gemm_rows_per_launch(t, M, K), nt = gemm_toks_per_launch(N, K);
+        const bool i8 = use_i8(t, N, K);
+        e = hipSuccess;
+        for (int64_t n0 = 0; n0 < N && e == hipSuccess; n0 += nt)
+            for (int64_t m0 = 0; m0 < M && e == hipSuccess; m0 += mr) {
+                const int64_t mc = M - m0 < mr ? M - m0 : mr, nc = N - n0 < nt ? N - n0 : nt;
+                gq::GemmAct x;
+                x.xdeq = c.xdeq + n0 * K;
+                x.xq = c.xq;
+                x.xd = c.xd;
+                e = gq::launch_gemm(t, (const uint8_t *)A + m0 * row_bytes_of(t, K), x, (uint16_t *)C + n0 * ldc + m0,
+                                    c.partials, gq::plan_gemm(t, mc, nc, K, i8), mc, nc, K, ldc, s);
+            }
     }
     if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (mmq): %s", hipGetErrorString(e));
     return GQ_OK;

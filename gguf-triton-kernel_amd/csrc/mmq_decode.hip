@@ -14,9 +14,10 @@
 // private, so a wave waits only on its own counted vmcnt -- no workgroup barrier in the loop.
 //
 // Activations.  The NT tokens are quantized to q8_1 (gguf_q8_1.hpp, bit-exact with
-// utils/quantize/q8_1.py) straight into LDS: the fp16 rows are LDS-DMA'd into each wave's
-// last ring slot FIRST (so waiting for them does not wait for the weight DMAs issued behind
-// them), quantized by the wave that staged them, and shared by one barrier.
+// utils/quantize/q8_1.py) straight into LDS: the fp16 values are loaded into registers (one
+// 16-byte load per lane, four lanes per 32-element block) ahead of the first weight DMA,
+// quantized by 4-lane DPP groups, written to LDS, and shared by one raw barrier (the second
+// ring slot's task is issued before it).  The C ABI routes N <= 4 tokens here (kGemvMaxTokens).
 //
 // Multiply.  Lane l takes unit u = l % P + P*i of a row (P = 64, or the power of two >= the
 // units per row for short rows, several rows per wave pass); it reads the unit's packed bytes

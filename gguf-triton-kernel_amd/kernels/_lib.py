@@ -71,29 +71,56 @@ def workspace_size(gtype: int, M: int, N: int, K: int) -> int:
     return int(lib().gq_mmq_workspace_size(gtype, M, N, K))
 
 
-def mmq(gtype: int, A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int,
-        out: torch.Tensor | None = None, workspace: torch.Tensor | None = None) -> torch.Tensor:
-    """C = (A @ B^T)^T as fp16 (N, M) on A's device; the common body of mmq_q8_0/q4_k/q6_k."""
+def _check_weights(gtype: int, A: torch.Tensor, M: int, K: int):
     qk, bb = BLOCK_ELEMS[gtype], BLOCK_BYTES[gtype]
     _require_device(A, "A")
-    _require_device(B, "B")
-    if A.device != B.device:
-        raise RuntimeError(f"A on {A.device} but B on {B.device}")
     if A.dtype not in (torch.int8, torch.uint8):
         raise RuntimeError(f"A must be the packed int8/uint8 block tensor, got {A.dtype}")
     if not A.is_contiguous():
         raise RuntimeError("A (packed blocks) must be contiguous")
     if A.numel() != M * (K // qk) * bb:
         raise RuntimeError(f"A has {A.numel()} bytes, expected M*K/{qk}*{bb} = {M * (K // qk) * bb}")
+
+
+def _check_acts(B: torch.Tensor, N: int, K: int) -> torch.Tensor:
+    """B as the fp16 (N, K) unit-column-stride tensor the ABI reads."""
+    _require_device(B, "B")
     if B.dtype != torch.float16:
         B = B.to(torch.float16)
     if B.dim() != 2 or B.shape[0] != N or B.shape[1] != K:
+        if B.numel() != N * K:
+            raise RuntimeError(f"B has {B.numel()} elements, expected N*K = {N * K}")
         B = B.reshape(N, K)
     if B.stride(1) != 1:
         B = B.contiguous()
-    C = out if out is not None else torch.empty((N, M), dtype=torch.float16, device=A.device)
+    return B
+
+
+def _check_out(out: torch.Tensor | None, N: int, M: int, dev) -> torch.Tensor:
+    C = out if out is not None else torch.empty((N, M), dtype=torch.float16, device=dev)
     if C.dtype != torch.float16 or C.dim() != 2 or C.stride(1) != 1 or C.shape[0] != N or C.shape[1] != M:
         raise RuntimeError("out must be an fp16 (N, M) tensor with unit column stride")
+    if C.device != dev:
+        raise RuntimeError(f"out on {C.device}, expected {dev}")
+    return C
+
+
+def _check_workspace(ws: torch.Tensor, need: int, dev):
+    if ws.device != dev or ws.dtype != torch.uint8 or not ws.is_contiguous():
+        raise RuntimeError("workspace must be a contiguous uint8 tensor on the weights' device")
+    if ws.numel() < need:
+        raise RuntimeError(f"workspace has {ws.numel()} bytes, this call needs {need}")
+
+
+def mmq(gtype: int, A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int,
+        out: torch.Tensor | None = None, workspace: torch.Tensor | None = None) -> torch.Tensor:
+    """C = (A @ B^T)^T as fp16 (N, M) on A's device; the common body of mmq_q8_0/q4_k/q6_k."""
+    _check_weights(gtype, A, M, K)
+    _require_device(B, "B")
+    if A.device != B.device:
+        raise RuntimeError(f"A on {A.device} but B on {B.device}")
+    B = _check_acts(B, N, K)
+    C = _check_out(out, N, M, A.device)
     if M == 0 or N == 0:
         return C
     need = workspace_size(gtype, M, N, K)
@@ -140,9 +167,8 @@ def dequantize_device(gtype: int, A: torch.Tensor, M: int, K: int) -> torch.Tens
 def act_prepare(B: torch.Tensor, N: int, K: int, workspace: torch.Tensor):
     """Quantize the activations once into the front of `workspace` (gq_act_prepare); any number
     of mmq_prepared calls with the same (N, K) then reuse them."""
-    _require_device(B, "B")
-    if B.dtype != torch.float16 or B.stride(-1) != 1:
-        B = B.to(torch.float16).contiguous()
+    B = _check_acts(B, N, K)
+    _check_workspace(workspace, 0, B.device)
     with torch.cuda.device(B.device):
         stream = torch.cuda.current_stream(B.device).cuda_stream
         _check(lib().gq_act_prepare(B.data_ptr(), N, K, B.stride(0), workspace.data_ptr(), workspace.numel(),
@@ -152,8 +178,11 @@ def act_prepare(B: torch.Tensor, N: int, K: int, workspace: torch.Tensor):
 def mmq_prepared(gtype: int, A: torch.Tensor, workspace: torch.Tensor, M: int, N: int, K: int,
                  out: torch.Tensor | None = None) -> torch.Tensor:
     """C (N, M) fp16 from packed A and the activations act_prepare left in `workspace`."""
-    _require_device(A, "A")
-    C = out if out is not None else torch.empty((N, M), dtype=torch.float16, device=A.device)
+    _check_weights(gtype, A, M, K)
+    _check_workspace(workspace, workspace_size(gtype, M, N, K), A.device)
+    C = _check_out(out, N, M, A.device)
+    if M == 0 or N == 0:
+        return C
     with torch.cuda.device(A.device):
         stream = torch.cuda.current_stream(A.device).cuda_stream
         _check(lib().gq_mmq_prepared(gtype, A.data_ptr(), workspace.data_ptr(), workspace.numel(), C.data_ptr(),

@@ -2,7 +2,7 @@
 
 BASELINE.json configs[4] / SURVEY.md 8(f)4 (no reference counterpart).  Each projection is a
 packed GGUF weight of its own type (gguf.mix.q4_k_m_layer_types); projections that share an
-input (q/k/v/o here, gate/up) quantize it once (gq_act_prepare) and run gq_mmq_prepared per
+input (q/k/v, gate/up) quantize it once (gq_act_prepare) and run gq_mmq_prepared per
 weight -- the dispatch is by type, per matrix, with no repacking.  At decode sizes (N <= 4)
 every call is the one-launch fused decode kernel instead (its quantizer is in-kernel).
 """
@@ -28,10 +28,13 @@ class GGUFLinear:
 
 
 class LayerMix:
-    """The seven projections of one Llama block: attn_q/k/v/output and ffn_gate/up read x
-    (K = 4096), ffn_down reads h (K = 11008).  forward(x, h) -> {name: (N, M) fp16}."""
+    """The seven projections of one Llama block, grouped by the input they read:
+    attn_q/k/v read the attention-normed hidden state x (K = 4096), attn_output the attention
+    output `attn`, ffn_gate/up the FFN-normed hidden state `x_ffn`, ffn_down the gated FFN
+    activation h (K = 11008).  forward(x, h, attn, x_ffn) -> {name: (N, M) fp16}; attn and
+    x_ffn default to x (the benchmark feeds one synthetic input to every K = 4096 group)."""
 
-    GROUPS = (("attn_q", "attn_k", "attn_v", "attn_output", "ffn_gate", "ffn_up"), ("ffn_down",))
+    GROUPS = (("attn_q", "attn_k", "attn_v"), ("attn_output",), ("ffn_gate", "ffn_up"), ("ffn_down",))
 
     def __init__(self, linears: dict):
         self.lin = linears
@@ -47,9 +50,11 @@ class LayerMix:
                 lins[name] = GGUFLinear(t.type_name, t.to_device(device), M, K)
         return cls(lins)
 
-    def forward(self, x: torch.Tensor, h: torch.Tensor, out: dict | None = None) -> dict:
+    def forward(self, x: torch.Tensor, h: torch.Tensor, attn: torch.Tensor | None = None,
+                x_ffn: torch.Tensor | None = None, out: dict | None = None) -> dict:
         res = {}
-        for group, inp in zip(self.GROUPS, (x, h)):
+        inputs = (x, x if attn is None else attn, x if x_ffn is None else x_ffn, h)
+        for group, inp in zip(self.GROUPS, inputs):
             N, K = inp.shape
             if N <= 4:  # decode: each call's kernel quantizes its tokens in LDS (one launch per weight)
                 for n in group:

@@ -61,7 +61,10 @@ int gq_mmq(gq_type t, const void *A, const void *B, void *C, int64_t M, int64_t 
  * type and M with that K, using the rest of the workspace (which must be at least
  * gq_mmq_workspace_size(t, M, N, K) bytes in total) for split-K partial sums.  One prepare
  * can serve several weight matrices that share an input (Q/K/V, gate/up).
- * gq_mmq(...) == gq_act_prepare(...) followed by gq_mmq_prepared(...).
+ * Same result as gq_mmq within the stated tolerances, not always the same kernels: for
+ * N <= 4 gq_mmq runs the one-launch fused decode kernel (quantizer in LDS) while the split
+ * form quantizes to the workspace and runs the decode-shaped GEMV; for Q8_0 with the int8
+ * GEMM form enabled (GQ_GEMM_I8=1) gq_act_prepare writes both activation forms.
  */
 int gq_act_prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *workspace, size_t workspace_bytes,
                    void *stream);

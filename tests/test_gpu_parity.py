@@ -111,7 +111,7 @@ def test_golden_cases(golden, fmt):
                                    (7, 8, 512), (33, 9, 256), (70, 16, 512), (129, 17, 768), (64, 64, 1024),
                                    (200, 130, 512), (96, 1, 2816)])
 def test_ragged_shapes(fmt, M, N, K):
-    """Tile edges of both paths (decode GEMV: N <= 8, MFMA GEMM: N > 8), odd row counts,
+    """Tile edges of both paths (decode: N <= 4, MFMA GEMM: N > 4), odd row counts,
     K that is not a multiple of the 2x256 K step."""
     qA = random_blocks(fmt, M, K, seed=M * 7 + N)
     B = random_activations(N, K, seed=K + N)
@@ -263,11 +263,13 @@ def test_blas_path(fmt, M, N, K, force, monkeypatch):
 
 
 def test_layer_mix_from_gguf(tmp_path):
-    """Q4_K_M-typed layer read from a GGUF file, shared-input groups quantized once."""
+    """Q4_K_M-typed layer read from a GGUF file; each projection group reads its own input
+    (x for q/k/v, the attention output for attn_output, the FFN input for gate/up, h for
+    ffn_down), shared-input groups quantized once."""
     from gguf import q4_k_m_layer_types, read_gguf, write_gguf
     from kernels.layer_mix import LayerMix
     types = q4_k_m_layer_types(0, 32)  # layer 0: attn_v / ffn_down in Q6_K
-    shapes = {n: (96, 512) for n in LayerMix.GROUPS[0]}
+    shapes = {n: (96, 512) for g in LayerMix.GROUPS[:3] for n in g}
     shapes["ffn_down"] = (64, 768)
     raw = {n: random_blocks(types[n], *shapes[n], seed=i) for i, n in enumerate(shapes)}
     p = tmp_path / "l.gguf"
@@ -275,12 +277,14 @@ def test_layer_mix_from_gguf(tmp_path):
     _, tens = read_gguf(p)
     layer = LayerMix.from_gguf(tens, 0, device=_dev())
     for N in (1, 20):
-        x = random_activations(N, 512, seed=N)
+        x, a, y = (random_activations(N, 512, seed=N + 10 * i) for i in range(3))
         h = random_activations(N, 768, seed=N + 1)
-        out = layer.forward(torch.from_numpy(x).to(_dev()), torch.from_numpy(h).to(_dev()))
+        d = {k: torch.from_numpy(v).to(_dev()) for k, v in (("x", x), ("a", a), ("y", y), ("h", h))}
+        out = layer.forward(d["x"], d["h"], attn=d["a"], x_ffn=d["y"])
         torch.cuda.synchronize()
+        src = {"attn_q": x, "attn_k": x, "attn_v": x, "attn_output": a, "ffn_gate": y, "ffn_up": y, "ffn_down": h}
         for n, (M, K) in shapes.items():
-            ideal = O.mmq_from_fp16(types[n], raw[n], x if K == 512 else h, M, N, K, O.IDEAL)
+            ideal = O.mmq_from_fp16(types[n], raw[n], src[n], M, N, K, O.IDEAL)
             assert O.max_rel_err(out[n].cpu().numpy(), ideal) <= tight(N), (n, N)
 
 

@@ -123,3 +123,51 @@ def test_row_sharded_q6_k_70b(M, K, G, N, monkeypatch):
     assert O.max_rel_err(got, ideal) <= (TIGHT_GEMV if N <= 4 else TIGHT_GEMM)
     exact = O.mmq_from_fp16("q6_k", sub, B, len(rows), N, K, O.EXACT)
     assert O.allclose(exact, got, 0.01)
+
+
+@pytest.mark.parametrize("fmt", ("q8_0", "q4_k", "q6_k"))
+def test_gemm_chunked_launches_bit_exact(fmt, monkeypatch):
+    """The GEMM path's 32-bit offset guard: calls over GQ_GEMM_MAX_BYTES of weights or of fp16
+    activations run as row x token chunks; with a small limit (many chunks in both dims) the
+    result equals the one-launch result bit for bit (split-K off on both)."""
+    from kernels._lib import TYPES, mmq
+    dev = _dev()
+    M, N, K = 700, 300, 1024
+    qA = random_blocks(fmt, M, K, seed=9)
+    B = random_activations(N, K, seed=10)
+    A_t = torch.from_numpy(qA.view(np.int8)).to(dev)
+    B_t = torch.from_numpy(B).to(dev)
+    monkeypatch.setenv("GQ_GEMM_SPLITS", "1")
+    monkeypatch.setenv("GQ_BLAS_MIN_TOKENS", "0")
+    one = mmq(TYPES[fmt], A_t, B_t, M, N, K)
+    monkeypatch.setenv("GQ_GEMM_MAX_BYTES", str(256 * 1024))  # 256 rows / 128 tokens per launch
+    many = mmq(TYPES[fmt], A_t, B_t, M, N, K)
+    torch.cuda.synchronize()
+    assert torch.equal(one.view(torch.int16), many.view(torch.int16))
+    ideal = O.mmq_from_fp16(fmt, qA, B, M, N, K, O.IDEAL)
+    assert O.max_rel_err(many.cpu().numpy(), ideal) <= TIGHT_GEMM
+
+
+def test_gemm_weights_over_4gib():
+    """A 4.5 GB Q8_0 weight tensor (131072 x 32768) at 16 tokens: two row chunks; sampled rows
+    from both against the oracle."""
+    from kernels._lib import TYPES, mmq
+    dev = _dev()
+    M, N, K = 131072, 16, 32768
+    row_bytes = K // 32 * 34
+    A_t = torch.empty(M * row_bytes, dtype=torch.int8, device=dev)
+    rows = np.array([0, 5, 70000, 100001, M - 1])
+    sub = random_blocks("q8_0", len(rows), K, seed=21)
+    base = torch.from_numpy(random_blocks("q8_0", 64, K, seed=22).view(np.int8)).to(dev)
+    for i in range(0, M, 64):
+        A_t[i * row_bytes:(i + 64) * row_bytes] = base
+    for j, r in enumerate(rows):
+        A_t[r * row_bytes:(r + 1) * row_bytes] = torch.from_numpy(sub[j * row_bytes:(j + 1) * row_bytes].view(np.int8)).to(dev)
+    B = random_activations(N, K, seed=23)
+    C = mmq(TYPES["q8_0"], A_t, torch.from_numpy(B).to(dev), M, N, K)
+    torch.cuda.synchronize()
+    got = C[:, torch.from_numpy(rows).to(dev)].cpu().numpy()
+    ideal = O.mmq_from_fp16("q8_0", sub, B, len(rows), N, K, O.IDEAL)
+    assert O.max_rel_err(got, ideal) <= TIGHT_GEMM
+    del A_t
+    torch.cuda.empty_cache()
