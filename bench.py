@@ -100,10 +100,11 @@ def model(fmt, M, K, N):
 class Runner:
     """Holds resident buffers for one config and the captured graphs."""
 
-    def __init__(self, fmt, M, K, N, dev, steps, seed=0):
+    def __init__(self, fmt, M, K, N, dev, steps, seed=0, act="q8_1"):
         import kernels._lib as kl
         self.kl, self.L = kl, kl.lib()
         self.fmt, self.M, self.K, self.N, self.dev = fmt, M, K, N, dev
+        self.act = kl.ACTS[act]
         self.gtype = GTYPE[fmt]
         wbytes, _, _ = model(fmt, M, K, N)
         self.ncopies = max(2, math.ceil(ROTATE_BYTES / wbytes))
@@ -112,7 +113,7 @@ class Runner:
         g = torch.Generator(device=dev).manual_seed(seed + 1)
         self.B = torch.randn(N, K, device=dev, generator=g).to(torch.float16)
         self.C = [torch.empty(N, M, dtype=torch.float16, device=dev) for _ in range(2)]
-        self.ws_bytes = kl.workspace_size(self.gtype, M, N, K)
+        self.ws_bytes = kl.workspace_size(self.gtype, M, N, K, act)
         self.ws = torch.empty(max(self.ws_bytes, 1), dtype=torch.uint8, device=dev)
         self.stream_ptr = None
 
@@ -122,21 +123,21 @@ class Runner:
     def step(self, i, c=None):
         A = self.weights[i % self.ncopies]
         C = self.C[i & 1] if c is None else c
-        rc = self.L.gq_mmq(self.gtype, A.data_ptr(), self.B.data_ptr(), C.data_ptr(), self.M, self.N, self.K,
-                           self.K, self.M, self.ws.data_ptr(), self.ws_bytes, self._stream())
+        rc = self.L.gq_mmq_ex(self.gtype, self.act, A.data_ptr(), self.B.data_ptr(), C.data_ptr(), self.M, self.N,
+                              self.K, self.K, self.M, self.ws.data_ptr(), self.ws_bytes, self._stream())
         if rc:
             raise RuntimeError(self.L.gq_last_error().decode())
 
     def prepare(self):
-        rc = self.L.gq_act_prepare(self.B.data_ptr(), self.N, self.K, self.K, self.ws.data_ptr(), self.ws_bytes,
-                                   self._stream())
+        rc = self.L.gq_act_prepare_ex(self.act, self.B.data_ptr(), self.N, self.K, self.K, self.ws.data_ptr(),
+                                      self.ws_bytes, self._stream())
         if rc:
             raise RuntimeError(self.L.gq_last_error().decode())
 
     def kernel(self, i):
         A = self.weights[i % self.ncopies]
-        rc = self.L.gq_mmq_prepared(self.gtype, A.data_ptr(), self.ws.data_ptr(), self.ws_bytes,
-                                    self.C[i & 1].data_ptr(), self.M, self.N, self.K, self.M, self._stream())
+        rc = self.L.gq_mmq_prepared_ex(self.gtype, self.act, A.data_ptr(), self.ws.data_ptr(), self.ws_bytes,
+                                       self.C[i & 1].data_ptr(), self.M, self.N, self.K, self.M, self._stream())
         if rc:
             raise RuntimeError(self.L.gq_last_error().decode())
 
@@ -490,41 +491,70 @@ def bench_config(name, steps, warmup, dev):
     return out
 
 
-def bench_layer(N, steps, warmup, dev):
+def bench_layer(Ns, acts, steps, warmup, dev):
     """BASELINE configs[4]: the seven projections of a Llama-7B block under GGUF Q4_K_M (layer 0:
     attn_v and ffn_down in Q6_K, the rest Q4_K), shared inputs quantized once per group
-    (kernels.layer_mix.LayerMix).  Weights rotate over >= 1 GiB of copies."""
+    (kernels.layer_mix.LayerMix), for each token count in Ns and activation format in acts
+    ("q8_1": the reference's semantics; "fp8": the e4m3 variant).  Weights rotate over >= 1 GiB."""
     from gguf import LLAMA_LAYER_SHAPES, q4_k_m_layer_types
     from kernels.layer_mix import GGUFLinear, LayerMix
     types = q4_k_m_layer_types(0, 32)
     one = {n: device_random_blocks(types[n], M, K, dev, seed=i) for i, (n, (M, K)) in enumerate(LLAMA_LAYER_SHAPES.items())}
     layer_bytes = sum(t.numel() for t in one.values())
     ncopies = max(2, math.ceil(ROTATE_BYTES / layer_bytes))
-    layers = [LayerMix({n: GGUFLinear(types[n], one[n] if c == 0 else one[n].clone(), *LLAMA_LAYER_SHAPES[n])
-                        for n in LLAMA_LAYER_SHAPES}) for c in range(ncopies)]
-    g = torch.Generator(device=dev).manual_seed(7)
-    x = torch.randn(N, 4096, device=dev, generator=g).to(torch.float16)
-    h = torch.randn(N, 11008, device=dev, generator=g).to(torch.float16)
-    outs = {n: torch.empty(N, M, dtype=torch.float16, device=dev) for n, (M, K) in LLAMA_LAYER_SHAPES.items()}
-    flops = sum(2.0 * N * M * K for M, K in LLAMA_LAYER_SHAPES.values())
-    for i in range(max(1, warmup)):  # also creates any library handles outside capture
-        layers[i % ncopies].forward(x, h, out=outs)
-    torch.cuda.synchronize(dev)
-    gr = torch.cuda.CUDAGraph()
-    s = torch.cuda.Stream(dev)
-    s.wait_stream(torch.cuda.current_stream(dev))
-    with torch.cuda.stream(s):
-        layers[0].forward(x, h, out=outs)
-    torch.cuda.current_stream(dev).wait_stream(s)
-    torch.cuda.synchronize(dev)
-    with torch.cuda.graph(gr):
-        for i in range(steps):
-            layers[i % ncopies].forward(x, h, out=outs)
-    gr.replay()
-    t = min(timed_replay(gr, dev) for _ in range(3)) / steps
-    return {"config": f"q4_k_m_llama7b_layer_m{N}", "fmt": "q4_k+q6_k", "M_tok": N, "ms_per_step": t * 1e3,
-            "tflops": flops / t / 1e12, "weight_GBps": layer_bytes / t / 1e9, "weight_bytes": layer_bytes,
-            "types": types, "weight_copies": ncopies}
+    lins = [{n: GGUFLinear(types[n], one[n] if c == 0 else one[n].clone(), *LLAMA_LAYER_SHAPES[n])
+             for n in LLAMA_LAYER_SHAPES} for c in range(ncopies)]
+    res = []
+    for act in acts:
+        layers = [LayerMix(lin, act=act) for lin in lins]
+        for N in Ns:
+            g = torch.Generator(device=dev).manual_seed(7)
+            x = torch.randn(N, 4096, device=dev, generator=g).to(torch.float16)
+            h = torch.randn(N, 11008, device=dev, generator=g).to(torch.float16)
+            outs = {n: torch.empty(N, M, dtype=torch.float16, device=dev) for n, (M, K) in LLAMA_LAYER_SHAPES.items()}
+            flops = sum(2.0 * N * M * K for M, K in LLAMA_LAYER_SHAPES.values())
+            for i in range(max(1, warmup)):  # also creates any library handles outside capture
+                layers[i % ncopies].forward(x, h, out=outs)
+            torch.cuda.synchronize(dev)
+            gr = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream(dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                layers[0].forward(x, h, out=outs)
+            torch.cuda.current_stream(dev).wait_stream(s)
+            torch.cuda.synchronize(dev)
+            with torch.cuda.graph(gr):
+                for i in range(steps):
+                    layers[i % ncopies].forward(x, h, out=outs)
+            gr.replay()
+            t = min(timed_replay(gr, dev) for _ in range(3)) / steps
+            res.append({"config": f"q4_k_m_llama7b_layer_m{N}", "act": act, "fmt": "q4_k+q6_k", "M_tok": N,
+                        "us_per_step": round(t * 1e6, 2), "tflops": round(flops / t / 1e12, 3),
+                        "weight_GBps": round(layer_bytes / t / 1e9, 1)})
+            del gr
+    del lins, layers
+    torch.cuda.empty_cache()
+    return {"config": "q4_k_m_llama7b_layer_msweep", "types": types, "weight_bytes": layer_bytes,
+            "weight_copies": ncopies, "points": res}
+
+
+def bench_fp8(names, steps, warmup, dev):
+    """The fp8 activation variant on BASELINE shapes: the step (gq_mmq_ex, GQ_ACT_FP8_E4M3)."""
+    out = []
+    for name in names:
+        fmt, M, K, N = CONFIGS[name]
+        r = Runner(fmt, M, K, N, dev, steps, act="fp8")
+        gw = r.capture(r.step, max(1, warmup))
+        gw.replay()
+        g = r.capture(r.step, steps)
+        g.replay()
+        t = min(timed_replay(g, dev) for _ in range(3)) / steps
+        wbytes, _, flops = model(fmt, M, K, N)
+        out.append({"config": name + "_fp8act", "act": "fp8", "us_per_step": round(t * 1e6, 2),
+                    "tflops": round(flops / t / 1e12, 3), "weight_GBps": round(wbytes / t / 1e9, 1)})
+        del r, g, gw
+        torch.cuda.empty_cache()
+    return out
 
 
 def bench_msweep(steps, warmup, dev, fmt="q4_k", M=4096, K=4096):
@@ -610,9 +640,11 @@ def main():
         for sname in CONFIGS:
             if sname != name:
                 sweep.append(bench_config(sname, sweep_steps, args.warmup, dev))
-        for n in (1, 128):
-            sweep.append(bench_layer(n, sweep_steps, args.warmup, dev))
+        sweep.append(bench_layer((1, 2, 4, 8, 16, 32, 64, 128, 256, 512), ("q8_1", "fp8"), sweep_steps, args.warmup,
+                                 dev))
         sweep.append(bench_msweep(sweep_steps, args.warmup, dev))
+        sweep.extend(bench_fp8(("q8_0_4096x4096_m128", "q4_k_11008x4096_m128", "q6_k_28672x8192_m128",
+                                "q4_k_4096x4096_m1"), sweep_steps, args.warmup, dev))
     cpu, cpu_var = None, None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu, cpu_var = cpu_baseline(fmt, M, K, N)

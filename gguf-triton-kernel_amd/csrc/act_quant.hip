@@ -17,6 +17,11 @@
 //          each 4-element group stored in the order (0,2,1,3) (see mmq_gemm.hip)
 //   I8   : codes int8 [rows][K] + d float BLOCK-major [K/32][ld] (ld = rows rounded up to 4) --
 //          the int8-MFMA GEMM's input: one tile's d of a K block is one contiguous run
+//   F8   : not q8_1 -- the fp8 activation variant (BASELINE configs[4]): per 32-element block
+//          X = 2^e, e the smallest integer with max|x| <= 448 * 2^e (X = 1 for an all-zero
+//          block), codes = OCP e4m3 (e4m3fn) of x / X, round to nearest even; codes [rows][K]
+//          with each 4-group stored (0,2,1,3) (the GEMM's fragment order), X as float in the
+//          I8 form's block-major layout
 #include "gguf_blocks.hpp"
 #include "gguf_internal.hpp"
 #include "gguf_q8_1.hpp"
@@ -38,6 +43,35 @@ __global__ __launch_bounds__(256) void act_quant_kernel(const uint16_t *__restri
 
     u32x4 v = {0, 0, 0, 0};
     if (live) v = ld16(X + row * ldx + 32 * j + 8 * sub);
+    if constexpr (MODE == ACT_F8) {
+        const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+        float x[8], amax = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            x[2 * i] = h2f(wd[i] & 0xffff);
+            x[2 * i + 1] = h2f(wd[i] >> 16);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(x[i]));
+        amax = fmaxf(amax, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax), 0xb1, 0xf, 0xf, false)));
+        amax = fmaxf(amax, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax), 0x4e, 0xf, 0xf, false)));
+        if (!live) return;
+        // amax = m * 2^E, m in [0.5, 1): amax <= 448 * 2^e  <=>  e >= E - 9 + (m > 0.875)
+        const uint32_t ab = __builtin_bit_cast(uint32_t, amax);
+        const int E = (int)((ab >> 23) & 0xff) - 126;
+        const int e = amax == 0.f ? 0 : E - 9 + ((ab & 0x7fffffu) > 0x600000u ? 1 : 0);
+        const float inv = __builtin_bit_cast(float, (uint32_t)(127 - e) << 23); // 2^-e, exact
+        uint32_t o[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) { // elements 4h..4h+3 -> bytes (0,2,1,3)
+            int w = __builtin_amdgcn_cvt_pk_fp8_f32(x[4 * h] * inv, x[4 * h + 2] * inv, 0, false);
+            w = __builtin_amdgcn_cvt_pk_fp8_f32(x[4 * h + 1] * inv, x[4 * h + 3] * inv, w, true);
+            o[h] = (uint32_t)w;
+        }
+        *(u32x2 *)(codes + row * K + 32 * j + 8 * sub) = (u32x2){o[0], o[1]};
+        if (sub == 0) dout[j * ((rows + 3) & ~(int64_t)3) + row] = __builtin_bit_cast(float, (uint32_t)(127 + e) << 23);
+        return;
+    }
     const Q81Quad q = q8_1_quad(v);
     if (!live) return;
 
@@ -88,6 +122,10 @@ hipError_t launch_act_quant(int mode, const uint16_t *X, int64_t ldx, int64_t ro
     case ACT_SOA:
         act_quant_kernel<ACT_SOA><<<grid, block, 0, s>>>(X, ldx, rows, K, nullptr, (int8_t *)out0, (float *)out1,
                                                           (float *)out2, nullptr);
+        break;
+    case ACT_F8:
+        act_quant_kernel<ACT_F8><<<grid, block, 0, s>>>(X, ldx, rows, K, nullptr, (int8_t *)out0, (float *)out1,
+                                                         nullptr, nullptr);
         break;
     case ACT_I8:
         act_quant_kernel<ACT_I8><<<grid, block, 0, s>>>(X, ldx, rows, K, nullptr, (int8_t *)out0, (float *)out1,

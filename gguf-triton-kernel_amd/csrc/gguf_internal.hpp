@@ -5,11 +5,17 @@
 
 namespace gq {
 
-enum ActMode : int { ACT_AOS = 0, ACT_SOA = 1, ACT_DEQ = 2, ACT_I8 = 3 };
+enum ActMode : int { ACT_AOS = 0, ACT_SOA = 1, ACT_DEQ = 2, ACT_I8 = 3, ACT_F8 = 4 };
+// Activation form the MFMA GEMM reads (mmq_gemm.hip): fp16 x~, q8_1 codes (Q8_0 int8 MFMA),
+// or the fp8 variant's e4m3 codes.
+enum ActForm : int { AF_F16 = 0, AF_I8 = 1, AF_F8 = 2 };
 
 // Activation quantizer (act_quant.hip).  AOS: out0 = q8_1 bytes.  SOA: out0 = int8 codes
 // [rows][K], out1 = float d [rows][K/32], out2 = float s [rows][K/32].  DEQ: out0 = fp16 x~.
 // I8: out0 = int8 codes [rows][K], out1 = float d [K/32][(rows + 3) & ~3] (block-major).
+// F8 (the fp8 activation variant, not q8_1): out0 = OCP e4m3 codes [rows][K], each 4-element
+// group stored (0,2,1,3); out1 = float 2^e [K/32][(rows + 3) & ~3], e the smallest integer with
+// max|x| <= 448 * 2^e over the block (2^0 for an all-zero block); code = e4m3(x / 2^e), RNE.
 hipError_t launch_act_quant(int mode, const uint16_t *X, int64_t ldx, int64_t rows, int64_t K, void *out0,
                             void *out1, void *out2, hipStream_t s);
 
@@ -30,20 +36,21 @@ struct GemmPlan {
     int rg = 2;                // 16-row groups per wave (8 waves: tile = 128*rg weight rows)
     int splits = 1;            // split-K factor (grid.z)
     int chunks_per_split = 1;  // 256-wide K stages (super-blocks) per split
-    bool i8 = false;           // Q8_0 only: int8 activations x int8 weights on v_mfma_i32_16x16x32_i8
+    int act = AF_F16;          // activation form (AF_I8: Q8_0 only)
     size_t partial_bytes = 0;  // fp32 partial slabs needed when splits > 1
 };
-// Activations as the GEMM reads them: fp16 x~ (act_quant DEQ) or, for plan.i8, int8 codes +
-// block-major fp32 d (act_quant I8).
+// Activations as the GEMM reads them: fp16 x~ (act_quant DEQ) or, for the code forms, codes +
+// block-major fp32 scales (act_quant I8 / F8).
 struct GemmAct {
     const uint16_t *xdeq = nullptr;
     const int8_t *xq = nullptr;
     const float *xd = nullptr;
+    int64_t ldd = 0; // row length of the block-major scale array (all the call's tokens)
 };
 // The MFMA GEMM needs K in whole 256-element stages (always true for Q4_K/Q6_K).
 bool gemm_supported(int fmt, int64_t K);
-// i8: request the int8-MFMA form (honoured for Q8_0 only).
-GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, bool i8 = false);
+// act: the activation form (AF_I8 is honoured for Q8_0 only).
+GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, int act = AF_F16);
 hipError_t launch_gemm(int fmt, const uint8_t *A, const GemmAct &x, uint16_t *C, float *partials,
                        const GemmPlan &plan, int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
 

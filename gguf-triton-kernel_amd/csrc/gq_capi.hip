@@ -78,40 +78,62 @@ int64_t gemm_toks_per_launch(int64_t N, int64_t K)
 bool use_i8(int t, int64_t N, int64_t K)
 {
     if (t != GQ_Q8_0 || use_gemv(N, K) || use_blas(N, K)) return false;
-    if (gemm_toks_per_launch(N, K) < N) return false; // its block-major d is not token-chunked
     const char *e = getenv("GQ_GEMM_I8");
     return e ? atoi(e) != 0 : false;
 }
 
-// GEMM-path activation forms in the workspace: fp16 x~ [N][K], then (int8 form) codes [N][K]
-// and block-major d [K/32][(N+3)&~3].
-size_t deq_bytes(int64_t N, int64_t K) { return align_up((size_t)N * K * 2); }
-size_t i8_code_bytes(int64_t N, int64_t K) { return align_up((size_t)N * K); }
-size_t i8_d_bytes(int64_t N, int64_t K) { return align_up((size_t)(K / 32) * (size_t)((N + 3) & ~(int64_t)3) * 4); }
-
-// Activation part of the workspace (what gq_act_prepare writes); depends on N, K only.
-size_t act_bytes(int64_t N, int64_t K)
+// Which kernels a call runs.  The q8_1 activations (the reference's semantics) go to the fused
+// decode / GEMV (N <= 4), the MFMA GEMM or, from blas_min_tokens(), dequant + hipBLASLt; the
+// fp8 variant (GQ_ACT_FP8_E4M3) always runs the MFMA GEMM on e4m3 codes.
+struct Route {
+    bool gemv = false, blas = false;
+    int form = gq::AF_F16; // GEMM activation form
+};
+Route route(int t, int act, int64_t N, int64_t K)
 {
+    Route r;
+    if (act == GQ_ACT_FP8_E4M3) {
+        r.form = gq::AF_F8;
+        return r;
+    }
+    r.gemv = use_gemv(N, K);
+    r.blas = use_blas(N, K);
+    r.form = use_i8(t, N, K) ? gq::AF_I8 : gq::AF_F16;
+    return r;
+}
+
+// GEMM-path activation forms in the workspace: fp16 x~ [N][K], then codes [N][K] and
+// block-major scales [K/32][(N+3)&~3] (q8_1: the int8 form; fp8 variant: only these two).
+int64_t scale_ld(int64_t N) { return (N + 3) & ~(int64_t)3; }
+size_t deq_bytes(int64_t N, int64_t K) { return align_up((size_t)N * K * 2); }
+size_t code_bytes(int64_t N, int64_t K) { return align_up((size_t)N * K); }
+size_t scale_bytes(int64_t N, int64_t K) { return align_up((size_t)(K / 32) * (size_t)scale_ld(N) * 4); }
+
+// Activation part of the workspace (what gq_act_prepare[_ex] writes); depends on act, N, K only.
+size_t act_bytes(int act, int64_t N, int64_t K)
+{
+    if (act == GQ_ACT_FP8_E4M3) return code_bytes(N, K) + scale_bytes(N, K);
     if (use_gemv(N, K)) {
         // SOA q8_1: codes + d + s
         return align_up((size_t)N * K) + 2 * align_up((size_t)N * (K / 32) * sizeof(float));
     }
-    return deq_bytes(N, K) + i8_code_bytes(N, K) + i8_d_bytes(N, K);
+    return deq_bytes(N, K) + code_bytes(N, K) + scale_bytes(N, K);
 }
 
-// Whole workspace: activations + (GEMM split-K) fp32 partial slabs.
-size_t ws_bytes(int t, int64_t M, int64_t N, int64_t K)
+// Whole workspace: activations + (GEMM split-K) fp32 partial slabs / (library path) fp16 W.
+size_t ws_bytes(int t, int act, int64_t M, int64_t N, int64_t K)
 {
-    size_t b = act_bytes(N, K);
-    if (use_blas(N, K)) b += align_up((size_t)M * K * 2) + gq::blas_workspace_bytes(); // fp16 W + hipBLASLt
-    else if (!use_gemv(N, K)) {
+    const Route r = route(t, act, N, K);
+    size_t b = act_bytes(act, N, K);
+    if (r.blas) b += align_up((size_t)M * K * 2) + gq::blas_workspace_bytes(); // fp16 W + hipBLASLt
+    else if (!r.gemv && gq::gemm_supported(t, K)) {
         // split-K partials of the largest need over the launch shapes (full and remainder chunks)
         const int64_t mr = gemm_rows_per_launch(t, M, K), nt = gemm_toks_per_launch(N, K);
         size_t p = 0;
         for (int64_t mc : {mr, M % mr})
             for (int64_t nc : {nt, N % nt})
                 if (mc > 0 && nc > 0) {
-                    const size_t q = gq::plan_gemm(t, mc, nc, K, use_i8(t, N, K)).partial_bytes;
+                    const size_t q = gq::plan_gemm(t, mc, nc, K, r.form).partial_bytes;
                     p = q > p ? q : p;
                 }
         b += align_up(p);
@@ -125,13 +147,17 @@ extern "C" {
 
 int gq_block_elems(gq_type t) { return block_elems(t); }
 int gq_block_bytes(gq_type t) { return block_bytes(t); }
-int gq_version(void) { return 100; }
+int gq_version(void) { return 101; }
 const char *gq_last_error(void) { return g_err.c_str(); }
 
-size_t gq_mmq_workspace_size(gq_type t, int64_t M, int64_t N, int64_t K)
+size_t gq_mmq_workspace_size_ex(gq_type t, gq_act act, int64_t M, int64_t N, int64_t K)
 {
     if (N <= 0 || K <= 0 || M < 0) return 0;
-    return ws_bytes(t, M, N, K);
+    return ws_bytes(t, act, M, N, K);
+}
+size_t gq_mmq_workspace_size(gq_type t, int64_t M, int64_t N, int64_t K)
+{
+    return gq_mmq_workspace_size_ex(t, GQ_ACT_Q8_1, M, N, K);
 }
 
 static int check_common(gq_type t, int64_t M, int64_t N, int64_t K)
@@ -144,42 +170,56 @@ static int check_common(gq_type t, int64_t M, int64_t N, int64_t K)
     return GQ_OK;
 }
 
+static int check_act(int act, int64_t K)
+{
+    if (act != GQ_ACT_Q8_1 && act != GQ_ACT_FP8_E4M3) return fail(GQ_EUNSUPPORTED, "unknown activation format %d", act);
+    if (act == GQ_ACT_FP8_E4M3 && !gq::gemm_supported(gq::Q8_0, K))
+        return fail(GQ_EUNSUPPORTED, "fp8 activations need K %% 256 == 0 (K=%lld)", (long long)K);
+    return GQ_OK;
+}
+
 struct Carved {
-    int8_t *xq;       // SOA codes (decode) / int8-form codes (GEMM)
-    float *xd, *xs;   // SOA d, s (decode) / int8-form block-major d (GEMM)
+    int8_t *xq;       // SOA codes (decode) / GEMM codes (int8 form, fp8 variant)
+    float *xd, *xs;   // SOA d, s (decode) / GEMM block-major scales
     uint16_t *xdeq;
     float *partials;
 };
 
-static Carved carve(void *workspace, int64_t N, int64_t K)
+static Carved carve(int act, void *workspace, int64_t N, int64_t K)
 {
     uint8_t *ws = (uint8_t *)workspace;
     Carved c{};
-    if (use_gemv(N, K)) {
+    if (act == GQ_ACT_FP8_E4M3) {
+        c.xq = (int8_t *)ws;
+        c.xd = (float *)(ws + code_bytes(N, K));
+    } else if (use_gemv(N, K)) {
         c.xq = (int8_t *)ws;
         c.xd = (float *)(ws + align_up((size_t)N * K));
         c.xs = (float *)((uint8_t *)c.xd + align_up((size_t)N * (K / 32) * sizeof(float)));
+        return c;
     } else {
         c.xdeq = (uint16_t *)ws;
         c.xq = (int8_t *)(ws + deq_bytes(N, K));
-        c.xd = (float *)(ws + deq_bytes(N, K) + i8_code_bytes(N, K));
-        c.partials = (float *)(ws + act_bytes(N, K));
+        c.xd = (float *)(ws + deq_bytes(N, K) + code_bytes(N, K));
     }
+    c.partials = (float *)(ws + act_bytes(act, N, K));
     return c;
 }
 
-// forms: bit 0 = fp16 x~ (DEQ), bit 1 = int8 codes + d (I8); only the GEMM path reads them
-static int prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *workspace, size_t workspace_bytes,
-                   hipStream_t s, int forms = 1)
+// q8_1 forms: bit 0 = fp16 x~ (DEQ), bit 1 = int8 codes + d (I8); only the GEMM path reads them
+static int prepare(int act, const void *B, int64_t N, int64_t K, int64_t ldb, void *workspace,
+                   size_t workspace_bytes, hipStream_t s, int forms = 1)
 {
     if (!B) return fail(GQ_EINVAL, "null activation pointer");
     if (ldb < K) return fail(GQ_EINVAL, "ldb=%lld < K=%lld", (long long)ldb, (long long)K);
-    const size_t need = act_bytes(N, K);
+    const size_t need = act_bytes(act, N, K);
     if (!workspace || workspace_bytes < need)
         return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace ? workspace_bytes : (size_t)0, need);
-    Carved c = carve(workspace, N, K);
+    Carved c = carve(act, workspace, N, K);
     hipError_t e = hipSuccess;
-    if (use_gemv(N, K)) {
+    if (act == GQ_ACT_FP8_E4M3) {
+        e = gq::launch_act_quant(gq::ACT_F8, (const uint16_t *)B, ldb, N, K, c.xq, c.xd, nullptr, s);
+    } else if (use_gemv(N, K)) {
         e = gq::launch_act_quant(gq::ACT_SOA, (const uint16_t *)B, ldb, N, K, c.xq, c.xd, c.xs, s);
     } else {
         if (forms & 1) e = gq::launch_act_quant(gq::ACT_DEQ, (const uint16_t *)B, ldb, N, K, c.xdeq, nullptr, nullptr, s);
@@ -190,15 +230,16 @@ static int prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *works
     return GQ_OK;
 }
 
-static int compute(gq_type t, const void *A, void *workspace, size_t workspace_bytes, void *C, int64_t M,
+static int compute(gq_type t, int act, const void *A, void *workspace, size_t workspace_bytes, void *C, int64_t M,
                    int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
     if (!A || !C || !workspace) return fail(GQ_EINVAL, "null pointer (A=%p C=%p workspace=%p)", A, C, workspace);
     if (ldc < M) return fail(GQ_EINVAL, "ldc=%lld < M=%lld", (long long)ldc, (long long)M);
-    const size_t need = ws_bytes(t, M, N, K);
+    const size_t need = ws_bytes(t, act, M, N, K);
     if (workspace_bytes < need) return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace_bytes, need);
-    Carved c = carve(workspace, N, K);
-    if (use_blas(N, K)) {
+    const Route r = route(t, act, N, K);
+    Carved c = carve(act, workspace, N, K);
+    if (r.blas) {
         uint16_t *W = (uint16_t *)c.partials; // after the activations: fp16 W, then the BLAS workspace
         uint8_t *bws = (uint8_t *)W + align_up((size_t)M * K * 2);
         hipError_t e = gq::launch_dequant(t, (const uint8_t *)A, W, M, K, K, true, s);
@@ -208,76 +249,99 @@ static int compute(gq_type t, const void *A, void *workspace, size_t workspace_b
         return GQ_OK;
     }
     hipError_t e;
-    if (use_gemv(N, K)) {
+    if (r.gemv) {
         e = gq::launch_gemv(t, (const uint8_t *)A, c.xq, c.xd, c.xs, (uint16_t *)C, M, N, K, ldc, s);
     } else {
         // chunks of < 2 GiB of weights and of activations per launch (32-bit buffer offsets)
         const int64_t mr = gemm_rows_per_launch(t, M, K), nt = gemm_toks_per_launch(N, K);
-        const bool i8 = use_i8(t, N, K);
         e = hipSuccess;
         for (int64_t n0 = 0; n0 < N && e == hipSuccess; n0 += nt)
             for (int64_t m0 = 0; m0 < M && e == hipSuccess; m0 += mr) {
                 const int64_t mc = M - m0 < mr ? M - m0 : mr, nc = N - n0 < nt ? N - n0 : nt;
                 gq::GemmAct x;
-                x.xdeq = c.xdeq + n0 * K;
-                x.xq = c.xq;
-                x.xd = c.xd;
+                x.xdeq = c.xdeq ? c.xdeq + n0 * K : nullptr;
+                x.xq = c.xq + n0 * K;
+                x.xd = c.xd + n0;
+                x.ldd = scale_ld(N);
                 e = gq::launch_gemm(t, (const uint8_t *)A + m0 * row_bytes_of(t, K), x, (uint16_t *)C + n0 * ldc + m0,
-                                    c.partials, gq::plan_gemm(t, mc, nc, K, i8), mc, nc, K, ldc, s);
+                                    c.partials, gq::plan_gemm(t, mc, nc, K, r.form), mc, nc, K, ldc, s);
             }
     }
     if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (mmq): %s", hipGetErrorString(e));
     return GQ_OK;
 }
 
-int gq_mmq(gq_type t, const void *A, const void *B, void *C, int64_t M, int64_t N, int64_t K, int64_t ldb,
-           int64_t ldc, void *workspace, size_t workspace_bytes, void *stream)
+int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int64_t M, int64_t N, int64_t K,
+              int64_t ldb, int64_t ldc, void *workspace, size_t workspace_bytes, void *stream)
 {
     g_err.clear();
     int rc = check_common(t, M, N, K);
     if (rc != GQ_OK) return rc;
+    if ((rc = check_act(act, K)) != GQ_OK) return rc;
     if (M == 0 || N == 0) return GQ_OK;
     if (K == 0) return fail(GQ_EINVAL, "K must be positive");
     if (!A || !B || !C) return fail(GQ_EINVAL, "null pointer (A=%p B=%p C=%p)", A, B, C);
     if (ldc < M) return fail(GQ_EINVAL, "ldc=%lld < M=%lld", (long long)ldc, (long long)M);
-    if (!workspace || workspace_bytes < ws_bytes(t, M, N, K))
-        return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace ? workspace_bytes : (size_t)0,
-                    ws_bytes(t, M, N, K));
+    const size_t need = ws_bytes(t, act, M, N, K);
+    if (!workspace || workspace_bytes < need)
+        return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace ? workspace_bytes : (size_t)0, need);
     if (ldb < K) return fail(GQ_EINVAL, "ldb=%lld < K=%lld", (long long)ldb, (long long)K);
-    if (use_gemv(N, K) && gq::decode_fused_ok(t, N, K) && !getenv("GQ_NO_FUSED_DECODE")) {
+    const Route r = route(t, act, N, K);
+    if (r.gemv && gq::decode_fused_ok(t, N, K) && !getenv("GQ_NO_FUSED_DECODE")) {
         // one launch: activation quantization in LDS + decode GEMV
         hipError_t e = gq::launch_decode_fused(t, (const uint8_t *)A, (const uint16_t *)B, ldb, (uint16_t *)C, M, N,
                                                K, ldc, (hipStream_t)stream);
         if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (decode): %s", hipGetErrorString(e));
         return GQ_OK;
     }
-    rc = prepare(B, N, K, ldb, workspace, workspace_bytes, (hipStream_t)stream, use_i8(t, N, K) ? 2 : 1);
+    rc = prepare(act, B, N, K, ldb, workspace, workspace_bytes, (hipStream_t)stream, r.form == gq::AF_I8 ? 2 : 1);
     if (rc != GQ_OK) return rc;
-    return compute(t, A, workspace, workspace_bytes, C, M, N, K, ldc, (hipStream_t)stream);
+    return compute(t, act, A, workspace, workspace_bytes, C, M, N, K, ldc, (hipStream_t)stream);
+}
+
+int gq_mmq(gq_type t, const void *A, const void *B, void *C, int64_t M, int64_t N, int64_t K, int64_t ldb,
+           int64_t ldc, void *workspace, size_t workspace_bytes, void *stream)
+{
+    return gq_mmq_ex(t, GQ_ACT_Q8_1, A, B, C, M, N, K, ldb, ldc, workspace, workspace_bytes, stream);
+}
+
+int gq_act_prepare_ex(gq_act act, const void *B, int64_t N, int64_t K, int64_t ldb, void *workspace,
+                      size_t workspace_bytes, void *stream)
+{
+    g_err.clear();
+    if (N < 0 || K < 0) return fail(GQ_EINVAL, "negative size");
+    if (K % 32 != 0) return fail(GQ_EINVAL, "K=%lld is not a multiple of 32", (long long)K);
+    int rc = check_act(act, K);
+    if (rc != GQ_OK) return rc;
+    if (N == 0 || K == 0) return GQ_OK;
+    // the weight type is not known here: write every form a later gq_mmq_prepared may read
+    // (the int8 form only when Q8_0 would use it)
+    return prepare(act, B, N, K, ldb, workspace, workspace_bytes, (hipStream_t)stream,
+                   use_i8(GQ_Q8_0, N, K) ? 3 : 1);
 }
 
 int gq_act_prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *workspace, size_t workspace_bytes,
                    void *stream)
 {
+    return gq_act_prepare_ex(GQ_ACT_Q8_1, B, N, K, ldb, workspace, workspace_bytes, stream);
+}
+
+int gq_mmq_prepared_ex(gq_type t, gq_act act, const void *A, void *workspace, size_t workspace_bytes, void *C,
+                       int64_t M, int64_t N, int64_t K, int64_t ldc, void *stream)
+{
     g_err.clear();
-    if (N < 0 || K < 0) return fail(GQ_EINVAL, "negative size");
-    if (K % 32 != 0) return fail(GQ_EINVAL, "K=%lld is not a multiple of 32", (long long)K);
-    if (N == 0 || K == 0) return GQ_OK;
-    // the weight type is not known here: write every form a later gq_mmq_prepared may read
-    // (the int8 form only when Q8_0 would use it)
-    return prepare(B, N, K, ldb, workspace, workspace_bytes, (hipStream_t)stream,
-                   use_i8(GQ_Q8_0, N, K) ? 3 : 1);
+    int rc = check_common(t, M, N, K);
+    if (rc != GQ_OK) return rc;
+    if ((rc = check_act(act, K)) != GQ_OK) return rc;
+    if (M == 0 || N == 0) return GQ_OK;
+    if (K == 0) return fail(GQ_EINVAL, "K must be positive");
+    return compute(t, act, A, workspace, workspace_bytes, C, M, N, K, ldc, (hipStream_t)stream);
 }
 
 int gq_mmq_prepared(gq_type t, const void *A, void *workspace, size_t workspace_bytes, void *C, int64_t M, int64_t N,
                     int64_t K, int64_t ldc, void *stream)
 {
-    g_err.clear();
-    int rc = check_common(t, M, N, K);
-    if (rc != GQ_OK) return rc;
-    if (M == 0 || N == 0) return GQ_OK;
-    if (K == 0) return fail(GQ_EINVAL, "K must be positive");
-    return compute(t, A, workspace, workspace_bytes, C, M, N, K, ldc, (hipStream_t)stream);
+    return gq_mmq_prepared_ex(t, GQ_ACT_Q8_1, A, workspace, workspace_bytes, C, M, N, K, ldc, stream);
 }
 
 int gq_dequantize(gq_type t, const void *A, void *W, int64_t M, int64_t K, int64_t ldw, void *stream)
@@ -302,6 +366,20 @@ int gq_quantize_q8_1(const void *X, void *Y, int64_t rows, int64_t K, int64_t ld
     if (!X || !Y) return fail(GQ_EINVAL, "null pointer");
     if (ldx < K) return fail(GQ_EINVAL, "ldx=%lld < K=%lld", (long long)ldx, (long long)K);
     hipError_t e = gq::launch_act_quant(gq::ACT_AOS, (const uint16_t *)X, ldx, rows, K, Y, nullptr, nullptr,
+                                        (hipStream_t)stream);
+    if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed: %s", hipGetErrorString(e));
+    return GQ_OK;
+}
+
+int gq_quantize_fp8(const void *X, void *codes, void *scales, int64_t rows, int64_t K, int64_t ldx, void *stream)
+{
+    g_err.clear();
+    if (rows < 0 || K < 0) return fail(GQ_EINVAL, "negative size");
+    if (K % 32 != 0) return fail(GQ_EINVAL, "K=%lld is not a multiple of 32", (long long)K);
+    if (rows == 0 || K == 0) return GQ_OK;
+    if (!X || !codes || !scales) return fail(GQ_EINVAL, "null pointer");
+    if (ldx < K) return fail(GQ_EINVAL, "ldx=%lld < K=%lld", (long long)ldx, (long long)K);
+    hipError_t e = gq::launch_act_quant(gq::ACT_F8, (const uint16_t *)X, ldx, rows, K, codes, scales, nullptr,
                                         (hipStream_t)stream);
     if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed: %s", hipGetErrorString(e));
     return GQ_OK;

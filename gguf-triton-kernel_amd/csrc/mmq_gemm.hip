@@ -6,11 +6,17 @@
 // v_mfma_f32_16x16x32_f16 with fp32 accumulation.  fp16 rather than bf16: the reference's
 // activations are fp16 and bf16 would drop three of their mantissa bits.
 //
-// Q8_0 has a second form (I8 = true, act_quant I8 form): the q8_1 codes and the weight codes
-// go into v_mfma_i32_16x16x32_i8 as they are (one 32-element block = one MFMA k-step, the
-// reference's int dot, mmq_q8_0.py:85-88), and every block's int32 tile is scaled by
-// dA[row]*dB[token] into the fp32 accumulators -- no weight dequantization, half the
-// activation bytes, four VALU ops per output per block.
+// Activation forms (template AM, gguf_internal.hpp ActForm):
+//   AF_F16: x~ = fp16(d*q), the q8_1 activation dequantized (act_quant DEQ form);
+//   AF_I8 (Q8_0 only): the q8_1 codes and the weight codes go into v_mfma_i32_16x16x32_i8 as
+//          they are (one 32-element block = one MFMA k-step, the reference's int dot,
+//          mmq_q8_0.py:85-88) and every block's int32 tile is scaled by dA[row]*dB[token] into
+//          the fp32 accumulators: no weight dequantization, half the activation bytes;
+//   AF_F8: the fp8 activation variant (BASELINE configs[4]): OCP e4m3 codes with a power-of-two
+//          scale per 32-element block (act_quant F8 form), widened to fp16 in registers by
+//          v_cvt_scalef32_pk_f16_fp8 (code * 2^e is exact in fp16) into the same fp16 MFMA.
+// AF_I8 and AF_F8 stage the same bytes: per token and sub-stage 64 code bytes, and the tile's
+// per-block fp32 scales (d, or 2^e) from a block-major [K/32][ldd] array.
 //
 // Workgroup = 8 waves = BM = 128*RG weight rows x BN = 16*NB tokens.  Wave w owns rows
 // 16*(RG*w + rg) + [0,16) (rg < RG) and every token of the tile: each weight is dequantized
@@ -23,7 +29,7 @@
 // LDS-DMA (global_load_lds_dwordx4: no VGPRs, no ds_write):
 //   weights     : per row the stage's raw block bytes (WStage<F> below), 16-byte pieces at
 //                 whatever (2-byte) alignment the blocks have (gfx950 runs unaligned);
-//   activations : BN token rows x 128 B (I8: x 64 B of codes + the tile's d), 16-byte pieces
+//   activations : BN token rows x 128 B (AF_I8/AF_F8: x 64 B of codes + the tile's scales), 16-byte pieces
 //                 XOR-swizzled on the SOURCE side (the DMA destination is lane-linear) so the
 //                 MFMA fragment reads of a lane group hit distinct banks.
 // Two weight-stage slots and an activation ring of up to 4 slots (Cfg below) keep the next
@@ -105,17 +111,18 @@ __device__ __forceinline__ uint32_t act_voff(int p) // byte offset of piece p (8
 
 constexpr int NWAVE = 8; // 512 threads: two waves per SIMD
 
-template <int F, int NB, int RG = 1, bool I8 = false>
+template <int F, int NB, int RG = 1, int AM = AF_F16>
 struct Cfg {
     // 128*RG weight rows x 16*NB tokens; wave w owns rows 16*(RG*w + rg) + [0, 16), rg < RG
     static constexpr int BN = 16 * NB, BM = 16 * NWAVE * RG;
     static constexpr int RBW = WStage<F>::RBW, NPW = RBW / 16;
     static constexpr int W_REAL = BM * NPW / 64;                              // DMA instructions per stage
-    // I8 activation sub-stage: BN x 64 code bytes (CI instructions), then one instruction for
-    // the tile's d of the sub-stage's two blocks (2 x BN floats)
+    // code-form (AF_I8 / AF_F8) activation sub-stage: BN x 64 code bytes (CI instructions), then
+    // one instruction for the tile's scales of the sub-stage's two blocks (2 x BN floats)
+    static constexpr bool CODES = AM != AF_F16;
     static constexpr int CI = BN * 64 / 1024 > 0 ? BN * 64 / 1024 : 1;
-    static constexpr int A_REAL = I8 ? CI + 1 : (BN * 8 / 64 > 0 ? BN * 8 / 64 : 1);
-    static constexpr int D_OFF = CI * 1024; // I8: byte offset of the d floats in a slot
+    static constexpr int A_REAL = CODES ? CI + 1 : (BN * 8 / 64 > 0 ? BN * 8 / 64 : 1);
+    static constexpr int D_OFF = CI * 1024; // code forms: byte offset of the scales in a slot
     static constexpr int NW = (W_REAL + NWAVE - 1) / NWAVE, NA = (A_REAL + NWAVE - 1) / NWAVE; // per wave
     static constexpr int W_SLOT = W_REAL * 1024, A_SLOT = A_REAL * 1024;
     // activation sub-stage ring: as deep as the LDS allows, at most 4*NWS-4 slots (W(w) must
@@ -135,7 +142,8 @@ struct Cfg {
     static constexpr int A_BASE = NWS * W_SLOT, SCRATCH = A_BASE + NAS * A_SLOT; // dummy DMAs land there
     static constexpr int LDS_BYTES = SCRATCH + (PAD ? 1024 : 0);
     static_assert((BM * NPW % 64 == 0 && (BN * 8) % 64 == 0) || BN * 8 < 64, "whole DMA instructions");
-    static_assert(!I8 || (F == Q8_0 && RG == 1 && BN <= 128), "int8 form: Q8_0, 128-row tiles, <= 128 tokens");
+    static_assert(AM != AF_I8 || (F == Q8_0 && RG == 1), "int8 form: Q8_0, 128-row tiles");
+    static_assert(!CODES || BN <= 128, "code forms: <= 128 tokens per tile");
     static_assert(LDS_BYTES <= LDS_MAX, "LDS budget");
     static_assert(NAS >= 3, "activation ring depth");
     static_assert((NAS - 2) * NA + 2 * NW <= 63, "vmcnt range");
@@ -216,7 +224,7 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, uint8_t *lds_
 }
 
 __device__ __forceinline__ int act_swz(int r) { return (r >> 1) & 7; }
-// I8 code rows are 64 B (four 16-byte pieces): piece q of token r lands in piece q ^ i8_swz(r),
+// Code rows are 64 B (four 16-byte pieces): piece q of token r lands in piece q ^ i8_swz(r),
 // so the 8-byte fragment reads of 16 tokens x 2 k-groups cover all 64 banks once.
 __device__ __forceinline__ int i8_swz(int r) { return (r >> 2) & 3; }
 
@@ -238,14 +246,14 @@ constexpr uint32_t DUMMY = 0u;
 // bytes into the same slot) so every wave issues the same sequence.
 // ABL: ablation bitmask for performance diagnosis (diagnostic build -DGQ_ABLATION only; 0 in
 // production): 1 = no MFMA, 2 = no weight DMA, 4 = no activation DMA, 8 = no dequantization.
-// I8 (Q8_0): X = int8 codes [N][K], XD = block-major d [K/32][ldd]; otherwise X = fp16 x~.
-template <int F, int NB, int RG, int ABL = 0, bool I8 = false>
+// AF_I8 / AF_F8: X = codes [N][K], XD = block-major scales [K/32][ldd]; AF_F16: X = fp16 x~.
+template <int F, int NB, int RG, int ABL = 0, int AM = AF_F16>
 __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A, const void *__restrict__ X,
                                                    const float *__restrict__ XD, uint16_t *__restrict__ C,
                                                    float *__restrict__ P, int64_t M, int64_t N, int64_t K,
-                                                   int64_t ldc, int wstages_per_split)
+                                                   int64_t ldc, int64_t ldd, int wstages_per_split)
 {
-    using G = Cfg<F, NB, RG, I8>;
+    using G = Cfg<F, NB, RG, AM>;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[G::LDS_BYTES];
 #ifdef GQ_GEMM_STAMPS
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
@@ -269,10 +277,11 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
     const __amdgpu_buffer_rsrc_t wrs =
         __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, (int)(uint32_t)((M * row_bytes + 15) & ~(int64_t)15), 0x00020000);
     const __amdgpu_buffer_rsrc_t ars =
-        __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, (int)(uint32_t)(N * K * (I8 ? 1 : 2)), 0x00020000);
-    const int64_t ldd = (N + 3) & ~(int64_t)3; // I8: row length of the block-major d array
-    const __amdgpu_buffer_rsrc_t drs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)XD, 0, I8 ? (int)(uint32_t)((K / 32) * ldd * 4) : 0, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, (int)(uint32_t)(N * K * (G::CODES ? 1 : 2)), 0x00020000);
+    // code forms: scales [K/32][ldd] from XD (this launch's first token), the last block's run
+    // holding this launch's N tokens
+    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)XD, 0, G::CODES ? (int)(uint32_t)(((K / 32 - 1) * ldd + N) * 4) : 0, 0x00020000);
 
     // weight DMA: instruction k = wave + 8i moves pieces p = 64k + lane: row p / NPW, piece p % NPW
     uint32_t wv[G::NW];
@@ -285,21 +294,24 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
         wv[i] = r < G::BM ? (uint32_t)(row * row_bytes) : DUMMY;
     }
     // activation DMA: instruction k moves pieces p = 64k + lane: token p >> 3, slot p & 7.
-    // I8: code instructions k < CI move pieces p: token p >> 2, piece p & 3 (swizzle i8_swz);
-    // instruction CI moves the d of the sub-stage's two blocks: lanes [0, BN/4) block 0, the
-    // next BN/4 block 1, four tokens per lane.
+    // Code forms: instructions k < CI move pieces p: token p >> 2, piece p & 3 (swizzle i8_swz;
+    // Q6_K: pieces 2, 3 are the second 32-element run, 64 elements on); instruction CI moves the
+    // scales of the sub-stage's two blocks: lanes [0, BN/4) block 0, the next BN/4 block 1,
+    // four tokens per lane.
     uint32_t av[G::NA];
 #pragma unroll
     for (int i = 0; i < G::NA; ++i) {
         const int k = wave + NWAVE * i, p = 64 * k + lane;
-        if constexpr (I8) {
+        if constexpr (G::CODES) {
             if (k < G::CI) {
-                const int r = p >> 2, q = p & 3;
+                const int r = p >> 2, q = p & 3, qs = q ^ i8_swz(r);
                 const int64_t tok = n0 + r < N ? n0 + r : N - 1;
-                av[i] = r < G::BN ? (uint32_t)(tok * K) + 16u * (uint32_t)(q ^ i8_swz(r)) : DUMMY;
+                const uint32_t po = F == Q6_K ? 64u * (uint32_t)(qs >> 1) + 16u * (uint32_t)(qs & 1) : 16u * (uint32_t)qs;
+                av[i] = r < G::BN ? (uint32_t)(tok * K) + po : DUMMY;
             } else {
                 const int b = lane / (G::BN / 4), j = lane - b * (G::BN / 4);
-                av[i] = k == G::CI && b < 2 ? (uint32_t)((b * ldd + n0 + 4 * j) * 4) : DUMMY;
+                const int64_t bstride = F == Q6_K ? 2 : 1; // Q6_K: blocks e0/32 and e0/32 + 2
+                av[i] = k == G::CI && b < 2 ? (uint32_t)((b * bstride * ldd + n0 + 4 * j) * 4) : DUMMY;
             }
         } else {
             const int r = p >> 3, q = p & 7;
@@ -333,9 +345,10 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
         for (int i = 0; i < G::NA; ++i) {
             const int k = wave + NWAVE * i;
             uint8_t *d = k < G::A_REAL ? dst + 1024 * k : lds + G::SCRATCH;
-            if constexpr (I8) {
-                if (k < G::CI) dma16(ars, d, av[i], (uint32_t)(64 * a));
-                else dma16(drs, d, av[i], (uint32_t)(8 * a * ldd)); // d of blocks 2a, 2a+1
+            if constexpr (G::CODES) {
+                const uint32_t e0 = act_soff<F>(a) / 2; // first element of the sub-stage
+                if (k < G::CI) dma16(ars, d, av[i], e0);
+                else dma16(drs, d, av[i], (uint32_t)((e0 / 32) * ldd * 4)); // scales of its two blocks
             } else {
                 dma16(ars, d, av[i], act_soff<F>(a));
             }
@@ -394,7 +407,7 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
 
             const uint8_t *wr = lds + (int)(w % G::NWS) * G::W_SLOT + G::RBW * myrow;
             const uint8_t *xs = lds + G::A_BASE + (int)(a % G::NAS) * G::A_SLOT;
-            if constexpr (I8) {
+            if constexpr (AM == AF_I8) {
                 // int8 form: per block b of the sub-stage one i8 MFMA per token tile, the int32
                 // tile scaled by dA[row] * dB[token] into the fp32 accumulators
                 const uint8_t *wq = wr - G::RBW * l16 + G::RBW * 4 * g; // row 16*wave + 4g (+i)
@@ -433,7 +446,17 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
 #pragma unroll
                 for (int t = 0; t < NB; ++t) {
                     const int r = 16 * t + l16;
-                    bfr[s][t] = *(const f16x8 *)(xs + 128 * r + 16 * ((4 * s + g) ^ act_swz(r)));
+                    if constexpr (AM == AF_F8) {
+                        // 8 e4m3 codes (stored in fragment order) and the block's 2^e scale
+                        const u32x2 c = *(const u32x2 *)(xs + 64 * r + 16 * ((2 * s + (g >> 1)) ^ i8_swz(r)) + 8 * (g & 1));
+                        const float sc = *(const float *)(xs + G::D_OFF + 4 * (G::BN * s + r));
+                        bfr[s][t] = frag4(__builtin_amdgcn_cvt_scalef32_pk_f16_fp8(c.x, sc, false),
+                                          __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(c.x, sc, true),
+                                          __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(c.y, sc, false),
+                                          __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(c.y, sc, true));
+                    } else {
+                        bfr[s][t] = *(const f16x8 *)(xs + 128 * r + 16 * ((4 * s + g) ^ act_swz(r)));
+                    }
                 }
             f16x8 af[RG][2];
 #pragma unroll
@@ -577,26 +600,26 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restric
     }
 }
 
-template <int F, int NB, int RG, bool I8 = false>
+template <int F, int NB, int RG, int AM = AF_F16>
 hipError_t launch_cfg(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P, const GemmPlan &pl, int64_t M,
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
-    using G = Cfg<F, NB, RG, I8>;
+    using G = Cfg<F, NB, RG, AM>;
     dim3 grid((unsigned)((M + G::BM - 1) / G::BM), (unsigned)((N + G::BN - 1) / G::BN), (unsigned)pl.splits);
     float *PP = pl.splits > 1 ? P : nullptr;
     const int cps = pl.chunks_per_split;
-    const void *X = I8 ? (const void *)x.xq : (const void *)x.xdeq;
+    const void *X = G::CODES ? (const void *)x.xq : (const void *)x.xdeq;
 #ifdef GQ_ABLATION
     const int abl = getenv("GQ_ABLATE") ? atoi(getenv("GQ_ABLATE")) : 0;
 #define GQ_ABL_CASE(v) \
-    case v: gemm_kernel<F, NB, RG, v, I8><<<grid, dim3(512), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, cps); break;
+    case v: gemm_kernel<F, NB, RG, v, AM><<<grid, dim3(512), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps); break;
     switch (abl) {
     GQ_ABL_CASE(1) GQ_ABL_CASE(6) GQ_ABL_CASE(8) GQ_ABL_CASE(15) GQ_ABL_CASE(16) GQ_ABL_CASE(31)
-    default: gemm_kernel<F, NB, RG, 0, I8><<<grid, dim3(512), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, cps); break;
+    default: gemm_kernel<F, NB, RG, 0, AM><<<grid, dim3(512), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps); break;
     }
 #undef GQ_ABL_CASE
 #else
-    gemm_kernel<F, NB, RG, 0, I8><<<grid, dim3(512), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, cps);
+    gemm_kernel<F, NB, RG, 0, AM><<<grid, dim3(512), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps);
 #endif
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || pl.splits == 1) return e;
@@ -613,12 +636,18 @@ hipError_t launch_fmt(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P,
     if constexpr (F == Q4_K)
         if (pl.rg == 2 && pl.nb == 8) return launch_cfg<F, 8, 2>(A, x, C, P, pl, M, N, K, ldc, s);
     if constexpr (F == Q8_0)
-        if (pl.i8) switch (pl.nb) {
-            case 1: return launch_cfg<F, 1, 1, true>(A, x, C, P, pl, M, N, K, ldc, s);
-            case 2: return launch_cfg<F, 2, 1, true>(A, x, C, P, pl, M, N, K, ldc, s);
-            case 4: return launch_cfg<F, 4, 1, true>(A, x, C, P, pl, M, N, K, ldc, s);
-            default: return launch_cfg<F, 8, 1, true>(A, x, C, P, pl, M, N, K, ldc, s);
+        if (pl.act == AF_I8) switch (pl.nb) {
+            case 1: return launch_cfg<F, 1, 1, AF_I8>(A, x, C, P, pl, M, N, K, ldc, s);
+            case 2: return launch_cfg<F, 2, 1, AF_I8>(A, x, C, P, pl, M, N, K, ldc, s);
+            case 4: return launch_cfg<F, 4, 1, AF_I8>(A, x, C, P, pl, M, N, K, ldc, s);
+            default: return launch_cfg<F, 8, 1, AF_I8>(A, x, C, P, pl, M, N, K, ldc, s);
             }
+    if (pl.act == AF_F8) switch (pl.nb) {
+        case 1: return launch_cfg<F, 1, 1, AF_F8>(A, x, C, P, pl, M, N, K, ldc, s);
+        case 2: return launch_cfg<F, 2, 1, AF_F8>(A, x, C, P, pl, M, N, K, ldc, s);
+        case 4: return launch_cfg<F, 4, 1, AF_F8>(A, x, C, P, pl, M, N, K, ldc, s);
+        default: return launch_cfg<F, 8, 1, AF_F8>(A, x, C, P, pl, M, N, K, ldc, s);
+        }
     switch (pl.nb) {
     case 1: return launch_cfg<F, 1, 1>(A, x, C, P, pl, M, N, K, ldc, s);
     case 2: return launch_cfg<F, 2, 1>(A, x, C, P, pl, M, N, K, ldc, s);
@@ -633,10 +662,10 @@ int pick_nb(int64_t N) { return N > 64 ? 8 : (N > 32 ? 4 : (N > 16 ? 2 : 1)); }
 
 bool gemm_supported(int /*fmt*/, int64_t K) { return K > 0 && K % 256 == 0; }
 
-GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, bool i8)
+GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, int act)
 {
     GemmPlan p;
-    p.i8 = i8 && fmt == Q8_0;
+    p.act = act == AF_I8 && fmt != Q8_0 ? AF_F16 : act;
     p.nb = pick_nb(N);
     if (const char *env = getenv("GQ_GEMM_NB")) p.nb = atoi(env);
     // two 16-row groups per wave (256-row tiles: half the activation traffic per weight) for
@@ -644,7 +673,9 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, bool i8)
     // (Q4_K only: Q6_K's padded 240-B rows and Q8_0's 272-B rows do not fit 256 rows twice)
     p.rg = (fmt == Q4_K && p.nb == 8 && M >= 8192) ? 2 : 1; // measured: 11008 rows 5% faster
     if (const char *env = getenv("GQ_GEMM_RG")) p.rg = (fmt == Q4_K && p.nb == 8 && atoi(env) == 2) ? 2 : 1;
+    if (p.act != AF_F16) p.rg = 1; // the code forms run 128-row tiles
     const int64_t nws = K / 256; // weight stages (super-blocks)
+    if (nws == 0) return p;      // not a GEMM shape (gemm_supported() is false): nothing to plan
     const int64_t bm = 128 * p.rg;
     const int64_t tiles = ((M + bm - 1) / bm) * ((N + 16 * p.nb - 1) / (16 * p.nb));
     // one workgroup per CU (LDS-bound): the largest split that keeps tiles * S <= 256 CUs, so no

@@ -16,6 +16,8 @@ LIB_DIR = os.path.join(os.path.dirname(_HERE), "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libgguf_mmq.so")
 
 GQ_Q8_0, GQ_Q4_K, GQ_Q6_K = 0, 1, 2
+GQ_ACT_Q8_1, GQ_ACT_FP8_E4M3 = 0, 1
+ACTS = {"q8_1": GQ_ACT_Q8_1, "fp8": GQ_ACT_FP8_E4M3}
 TYPES = {"q8_0": GQ_Q8_0, "q4_k": GQ_Q4_K, "q6_k": GQ_Q6_K}
 BLOCK_ELEMS = {GQ_Q8_0: 32, GQ_Q4_K: 256, GQ_Q6_K: 256}
 BLOCK_BYTES = {GQ_Q8_0: 34, GQ_Q4_K: 144, GQ_Q6_K: 210}
@@ -31,6 +33,11 @@ SIGNATURES = {
     "gq_mmq_prepared": ([_I, _P, _P, _SZ, _P, _I64, _I64, _I64, _I64, _P], _I),
     "gq_quantize_q8_1": ([_P, _P, _I64, _I64, _I64, _P], _I),
     "gq_dequantize": ([_I, _P, _P, _I64, _I64, _I64, _P], _I),
+    "gq_mmq_workspace_size_ex": ([_I, _I, _I64, _I64, _I64], _SZ),
+    "gq_mmq_ex": ([_I, _I, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P], _I),
+    "gq_act_prepare_ex": ([_I, _P, _I64, _I64, _I64, _P, _SZ, _P], _I),
+    "gq_mmq_prepared_ex": ([_I, _I, _P, _P, _SZ, _P, _I64, _I64, _I64, _I64, _P], _I),
+    "gq_quantize_fp8": ([_P, _P, _P, _I64, _I64, _I64, _P], _I),
     "gq_last_error": ([], ctypes.c_char_p),
     "gq_version": ([], _I),
 }
@@ -67,8 +74,8 @@ def _require_device(t: torch.Tensor, name: str):
                            "the MMQ kernels have no CPU path")
 
 
-def workspace_size(gtype: int, M: int, N: int, K: int) -> int:
-    return int(lib().gq_mmq_workspace_size(gtype, M, N, K))
+def workspace_size(gtype: int, M: int, N: int, K: int, act: str = "q8_1") -> int:
+    return int(lib().gq_mmq_workspace_size_ex(gtype, ACTS[act], M, N, K))
 
 
 def _check_weights(gtype: int, A: torch.Tensor, M: int, K: int):
@@ -113,8 +120,9 @@ def _check_workspace(ws: torch.Tensor, need: int, dev):
 
 
 def mmq(gtype: int, A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int,
-        out: torch.Tensor | None = None, workspace: torch.Tensor | None = None) -> torch.Tensor:
-    """C = (A @ B^T)^T as fp16 (N, M) on A's device; the common body of mmq_q8_0/q4_k/q6_k."""
+        out: torch.Tensor | None = None, workspace: torch.Tensor | None = None, act: str = "q8_1") -> torch.Tensor:
+    """C = (A @ B^T)^T as fp16 (N, M) on A's device; the common body of mmq_q8_0/q4_k/q6_k.
+    act="fp8": the fp8 activation variant (gq_mmq_ex, GQ_ACT_FP8_E4M3) instead of q8_1."""
     _check_weights(gtype, A, M, K)
     _require_device(B, "B")
     if A.device != B.device:
@@ -123,13 +131,13 @@ def mmq(gtype: int, A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int,
     C = _check_out(out, N, M, A.device)
     if M == 0 or N == 0:
         return C
-    need = workspace_size(gtype, M, N, K)
+    need = workspace_size(gtype, M, N, K, act)
     if workspace is None or workspace.numel() < need:
         workspace = torch.empty(max(need, 1), dtype=torch.uint8, device=A.device)
     with torch.cuda.device(A.device):
         stream = torch.cuda.current_stream(A.device).cuda_stream
-        _check(lib().gq_mmq(gtype, A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, B.stride(0), C.stride(0),
-                            workspace.data_ptr(), workspace.numel(), stream))
+        _check(lib().gq_mmq_ex(gtype, ACTS[act], A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, B.stride(0),
+                               C.stride(0), workspace.data_ptr(), workspace.numel(), stream))
     return C
 
 
@@ -164,27 +172,42 @@ def dequantize_device(gtype: int, A: torch.Tensor, M: int, K: int) -> torch.Tens
     return W
 
 
-def act_prepare(B: torch.Tensor, N: int, K: int, workspace: torch.Tensor):
-    """Quantize the activations once into the front of `workspace` (gq_act_prepare); any number
-    of mmq_prepared calls with the same (N, K) then reuse them."""
+def act_prepare(B: torch.Tensor, N: int, K: int, workspace: torch.Tensor, act: str = "q8_1"):
+    """Quantize the activations once into the front of `workspace` (gq_act_prepare_ex); any
+    number of mmq_prepared calls with the same (N, K, act) then reuse them."""
     B = _check_acts(B, N, K)
     _check_workspace(workspace, 0, B.device)
     with torch.cuda.device(B.device):
         stream = torch.cuda.current_stream(B.device).cuda_stream
-        _check(lib().gq_act_prepare(B.data_ptr(), N, K, B.stride(0), workspace.data_ptr(), workspace.numel(),
-                                    stream))
+        _check(lib().gq_act_prepare_ex(ACTS[act], B.data_ptr(), N, K, B.stride(0), workspace.data_ptr(),
+                                       workspace.numel(), stream))
 
 
 def mmq_prepared(gtype: int, A: torch.Tensor, workspace: torch.Tensor, M: int, N: int, K: int,
-                 out: torch.Tensor | None = None) -> torch.Tensor:
+                 out: torch.Tensor | None = None, act: str = "q8_1") -> torch.Tensor:
     """C (N, M) fp16 from packed A and the activations act_prepare left in `workspace`."""
     _check_weights(gtype, A, M, K)
-    _check_workspace(workspace, workspace_size(gtype, M, N, K), A.device)
+    _check_workspace(workspace, workspace_size(gtype, M, N, K, act), A.device)
     C = _check_out(out, N, M, A.device)
     if M == 0 or N == 0:
         return C
     with torch.cuda.device(A.device):
         stream = torch.cuda.current_stream(A.device).cuda_stream
-        _check(lib().gq_mmq_prepared(gtype, A.data_ptr(), workspace.data_ptr(), workspace.numel(), C.data_ptr(),
-                                     M, N, K, C.stride(0), stream))
+        _check(lib().gq_mmq_prepared_ex(gtype, ACTS[act], A.data_ptr(), workspace.data_ptr(), workspace.numel(),
+                                        C.data_ptr(), M, N, K, C.stride(0), stream))
     return C
+
+
+def quantize_fp8_device(X: torch.Tensor):
+    """The fp8 variant's activation quantizer (gq_quantize_fp8) -> (codes uint8 (rows, K) in the
+    (0,2,1,3) group order, scales float32 (K/32, (rows+3)&~3))."""
+    _require_device(X, "X")
+    X2 = X.to(torch.float16).reshape(-1, X.shape[-1]).contiguous()
+    rows, K = X2.shape
+    codes = torch.empty((rows, K), dtype=torch.uint8, device=X.device)
+    scales = torch.empty((K // 32, (rows + 3) & ~3), dtype=torch.float32, device=X.device)
+    with torch.cuda.device(X.device):
+        stream = torch.cuda.current_stream(X.device).cuda_stream
+        _check(lib().gq_quantize_fp8(X2.data_ptr(), codes.data_ptr(), scales.data_ptr(), rows, K, X2.stride(0),
+                                     stream))
+    return codes, scales

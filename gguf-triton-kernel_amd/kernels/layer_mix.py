@@ -23,8 +23,8 @@ class GGUFLinear:
     def __call__(self, x: torch.Tensor) -> torch.Tensor:
         return _lib.mmq(self.gtype, self.A, x, self.M, x.shape[0], self.K)
 
-    def workspace_bytes(self, N: int) -> int:
-        return _lib.workspace_size(self.gtype, self.M, N, self.K)
+    def workspace_bytes(self, N: int, act: str = "q8_1") -> int:
+        return _lib.workspace_size(self.gtype, self.M, N, self.K, act)
 
 
 class LayerMix:
@@ -36,11 +36,12 @@ class LayerMix:
 
     GROUPS = (("attn_q", "attn_k", "attn_v"), ("attn_output",), ("ffn_gate", "ffn_up"), ("ffn_down",))
 
-    def __init__(self, linears: dict):
+    def __init__(self, linears: dict, act: str = "q8_1"):
         self.lin = linears
+        self.act = act  # "q8_1" (the reference's activation quantization) or "fp8" (e4m3 variant)
 
     @classmethod
-    def from_gguf(cls, tensors: dict, layer: int, device="cuda"):
+    def from_gguf(cls, tensors: dict, layer: int, device="cuda", act: str = "q8_1"):
         """From read_gguf() tensors named blk.<layer>.<proj>.weight."""
         lins = {}
         for group in cls.GROUPS:
@@ -48,7 +49,7 @@ class LayerMix:
                 t = tensors[f"blk.{layer}.{name}.weight"]
                 M, K = t.shape
                 lins[name] = GGUFLinear(t.type_name, t.to_device(device), M, K)
-        return cls(lins)
+        return cls(lins, act)
 
     def forward(self, x: torch.Tensor, h: torch.Tensor, attn: torch.Tensor | None = None,
                 x_ffn: torch.Tensor | None = None, out: dict | None = None) -> dict:
@@ -56,15 +57,15 @@ class LayerMix:
         inputs = (x, x if attn is None else attn, x if x_ffn is None else x_ffn, h)
         for group, inp in zip(self.GROUPS, inputs):
             N, K = inp.shape
-            if N <= 4:  # decode: each call's kernel quantizes its tokens in LDS (one launch per weight)
+            if N <= 4 and self.act == "q8_1":  # decode: each call quantizes its tokens in LDS (one launch)
                 for n in group:
                     L = self.lin[n]
                     res[n] = _lib.mmq(L.gtype, L.A, inp, L.M, N, K, out=None if out is None else out[n])
                 continue
-            ws_bytes = max(self.lin[n].workspace_bytes(N) for n in group)
+            ws_bytes = max(self.lin[n].workspace_bytes(N, self.act) for n in group)
             ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=inp.device)
-            _lib.act_prepare(inp, N, K, ws)
+            _lib.act_prepare(inp, N, K, ws, act=self.act)
             for n in group:
                 L = self.lin[n]
-                res[n] = _lib.mmq_prepared(L.gtype, L.A, ws, L.M, N, K, None if out is None else out[n])
+                res[n] = _lib.mmq_prepared(L.gtype, L.A, ws, L.M, N, K, None if out is None else out[n], act=self.act)
         return res

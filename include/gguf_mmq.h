@@ -15,6 +15,9 @@
  *   gq_mmq(GQ_Q6_K, ...)  <- kernels/mmq_q6_k.py:197  mmq_q6_k(A, B, M, N, K)
  *   gq_quantize_q8_1      <- utils/quantize/q8_1.py:18 quantize_to_q8_1 (on the device)
  *   gq_dequantize         <- utils/quantize/q4_k.py:125, q6_k.py:117, q8_0.py:52 dequantize (device)
+ * Beyond the reference (no counterpart there):
+ *   gq_*_ex(..., GQ_ACT_FP8_E4M3, ...)  the fp8 activation variant (BASELINE.json configs[4])
+ *   gq_quantize_fp8                     its activation quantizer
  */
 #ifndef GGUF_MMQ_H
 #define GGUF_MMQ_H
@@ -27,6 +30,16 @@ extern "C" {
 #endif
 
 typedef enum { GQ_Q8_0 = 0, GQ_Q4_K = 1, GQ_Q6_K = 2 } gq_type;
+
+/* How the activations are quantized before the matmul.
+ *   GQ_ACT_Q8_1      the reference's semantics: q8_1 (int8 per 32 elements, utils/quantize/q8_1.py).
+ *   GQ_ACT_FP8_E4M3  the fp8 variant: per 32-element block a power-of-two scale X = 2^e (e the
+ *                    smallest integer with max|x| <= 448 * X; X = 1 for an all-zero block) and
+ *                    OCP e4m3 (e4m3fn) codes of x / X, round to nearest even; the weights stay in
+ *                    their GGUF precision (dequantized to fp16 in registers), products exact in
+ *                    fp32.  Needs K % 256 == 0.  Inputs with |x| >= 61440 may round to 65536 and
+ *                    overflow fp16. */
+typedef enum { GQ_ACT_Q8_1 = 0, GQ_ACT_FP8_E4M3 = 1 } gq_act;
 
 enum {
     GQ_OK = 0,
@@ -41,6 +54,7 @@ int gq_block_bytes(gq_type t);
 
 /* Device workspace gq_mmq needs for this shape (bytes; the activation quantizer's output). */
 size_t gq_mmq_workspace_size(gq_type t, int64_t M, int64_t N, int64_t K);
+size_t gq_mmq_workspace_size_ex(gq_type t, gq_act act, int64_t M, int64_t N, int64_t K);
 
 /*
  * C[n * ldc + m] = sum_k W[m][k] * x~[n][k]  for m < M, n < N (fp16 out, fp32 accumulate)
@@ -54,6 +68,9 @@ size_t gq_mmq_workspace_size(gq_type t, int64_t M, int64_t N, int64_t K);
  */
 int gq_mmq(gq_type t, const void *A, const void *B, void *C, int64_t M, int64_t N, int64_t K, int64_t ldb,
            int64_t ldc, void *workspace, size_t workspace_bytes, void *stream);
+/* gq_mmq with the activation format chosen (gq_mmq == gq_mmq_ex(t, GQ_ACT_Q8_1, ...)). */
+int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int64_t M, int64_t N, int64_t K,
+              int64_t ldb, int64_t ldc, void *workspace, size_t workspace_bytes, void *stream);
 
 /*
  * Split form of gq_mmq.  gq_act_prepare quantizes B into the front of `workspace` (that
@@ -70,6 +87,11 @@ int gq_act_prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *works
                    void *stream);
 int gq_mmq_prepared(gq_type t, const void *A, void *workspace, size_t workspace_bytes, void *C, int64_t M, int64_t N,
                     int64_t K, int64_t ldc, void *stream);
+/* The split form with the activation format chosen (both calls must name the same one). */
+int gq_act_prepare_ex(gq_act act, const void *B, int64_t N, int64_t K, int64_t ldb, void *workspace,
+                      size_t workspace_bytes, void *stream);
+int gq_mmq_prepared_ex(gq_type t, gq_act act, const void *A, void *workspace, size_t workspace_bytes, void *C,
+                       int64_t M, int64_t N, int64_t K, int64_t ldc, void *stream);
 
 /*
  * Dequantize packed `t` weights to fp16: W[m * ldw + k] = w (the reference's block formulas,
@@ -84,6 +106,13 @@ int gq_dequantize(gq_type t, const void *A, void *W, int64_t M, int64_t K, int64
  * rows x K fp16 (row stride ldx elements) -> rows * K/32 blocks of 36 bytes, row-major.
  */
 int gq_quantize_q8_1(const void *X, void *Y, int64_t rows, int64_t K, int64_t ldx, void *stream);
+
+/*
+ * The fp8 variant's activation quantizer (GQ_ACT_FP8_E4M3 above) on the device: rows x K fp16
+ * (row stride ldx) -> codes [rows][K] e4m3fn bytes, each 4-element group stored in the order
+ * (0,2,1,3), and scales [K/32][(rows + 3) & ~3] float X = 2^e (block-major).
+ */
+int gq_quantize_fp8(const void *X, void *codes, void *scales, int64_t rows, int64_t K, int64_t ldx, void *stream);
 
 /* Text of the last error on this thread ("" if none). */
 const char *gq_last_error(void);

@@ -139,3 +139,72 @@ def max_rel_err(a, b) -> float:
     mb = float(np.max(np.abs(b))) if b.size else 0.0
     d = float(np.max(np.abs(a - b))) if b.size else 0.0
     return d / mb if mb > 0 else d
+
+
+# ---- fp8 activation variant (BASELINE.json configs[4]; no reference counterpart) ----------
+# The checker for GQ_ACT_FP8_E4M3 (include/gguf_mmq.h): per 32-element block X = 2^e with e the
+# smallest integer such that max|x| <= 448 * 2^e (X = 1 for an all-zero block); codes = OCP
+# e4m3fn(x / X) with round-to-nearest-even.  Restated from the OCP 8-bit floating point
+# specification (e4m3fn: bias 7, no infinities, max normal 448 = 1.75 * 2^8, subnormal step 2^-9).
+
+def e4m3_encode(v) -> np.ndarray:
+    """float32 values with |v| <= 448 -> uint8 e4m3fn codes, round to nearest even."""
+    v = np.asarray(v, np.float32)
+    a = np.abs(v).astype(np.float64)
+    sign = np.signbit(v).astype(np.uint8) << 7
+    _, E = np.frexp(a)                             # a = m * 2^E, m in [0.5, 1)
+    exp = np.maximum(E - 1, -6)                    # exponent of the leading bit, subnormal floor
+    quantum = np.ldexp(1.0, exp - 3)               # 3 mantissa bits
+    q = np.rint(a / quantum)                       # RNE (np.rint: half to even)
+    val = q * quantum
+    sub = val < 2.0 ** -6
+    _, Ev = np.frexp(np.where(sub, 1.0, val))
+    ev = Ev - 1
+    m3 = np.rint((np.where(sub, 1.0, val) / np.ldexp(1.0, ev) - 1.0) * 8).astype(np.int64)
+    bits = np.where(sub, q.astype(np.int64), ((ev + 7) << 3) | m3)
+    assert np.all(bits <= 0x7E), "e4m3 overflow"
+    return (bits.astype(np.uint8) | sign).astype(np.uint8)
+
+
+def e4m3_decode(c) -> np.ndarray:
+    """uint8 e4m3fn codes -> float32 (0x7F / 0xFF NaN codes are never produced here)."""
+    c = np.asarray(c, np.uint8).astype(np.int64)
+    s = np.where(c & 0x80, -1.0, 1.0)
+    e = (c >> 3) & 0xF
+    m = c & 7
+    mag = np.where(e == 0, m * 2.0 ** -9, (1.0 + m / 8.0) * np.ldexp(1.0, e - 7))
+    return (s * mag).astype(np.float32)
+
+
+def quantize_fp8(x_f16):
+    """fp16 (rows, K) -> (codes uint8 (rows, K) in element order, X float32 (rows, K/32))."""
+    x = np.asarray(x_f16, np.float16).astype(np.float32)
+    rows, K = x.shape
+    xb = x.reshape(rows, K // 32, 32)
+    amax = np.abs(xb).max(axis=2)
+    m, E = np.frexp(amax)
+    e = np.where(amax == 0, 0, E - 9 + (m > 0.875))
+    X = np.ldexp(np.float32(1.0), e).astype(np.float32)
+    codes = e4m3_encode(xb / X[:, :, None]).reshape(rows, K)
+    return codes, X
+
+
+def fp8_permuted(codes) -> np.ndarray:
+    """Element order -> the device layout: each 4-group stored (0,2,1,3)."""
+    c = np.asarray(codes).reshape(-1, 4)
+    return c[:, [0, 2, 1, 3]].reshape(np.asarray(codes).shape)
+
+
+def mmq_fp8_ideal(fmt: str, A, B_f16, M: int, N: int, K: int) -> np.ndarray:
+    """The fp8 variant's exact value: fp32 dequantized weights x e4m3-quantized activations,
+    summed in float64, rounded once to fp16 -> (N, M)."""
+    W = dequant(fmt, A).reshape(M, K).astype(np.float64)
+    codes, X = quantize_fp8(B_f16)
+    xt = (e4m3_decode(codes).reshape(N, K // 32, 32) * X[:, :, None]).reshape(N, K).astype(np.float64)
+    return (xt @ W.T).astype(np.float16)
+
+
+def mmq_fp32_dequant(fmt: str, A, B_f16, M: int, N: int, K: int) -> np.ndarray:
+    """fp32-dequant reference with UNquantized activations -> (N, M) float32."""
+    W = dequant(fmt, A).reshape(M, K).astype(np.float64)
+    return (np.asarray(B_f16, np.float16).astype(np.float64) @ W.T).astype(np.float32)

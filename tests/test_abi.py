@@ -64,6 +64,22 @@ def test_host_argument_checks():
     assert L.gq_quantize_q8_1(p, p, 2, 40, 40, None) == 1
 
 
+def test_fp8_host_argument_checks():
+    """The fp8 activation variant's entry points (gq_*_ex with GQ_ACT_FP8_E4M3) refuse shapes the
+    MFMA GEMM cannot take, and unknown activation formats, before any launch."""
+    import kernels._lib as kl
+    L = kl.lib()
+    p = ctypes.c_void_p(16)
+    assert L.gq_mmq_workspace_size_ex(0, 1, 8, 4, 96) > 0  # K % 256 != 0: sized, then refused
+    assert L.gq_mmq_ex(0, 1, p, p, p, 8, 4, 96, 96, 8, p, 1 << 20, None) == 3
+    assert b"256" in L.gq_last_error()
+    assert L.gq_mmq_ex(1, 9, p, p, p, 8, 4, 256, 256, 8, p, 1 << 20, None) == 3
+    assert L.gq_act_prepare_ex(1, p, 4, 96, 96, p, 1 << 20, None) == 3
+    assert L.gq_quantize_fp8(p, p, p, 2, 40, 40, None) == 1
+    for t in (0, 1, 2):
+        assert 0 < kl.workspace_size(t, 4096, 128, 4096, "fp8") < kl.workspace_size(t, 4096, 128, 4096)
+
+
 def test_workspace_sizes():
     import kernels._lib as kl
     for t in (0, 1, 2):
