@@ -34,7 +34,9 @@
 //                 MFMA fragment reads of a lane group hit distinct banks.
 // Two weight-stage slots and an activation ring of up to 4 slots (Cfg below) keep the next
 // sub-stages in flight while one is multiplied; one s_barrier per sub-stage, preceded by a
-// counted vmcnt (never vmcnt(0) inside the loop).
+// counted vmcnt (never vmcnt(0) inside the loop).  The DMAs are issued either by every wave
+// (NL = 0) or by NL = 4 extra loader waves that multiply nothing (the fp16 form's default:
+// the multiplying waves then never stall on vector-memory issue).
 //
 // MFMA 16x16x32 (f16 and i8) maps (gfx950): lane l holds A[row l&15][k 8(l>>4)+j] and
 // B[k 8(l>>4)+j][col l&15]; D[row 4(l>>4)+i][col l&15] in acc element i.  Weight rows are the
@@ -111,10 +113,12 @@ __device__ __forceinline__ uint32_t act_voff(int p) // byte offset of piece p (8
 
 constexpr int NWAVE = 8; // 512 threads: two waves per SIMD
 
-template <int F, int NB, int RG = 1, int AM = AF_F16>
+template <int F, int NB, int RG = 1, int AM = AF_F16, int NL = 0>
 struct Cfg {
-    // 128*RG weight rows x 16*NB tokens; wave w owns rows 16*(RG*w + rg) + [0, 16), rg < RG
+    // 128*RG weight rows x 16*NB tokens; wave w owns rows 16*(RG*w + rg) + [0, 16), rg < RG.
+    // NL > 0: NL more waves that only issue the DMAs (loader waves); 0: every wave issues its share
     static constexpr int BN = 16 * NB, BM = 16 * NWAVE * RG;
+    static constexpr int ISSUERS = NL > 0 ? NL : NWAVE, THREADS = 64 * (NWAVE + NL);
     static constexpr int RBW = WStage<F>::RBW, NPW = RBW / 16;
     static constexpr int W_REAL = BM * NPW / 64;                              // DMA instructions per stage
     // code-form (AF_I8 / AF_F8) activation sub-stage: BN x 64 code bytes (CI instructions), then
@@ -123,7 +127,7 @@ struct Cfg {
     static constexpr int CI = BN * 64 / 1024 > 0 ? BN * 64 / 1024 : 1;
     static constexpr int A_REAL = CODES ? CI + 1 : (BN * 8 / 64 > 0 ? BN * 8 / 64 : 1);
     static constexpr int D_OFF = CI * 1024; // code forms: byte offset of the scales in a slot
-    static constexpr int NW = (W_REAL + NWAVE - 1) / NWAVE, NA = (A_REAL + NWAVE - 1) / NWAVE; // per wave
+    static constexpr int NW = (W_REAL + ISSUERS - 1) / ISSUERS, NA = (A_REAL + ISSUERS - 1) / ISSUERS; // per issuer
     static constexpr int W_SLOT = W_REAL * 1024, A_SLOT = A_REAL * 1024;
     // activation sub-stage ring: as deep as the LDS allows, at most 4*NWS-4 slots (W(w) must
     // be issued before A(4w): see the pipeline note below) and GQ_GEMM_NAS_CAP.  Two weight
@@ -132,7 +136,7 @@ struct Cfg {
     // 6-9% slower on every K-quant shape; tools/gemm_stamps.py)
     static constexpr int NWS = 2;
     // padding DMAs (instruction counts not a multiple of the wave count) land in a scratch KiB
-    static constexpr bool PAD = W_REAL % NWAVE != 0 || A_REAL % NWAVE != 0;
+    static constexpr bool PAD = W_REAL % ISSUERS != 0 || A_REAL % ISSUERS != 0;
     static constexpr int NAS_FIT = (LDS_MAX - (PAD ? 1024 : 0) - NWS * W_SLOT) / A_SLOT;
 #ifndef GQ_GEMM_NAS_CAP // activation ring depth cap: 4 measured best (Q4_K 4096^2 x128: 6 slots
 #define GQ_GEMM_NAS_CAP 4  // 19.6 us, 4 slots 18.8, 3 slots 19.4; Q6_K x128: 3 slots +15%)
@@ -247,13 +251,13 @@ constexpr uint32_t DUMMY = 0u;
 // ABL: ablation bitmask for performance diagnosis (diagnostic build -DGQ_ABLATION only; 0 in
 // production): 1 = no MFMA, 2 = no weight DMA, 4 = no activation DMA, 8 = no dequantization.
 // AF_I8 / AF_F8: X = codes [N][K], XD = block-major scales [K/32][ldd]; AF_F16: X = fp16 x~.
-template <int F, int NB, int RG, int ABL = 0, int AM = AF_F16>
-__global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A, const void *__restrict__ X,
+template <int F, int NB, int RG, int ABL = 0, int AM = AF_F16, int NL = 0>
+__global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *__restrict__ A, const void *__restrict__ X,
                                                    const float *__restrict__ XD, uint16_t *__restrict__ C,
                                                    float *__restrict__ P, int64_t M, int64_t N, int64_t K,
                                                    int64_t ldc, int64_t ldd, int wstages_per_split)
 {
-    using G = Cfg<F, NB, RG, AM>;
+    using G = Cfg<F, NB, RG, AM, NL>;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[G::LDS_BYTES];
 #ifdef GQ_GEMM_STAMPS
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
@@ -262,6 +266,9 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // DMA issuer index: loader waves NWAVE.. (NL > 0), else every wave
+    const bool loader = NL > 0 && wave >= NWAVE;
+    const int iw = NL > 0 ? wave - NWAVE : wave;
     const int g = lane >> 4, l16 = lane & 15;
     const int64_t m0 = (int64_t)blockIdx.x * G::BM;
     const int64_t n0 = (int64_t)blockIdx.y * G::BN;
@@ -288,7 +295,7 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
     int wpc[G::NW];
 #pragma unroll
     for (int i = 0; i < G::NW; ++i) {
-        const int p = 64 * (wave + NWAVE * i) + lane, r = p / G::NPW;
+        const int p = 64 * (iw + G::ISSUERS * i) + lane, r = p / G::NPW;
         wpc[i] = p - r * G::NPW;
         const int64_t row = m0 + r < M ? m0 + r : M - 1;
         wv[i] = r < G::BM ? (uint32_t)(row * row_bytes) : DUMMY;
@@ -301,7 +308,7 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
     uint32_t av[G::NA];
 #pragma unroll
     for (int i = 0; i < G::NA; ++i) {
-        const int k = wave + NWAVE * i, p = 64 * k + lane;
+        const int k = iw + G::ISSUERS * i, p = 64 * k + lane;
         if constexpr (G::CODES) {
             if (k < G::CI) {
                 const int r = p >> 2, q = p & 3, qs = q ^ i8_swz(r);
@@ -326,7 +333,7 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
         uint8_t *dst = lds + (int)(w % G::NWS) * G::W_SLOT;
 #pragma unroll
         for (int i = 0; i < G::NW; ++i) {
-            const int k = wave + NWAVE * i;
+            const int k = iw + G::ISSUERS * i;
             uint32_t vo, so;
             if constexpr (F == Q6_K) { // super-block image: pieces +16i (i < 13) and +194 (d at 222)
                 vo = wv[i] + (uint32_t)WStage<F>::SB * (uint32_t)w + (wpc[i] < 13 ? 16u * wpc[i] : 194u); // piece 14 = 13 again
@@ -343,7 +350,7 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
         uint8_t *dst = lds + G::A_BASE + (int)(a % G::NAS) * G::A_SLOT;
 #pragma unroll
         for (int i = 0; i < G::NA; ++i) {
-            const int k = wave + NWAVE * i;
+            const int k = iw + G::ISSUERS * i;
             uint8_t *d = k < G::A_REAL ? dst + 1024 * k : lds + G::SCRATCH;
             if constexpr (G::CODES) {
                 const uint32_t e0 = act_soff<F>(a) / 2; // first element of the sub-stage
@@ -379,12 +386,28 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
 #ifdef GQ_GEMM_STAMPS
     const unsigned long long t_setup = __builtin_amdgcn_s_memtime() - t_start;
 #endif
+    if (loader) { // loader waves: the DMA schedule of the pipeline note, no multiply
+        if (w0 < w1) {
+            const int64_t a0 = 4 * w0, a1 = 4 * w1;
+#pragma unroll
+            for (int i = 0; i < G::NWS - 1; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
+#pragma unroll
+            for (int i = 0; i < G::NAS - 1; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
+            for (int64_t a = a0; a < a1; ++a) {
+                wait_a((int)(a - a0)); // A(a) landed -> barrier: the compute waves take sub-stage a
+                issue_a(a + G::NAS - 1 < a1 ? a + G::NAS - 1 : a1 - 1);
+                if ((a & 3) == 0) issue_w((a >> 2) + G::NWS - 1 < w1 ? (a >> 2) + G::NWS - 1 : w1 - 1);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        return;
+    }
     if (w0 < w1) {
         const int64_t a0 = 4 * w0, a1 = 4 * w1;
 #pragma unroll
-        for (int i = 0; i < G::NWS - 1; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
+        for (int i = 0; i < G::NWS - 1 && NL == 0; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
 #pragma unroll
-        for (int i = 0; i < G::NAS - 1; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
+        for (int i = 0; i < G::NAS - 1 && NL == 0; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
 #ifdef GQ_GEMM_STAMPS
         t_issued = __builtin_amdgcn_s_memtime() - t_start;
 #endif
@@ -393,7 +416,8 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
 #ifdef GQ_GEMM_STAMPS
             const unsigned long long tw = __builtin_amdgcn_s_memtime();
 #endif
-            wait_a((int)(a - a0));
+            if constexpr (NL > 0) asm volatile("s_barrier" ::: "memory"); // the loaders' wait_a
+            else wait_a((int)(a - a0));
 #ifdef GQ_GEMM_STAMPS
             {
                 const unsigned long long tn = __builtin_amdgcn_s_memtime();
@@ -402,8 +426,10 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
             }
 #endif
             const int64_t w = a >> 2;
-            issue_a(a + G::NAS - 1 < a1 ? a + G::NAS - 1 : a1 - 1);
-            if (s4 == 0) issue_w(w + G::NWS - 1 < w1 ? w + G::NWS - 1 : w1 - 1);
+            if constexpr (NL == 0) {
+                issue_a(a + G::NAS - 1 < a1 ? a + G::NAS - 1 : a1 - 1);
+                if (s4 == 0) issue_w(w + G::NWS - 1 < w1 ? w + G::NWS - 1 : w1 - 1);
+            }
 
             const uint8_t *wr = lds + (int)(w % G::NWS) * G::W_SLOT + G::RBW * myrow;
             const uint8_t *xs = lds + G::A_BASE + (int)(a % G::NAS) * G::A_SLOT;
@@ -483,7 +509,7 @@ __global__ __launch_bounds__(512) void gemm_kernel(const uint8_t *__restrict__ A
                     }
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // no DMA may land after the workgroup exits
+        if constexpr (NL == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // no DMA may land after the workgroup exits
     }
 #ifdef GQ_GEMM_STAMPS
     t_loop = __builtin_amdgcn_s_memtime() - t_start;
@@ -600,11 +626,11 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restric
     }
 }
 
-template <int F, int NB, int RG, int AM = AF_F16>
+template <int F, int NB, int RG, int AM = AF_F16, int NL = 0>
 hipError_t launch_cfg(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P, const GemmPlan &pl, int64_t M,
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
-    using G = Cfg<F, NB, RG, AM>;
+    using G = Cfg<F, NB, RG, AM, NL>;
     dim3 grid((unsigned)((M + G::BM - 1) / G::BM), (unsigned)((N + G::BN - 1) / G::BN), (unsigned)pl.splits);
     float *PP = pl.splits > 1 ? P : nullptr;
     const int cps = pl.chunks_per_split;
@@ -612,14 +638,14 @@ hipError_t launch_cfg(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P,
 #ifdef GQ_ABLATION
     const int abl = getenv("GQ_ABLATE") ? atoi(getenv("GQ_ABLATE")) : 0;
 #define GQ_ABL_CASE(v) \
-    case v: gemm_kernel<F, NB, RG, v, AM><<<grid, dim3(512), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps); break;
+    case v: gemm_kernel<F, NB, RG, v, AM, NL><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps); break;
     switch (abl) {
     GQ_ABL_CASE(1) GQ_ABL_CASE(6) GQ_ABL_CASE(8) GQ_ABL_CASE(15) GQ_ABL_CASE(16) GQ_ABL_CASE(31)
-    default: gemm_kernel<F, NB, RG, 0, AM><<<grid, dim3(512), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps); break;
+    default: gemm_kernel<F, NB, RG, 0, AM, NL><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps); break;
     }
 #undef GQ_ABL_CASE
 #else
-    gemm_kernel<F, NB, RG, 0, AM><<<grid, dim3(512), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps);
+    gemm_kernel<F, NB, RG, 0, AM, NL><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps);
 #endif
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || pl.splits == 1) return e;
@@ -648,6 +674,12 @@ hipError_t launch_fmt(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P,
         case 4: return launch_cfg<F, 4, 1, AF_F8>(A, x, C, P, pl, M, N, K, ldc, s);
         default: return launch_cfg<F, 8, 1, AF_F8>(A, x, C, P, pl, M, N, K, ldc, s);
         }
+    if (pl.loaders == 4) switch (pl.nb) {
+        case 1: return launch_cfg<F, 1, 1, AF_F16, 4>(A, x, C, P, pl, M, N, K, ldc, s);
+        case 2: return launch_cfg<F, 2, 1, AF_F16, 4>(A, x, C, P, pl, M, N, K, ldc, s);
+        case 4: return launch_cfg<F, 4, 1, AF_F16, 4>(A, x, C, P, pl, M, N, K, ldc, s);
+        default: return launch_cfg<F, 8, 1, AF_F16, 4>(A, x, C, P, pl, M, N, K, ldc, s);
+        }
     switch (pl.nb) {
     case 1: return launch_cfg<F, 1, 1>(A, x, C, P, pl, M, N, K, ldc, s);
     case 2: return launch_cfg<F, 2, 1>(A, x, C, P, pl, M, N, K, ldc, s);
@@ -674,6 +706,11 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, int act)
     p.rg = (fmt == Q4_K && p.nb == 8 && M >= 8192) ? 2 : 1; // measured: 11008 rows 5% faster
     if (const char *env = getenv("GQ_GEMM_RG")) p.rg = (fmt == Q4_K && p.nb == 8 && atoi(env) == 2) ? 2 : 1;
     if (p.act != AF_F16) p.rg = 1; // the code forms run 128-row tiles
+    // four loader waves (DMA issue off the multiplying waves' path) for the 128-row fp16 form:
+    // Q6_K 28672x8192x128 116.5 -> 103.7 us, Q4_K 4096^2x128 17.4 -> 16.7, Q8_0 4096^2x128
+    // 20.6 -> 20.1 (profiles/r02/loader_tune.txt); GQ_GEMM_LOADERS=0 restores all-wave issue
+    p.loaders = p.act == AF_F16 && p.rg == 1 ? 4 : 0;
+    if (const char *env = getenv("GQ_GEMM_LOADERS")) p.loaders = p.act == AF_F16 && p.rg == 1 && atoi(env) == 4 ? 4 : 0;
     const int64_t nws = K / 256; // weight stages (super-blocks)
     if (nws == 0) return p;      // not a GEMM shape (gemm_supported() is false): nothing to plan
     const int64_t bm = 128 * p.rg;

@@ -17,7 +17,7 @@ for cfg in "$@"; do
     d="$OUT/$cfg/p$i"
     mkdir -p "$d"
     timeout -k 10 300 rocprofv3 --pmc $ctrs --kernel-trace --output-format csv -d "$d" -o run -- \
-        python3 "$ROOT/bench.py" --config "$cfg" --steps 10 --warmup 2 --no-cpu > "$d/bench.json" 2> "$d/err.txt"
+        python3 "$ROOT/bench.py" --config "$cfg" --steps 10 --warmup 2 --no-cpu --quick > "$d/bench.json" 2> "$d/err.txt"
     rc=$?
     echo "$cfg pass $i ($ctrs): rc=$rc"
     if [ $rc -ne 0 ]; then tail -5 "$d/err.txt"; if [ $rc -ge 124 ]; then exit $rc; fi; fi
