@@ -38,6 +38,7 @@ struct GemmPlan {
     int chunks_per_split = 1;  // 256-wide K stages (super-blocks) per split
     int act = AF_F16;          // activation form (AF_I8: Q8_0 only)
     int loaders = 0;           // 4: four dedicated DMA-issuing waves beside the 8 multiplying ones
+    int pf16 = 0;              // split-K partials stored as fp16 (else fp32)
     size_t partial_bytes = 0;  // fp32 partial slabs needed when splits > 1
 };
 // Activations as the GEMM reads them: fp16 x~ (act_quant DEQ) or, for the code forms, codes +

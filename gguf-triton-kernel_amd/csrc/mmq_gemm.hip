@@ -255,7 +255,7 @@ template <int F, int NB, int RG, int ABL = 0, int AM = AF_F16, int NL = 0>
 __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *__restrict__ A, const void *__restrict__ X,
                                                    const float *__restrict__ XD, uint16_t *__restrict__ C,
                                                    float *__restrict__ P, int64_t M, int64_t N, int64_t K,
-                                                   int64_t ldc, int64_t ldd, int wstages_per_split)
+                                                   int64_t ldc, int64_t ldd, int wstages_per_split, int pf16)
 {
     using G = Cfg<F, NB, RG, AM, NL>;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[G::LDS_BYTES];
@@ -536,14 +536,62 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
         return;
     }
     if (P != nullptr) {
-        // split-K partial: the tile's accumulators in register order, one contiguous BM*BN-float
-        // block per (tile, split): every store instruction writes 1 KiB contiguous
+        // split-K partial: the tile's accumulators in register order, one contiguous block per
+        // (tile, split): every store instruction writes 1 KiB contiguous.  pf16: fp16 partials
+        // (half the bytes; token tiles 2u, 2u+1 side by side in one 16-byte lane store), each
+        // wave's values scaled by 2^-e, e = max(0, E - 14) for their largest |value| in
+        // [2^E, 2^E+1): stored values stay below 2^15 (no overflow, whatever the magnitudes);
+        // e = 0 -- plain fp16 -- whenever every value is below 2^15.  The e's (one int per
+        // wave and block, read by the reduce as a scalar) follow the blocks.
         const int64_t tile = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-        f32x4 *blk = (f32x4 *)(P + (tile * gridDim.z + blockIdx.z) * (int64_t)(G::BM * G::BN));
+        if (pf16) {
+            const int64_t bidx = tile * gridDim.z + blockIdx.z;
+            uint16_t *hb = (uint16_t *)P + bidx * (int64_t)(G::BM * G::BN);
+            float mx = 0.f;
 #pragma unroll
-        for (int rg = 0; rg < RG; ++rg)
+            for (int rg = 0; rg < RG; ++rg)
 #pragma unroll
-            for (int t = 0; t < NB; ++t) blk[((RG * wave + rg) * NB + t) * 64 + lane] = acc[rg][t];
+                for (int t = 0; t < NB; ++t)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) mx = fmaxf(mx, fabsf(acc[rg][t][i]));
+            // wave max: DPP row shifts, row broadcasts 15 / 31 (values >= 0, so the zeros of
+            // out-of-range lanes are harmless), lane 63 holds it
+            int m = __builtin_bit_cast(int, mx);
+            m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x111, 0xf, 0xf, true))));
+            m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x112, 0xf, 0xf, true))));
+            m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x114, 0xf, 0xf, true))));
+            m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x118, 0xf, 0xf, true))));
+            m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x142, 0xa, 0xf, true))));
+            m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x143, 0xc, 0xf, true))));
+            const uint32_t mb = (uint32_t)__builtin_amdgcn_readlane(m, 63);
+            const int E = (int)((mb >> 23) & 0xff) - 127;
+            const int e = E - 14 > 0 ? (E - 14 < 127 ? E - 14 : 126) : 0;
+            const float down = __builtin_bit_cast(float, (uint32_t)(127 - e) << 23);
+            int *es = (int *)((uint16_t *)P + (int64_t)gridDim.x * gridDim.y * gridDim.z * (G::BM * G::BN));
+            if (lane == 0) es[bidx * NWAVE + wave] = e; // (its RG row groups share it)
+            auto pk = [down](const f32x4 &v) {
+                return (u32x2){(uint32_t)f2h_bits(v[0] * down) | ((uint32_t)f2h_bits(v[1] * down) << 16),
+                               (uint32_t)f2h_bits(v[2] * down) | ((uint32_t)f2h_bits(v[3] * down) << 16)};
+            };
+#pragma unroll
+            for (int rg = 0; rg < RG; ++rg) {
+                if constexpr (NB == 1) {
+                    ((u32x2 *)hb)[(RG * wave + rg) * 64 + lane] = pk(acc[rg][0]);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < NB / 2; ++u) {
+                        const u32x2 lo = pk(acc[rg][2 * u]), hi = pk(acc[rg][2 * u + 1]);
+                        ((u32x4 *)hb)[((RG * wave + rg) * (NB / 2) + u) * 64 + lane] = (u32x4){lo.x, lo.y, hi.x, hi.y};
+                    }
+                }
+            }
+        } else {
+            f32x4 *blk = (f32x4 *)(P + (tile * gridDim.z + blockIdx.z) * (int64_t)(G::BM * G::BN));
+#pragma unroll
+            for (int rg = 0; rg < RG; ++rg)
+#pragma unroll
+                for (int t = 0; t < NB; ++t) blk[((RG * wave + rg) * NB + t) * 64 + lane] = acc[rg][t];
+        }
 #ifdef GQ_GEMM_STAMPS
         stamp_out();
 #endif
@@ -578,6 +626,67 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
 // element (q = (wr*NB + t)*64 + lane, i) = D[row 16*wr + 4*(lane>>4) + i][token 16t + (lane&15)]
 // (wr = RG*wave + rg, the wave's row group).
 // One thread per (tile, q): S coalesced 16-byte loads, one 8-byte fp16 store.
+// fp16 partials (pf16): unit q = ((wr*(NB/2) + u)*64 + lane) holds token tiles 2u, 2u+1 of the
+// lane's 4 rows (NB = 1: one tile, 8 bytes), scaled by 2^-e (e per (block, wave), an int each
+// after all blocks); rescaled and summed in fp32 in split order.
+template <int NB, int RG>
+__global__ __launch_bounds__(256) void gemm_reduce_f16_kernel(const uint16_t *__restrict__ P, uint16_t *__restrict__ C,
+                                                              int64_t M, int64_t N, int64_t ldc, int S, int tiles_x,
+                                                              int64_t nq)
+{
+    // one thread per 8-byte item (a token tile's 4 rows of one lane): twice the threads of
+    // 16-byte units, so twice the loads in flight in this latency-bound kernel
+    constexpr int TPU = NB == 1 ? 1 : 2;        // token tiles per 16-byte store unit
+    constexpr int QPT = NWAVE * RG * NB * 64;   // 8-byte items per tile block
+    constexpr int BPT = QPT / 256 > 0 ? QPT / 256 : 1;
+    const int64_t ntiles = nq / QPT;
+    int64_t tile, chunk;
+    if (ntiles % 8 == 0) { // same XCD placement as gemm_reduce_kernel
+        const int64_t i = blockIdx.x / 8;
+        tile = blockIdx.x % 8 + 8 * (i / BPT);
+        chunk = i % BPT;
+    } else {
+        tile = blockIdx.x / BPT;
+        chunk = blockIdx.x % BPT;
+    }
+    const int it = (int)(chunk * 256 + threadIdx.x);
+    if (tile >= ntiles || it >= QPT) return;
+    const int q = TPU == 2 ? it >> 1 : it, j = TPU == 2 ? it & 1 : 0; // unit, tile within the unit
+    const int lane = q & 63, u = (q >> 6) % (NB / TPU), wr = (q >> 6) / (NB / TPU);
+    const int64_t m0 = (tile % tiles_x) * (16 * NWAVE * RG), n0 = (tile / tiles_x) * (16 * NB);
+    const int64_t blk = (int64_t)QPT * 4; // halves per (tile, split) block
+    const int *es = (const int *)(P + ntiles * S * blk);
+    const int wv = __builtin_amdgcn_readfirstlane(wr / RG); // uniform: a reduce wave is one GEMM wave's rows
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int s0 = 0; s0 < S; s0 += 8) {
+        u32x2 v[8];
+        float up[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            up[i] = s0 + i < S ? __builtin_bit_cast(float, (uint32_t)(127 + es[(tile * S + s0 + i) * NWAVE + wv]) << 23) : 0.f;
+            v[i] = s0 + i < S ? ((const u32x2 *)(P + (tile * S + s0 + i) * blk))[it] : (u32x2){0, 0};
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            acc[0] += h2f(v[i].x & 0xffffu) * up[i];
+            acc[1] += h2f(v[i].x >> 16) * up[i];
+            acc[2] += h2f(v[i].y & 0xffffu) * up[i];
+            acc[3] += h2f(v[i].y >> 16) * up[i];
+        }
+    }
+    const int64_t row = m0 + 16 * wr + 4 * (lane >> 4);
+    const int64_t tok = n0 + 16 * (TPU * u + j) + (lane & 15);
+    if (row >= M || tok >= N) return;
+    uint16_t *dst = C + tok * ldc + row;
+    if (row + 4 <= M) {
+        const u32x2 o = {(uint32_t)f2h_bits(acc[0]) | ((uint32_t)f2h_bits(acc[1]) << 16),
+                         (uint32_t)f2h_bits(acc[2]) | ((uint32_t)f2h_bits(acc[3]) << 16)};
+        *(u32x2 *)dst = o;
+    } else {
+        for (int i = 0; i < 4 && row + i < M; ++i) dst[i] = f2h_bits(acc[i]);
+    }
+}
+
 template <int NB, int RG>
 __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restrict__ P, uint16_t *__restrict__ C,
                                                           int64_t M, int64_t N, int64_t ldc, int S, int tiles_x,
@@ -638,17 +747,23 @@ hipError_t launch_cfg(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P,
 #ifdef GQ_ABLATION
     const int abl = getenv("GQ_ABLATE") ? atoi(getenv("GQ_ABLATE")) : 0;
 #define GQ_ABL_CASE(v) \
-    case v: gemm_kernel<F, NB, RG, v, AM, NL><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps); break;
+    case v: gemm_kernel<F, NB, RG, v, AM, NL><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps, pl.pf16); break;
     switch (abl) {
     GQ_ABL_CASE(1) GQ_ABL_CASE(6) GQ_ABL_CASE(8) GQ_ABL_CASE(15) GQ_ABL_CASE(16) GQ_ABL_CASE(31)
-    default: gemm_kernel<F, NB, RG, 0, AM, NL><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps); break;
+    default: gemm_kernel<F, NB, RG, 0, AM, NL><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps, pl.pf16); break;
     }
 #undef GQ_ABL_CASE
 #else
-    gemm_kernel<F, NB, RG, 0, AM, NL><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps);
+    gemm_kernel<F, NB, RG, 0, AM, NL><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps, pl.pf16);
 #endif
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || pl.splits == 1) return e;
+    if (pl.pf16) {
+        const int64_t nq = (int64_t)grid.x * grid.y * (NWAVE * RG * NB * 64);
+        gemm_reduce_f16_kernel<NB, RG><<<dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s>>>(
+            (const uint16_t *)P, C, M, N, ldc, pl.splits, (int)grid.x, nq);
+        return hipGetLastError();
+    }
     const int64_t nq = (int64_t)grid.x * grid.y * (NWAVE * RG * NB * 64);
     gemm_reduce_kernel<NB, RG><<<dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s>>>(P, C, M, N, ldc, pl.splits,
                                                                                          (int)grid.x, nq);
@@ -727,8 +842,14 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, int act)
     S = (nws + sps - 1) / sps;
     p.splits = (int)S;
     p.chunks_per_split = (int)sps;
+    // fp16 partials (default; GQ_GEMM_PARTIAL=f32 for fp32): half the round trip, each wave's
+    // partial values rounded to fp16 after a power-of-two scale that keeps them below 2^15
+    // (Q8_0 4096^2 x128 step 23.2 -> 22.1 us; profiles/r02/pf16_step.txt)
+    p.pf16 = 1;
+    if (const char *env = getenv("GQ_GEMM_PARTIAL")) p.pf16 = env[0] == 'f' && env[1] == '1';
     // blocked partials: S x (tiles) x 128 rows x 16*nb tokens (padded tiles)
-    p.partial_bytes = S > 1 ? (size_t)S * tiles * bm * 16 * p.nb * sizeof(float) : 0;
+    p.partial_bytes = S > 1 ? (size_t)S * tiles * bm * 16 * p.nb * (p.pf16 ? 2 : sizeof(float)) : 0;
+    if (S > 1 && p.pf16) p.partial_bytes += (size_t)S * tiles * NWAVE * sizeof(int); // the per-wave e's
     return p;
 }
 

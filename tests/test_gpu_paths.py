@@ -171,3 +171,26 @@ def test_gemm_weights_over_4gib():
     assert O.max_rel_err(got, ideal) <= TIGHT_GEMM
     del A_t
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("partial", ("f16", "f32"))
+def test_split_k_partials_huge_cancelling_sums(partial, monkeypatch):
+    """Split-K partial sums far outside fp16's range whose total cancels to ~0: the second half
+    of K repeats the first half's weights against negated activations.  fp16 partials carry a
+    per-wave power-of-two scale, so neither form overflows (no inf/NaN) and both cancel."""
+    from kernels._lib import TYPES, mmq
+    monkeypatch.setenv("GQ_GEMM_PARTIAL", partial)
+    monkeypatch.setenv("GQ_GEMM_SPLITS", "8")
+    dev = _dev()
+    M, N, K = 256, 128, 4096
+    half = random_blocks("q8_0", M, K // 2, seed=31).reshape(M, -1)
+    qA = np.concatenate([half, half], axis=1).reshape(-1)
+    x = (random_activations(N, K // 2, seed=32).astype(np.float32) * 20000).clip(-60000, 60000).astype(np.float16)
+    B = np.concatenate([x, -x], axis=1)
+    C = mmq(TYPES["q8_0"], torch.from_numpy(qA.view(np.int8)).to(dev), torch.from_numpy(B).to(dev), M, N, K)
+    torch.cuda.synchronize()
+    got = C.float().cpu().numpy()
+    assert np.isfinite(got).all()
+    first = np.abs(O.mmq_from_fp16("q8_0", half.reshape(-1), x, M, N, K // 2, O.IDEAL).astype(np.float32)).max()
+    assert first == np.inf or first > 65504  # the half sums overflow fp16 (so do the split partials)
+    assert np.abs(got).max() <= 1e-4 * 65504
