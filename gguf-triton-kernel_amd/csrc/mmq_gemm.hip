@@ -134,14 +134,21 @@ struct Cfg {
     // slots (one super-block ahead): at kernel start every workgroup's prologue DMAs are issued
     // together, and a smaller burst lands the first sub-stage sooner (three slots measured
     // 6-9% slower on every K-quant shape; tools/gemm_stamps.py)
-    static constexpr int NWS = 2;
+#ifndef GQ_GEMM_SMALL_NWS // weight-stage slots for 16- and 32-token tiles (latency-bound: deeper rings)
+#define GQ_GEMM_SMALL_NWS 2
+#endif
+#ifndef GQ_GEMM_SMALL_NAS_CAP
+#define GQ_GEMM_SMALL_NAS_CAP 4
+#endif
+    static constexpr int NWS = NB <= 2 ? GQ_GEMM_SMALL_NWS : 2;
     // padding DMAs (instruction counts not a multiple of the wave count) land in a scratch KiB
     static constexpr bool PAD = W_REAL % ISSUERS != 0 || A_REAL % ISSUERS != 0;
     static constexpr int NAS_FIT = (LDS_MAX - (PAD ? 1024 : 0) - NWS * W_SLOT) / A_SLOT;
 #ifndef GQ_GEMM_NAS_CAP // activation ring depth cap: 4 measured best (Q4_K 4096^2 x128: 6 slots
 #define GQ_GEMM_NAS_CAP 4  // 19.6 us, 4 slots 18.8, 3 slots 19.4; Q6_K x128: 3 slots +15%)
 #endif
-    static constexpr int NAS_MAX = 4 * NWS - 4 < GQ_GEMM_NAS_CAP ? 4 * NWS - 4 : GQ_GEMM_NAS_CAP;
+    static constexpr int NAS_CAP = NB <= 2 ? GQ_GEMM_SMALL_NAS_CAP : GQ_GEMM_NAS_CAP;
+    static constexpr int NAS_MAX = 4 * NWS - 4 < NAS_CAP ? 4 * NWS - 4 : NAS_CAP;
     static constexpr int NAS = NAS_FIT < NAS_MAX ? NAS_FIT : NAS_MAX;
     static constexpr int A_BASE = NWS * W_SLOT, SCRATCH = A_BASE + NAS * A_SLOT; // dummy DMAs land there
     static constexpr int LDS_BYTES = SCRATCH + (PAD ? 1024 : 0);
