@@ -478,7 +478,10 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
             }
         }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // no DMA may land after the wave exits
+    // no DMA may land after the wave exits: every issued task was waited for in the loop, so
+    // only a wave without tasks (its task-0 DMA is never waited for) has one in flight; the
+    // output stores need no wait
+    if (ntask == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifdef GQ_DECODE_STAMPS
     const unsigned long long t_end = __builtin_amdgcn_s_memtime();
     const int gw_id = blockIdx.x * DW + wave;
