@@ -666,12 +666,22 @@ __global__ __launch_bounds__(256) void gemm_reduce_f16_kernel(const uint16_t *__
     const int wv = __builtin_amdgcn_readfirstlane(wr / RG); // uniform: a reduce wave is one GEMM wave's rows
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int s0 = 0; s0 < S; s0 += 8) {
+        // every load unconditional (split index clamped), the surplus zeroed after: a load
+        // under a per-split condition compiles to a branch and a wait per split (8 serialized
+        // round trips)
         u32x2 v[8];
+        int ev[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int64_t sp = tile * S + (s0 + i < S ? s0 + i : S - 1);
+            ev[i] = es[sp * NWAVE + wv];
+            v[i] = ((const u32x2 *)(P + sp * blk))[it];
+        }
         float up[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            up[i] = s0 + i < S ? __builtin_bit_cast(float, (uint32_t)(127 + es[(tile * S + s0 + i) * NWAVE + wv]) << 23) : 0.f;
-            v[i] = s0 + i < S ? ((const u32x2 *)(P + (tile * S + s0 + i) * blk))[it] : (u32x2){0, 0};
+            up[i] = __builtin_bit_cast(float, (uint32_t)(127 + ev[i]) << 23);
+            if (s0 + i >= S) v[i] = (u32x2){0, 0};
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -726,7 +736,10 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restric
     for (int s0 = 0; s0 < S; s0 += 8) {
         f32x4 v[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = s0 + i < S ? src[(int64_t)(s0 + i) * QPT] : (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < 8; ++i) v[i] = src[(int64_t)(s0 + i < S ? s0 + i : S - 1) * QPT]; // unconditional (see above)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (s0 + i >= S) v[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc += v[i];
     }
