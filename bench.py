@@ -491,11 +491,12 @@ def bench_config(name, steps, warmup, dev):
     return out
 
 
-def bench_layer(Ns, acts, steps, warmup, dev):
+def bench_layer(Ns, acts, steps, warmup, dev, fuse=True):
     """BASELINE configs[4]: the seven projections of a Llama-7B block under GGUF Q4_K_M (layer 0:
     attn_v and ffn_down in Q6_K, the rest Q4_K), shared inputs quantized once per group
-    (kernels.layer_mix.LayerMix), for each token count in Ns and activation format in acts
-    ("q8_1": the reference's semantics; "fp8": the e4m3 variant).  Weights rotate over >= 1 GiB."""
+    (kernels.layer_mix.LayerMix; fuse: q+k and gate+up as one call each), for each token count in
+    Ns and activation format in acts ("q8_1": the reference's semantics; "fp8": the e4m3 variant).
+    Weights rotate over >= 1 GiB."""
     from gguf import LLAMA_LAYER_SHAPES, q4_k_m_layer_types
     from kernels.layer_mix import GGUFLinear, LayerMix
     types = q4_k_m_layer_types(0, 32)
@@ -506,14 +507,14 @@ def bench_layer(Ns, acts, steps, warmup, dev):
              for n in LLAMA_LAYER_SHAPES} for c in range(ncopies)]
     res = []
     for act in acts:
-        layers = [LayerMix(lin, act=act) for lin in lins]
+        layers = [LayerMix(lin, act=act, fuse=fuse) for lin in lins]
         for N in Ns:
             g = torch.Generator(device=dev).manual_seed(7)
             x = torch.randn(N, 4096, device=dev, generator=g).to(torch.float16)
             h = torch.randn(N, 11008, device=dev, generator=g).to(torch.float16)
             outs = {n: torch.empty(N, M, dtype=torch.float16, device=dev) for n, (M, K) in LLAMA_LAYER_SHAPES.items()}
             flops = sum(2.0 * N * M * K for M, K in LLAMA_LAYER_SHAPES.values())
-            for i in range(max(1, warmup)):  # also creates any library handles outside capture
+            for i in range(max(ncopies, warmup)):  # library handles, every copy's buffers: outside capture
                 layers[i % ncopies].forward(x, h, out=outs)
             torch.cuda.synchronize(dev)
             gr = torch.cuda.CUDAGraph()
@@ -528,7 +529,7 @@ def bench_layer(Ns, acts, steps, warmup, dev):
                     layers[i % ncopies].forward(x, h, out=outs)
             gr.replay()
             t = min(timed_replay(gr, dev) for _ in range(3)) / steps
-            res.append({"config": f"q4_k_m_llama7b_layer_m{N}", "act": act, "fmt": "q4_k+q6_k", "M_tok": N,
+            res.append({"config": f"q4_k_m_llama7b_layer_m{N}", "act": act, "fused": fuse, "fmt": "q4_k+q6_k", "M_tok": N,
                         "us_per_step": round(t * 1e6, 2), "tflops": round(flops / t / 1e12, 3),
                         "weight_GBps": round(layer_bytes / t / 1e9, 1)})
             del gr
@@ -595,6 +596,8 @@ def main():
     ap.add_argument("--quick", action="store_true", help="headline only: no per-type sweep")
     ap.add_argument("--sweep", action="store_true", help="(the default; kept for old command lines)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--layer-only", action="store_true",
+                    help="print only the Q4_K_M layer sweep (fused and unfused), one JSON line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -616,6 +619,11 @@ def main():
         else:
             dist.init_process_group(backend)
     torch.cuda.set_device(dev)
+    if args.layer_only:
+        Ns = (1, 2, 4, 8, 16, 32, 64, 128, 256, 512)
+        print(json.dumps([bench_layer(Ns, ("q8_1",), max(20, args.steps // 4), args.warmup, dev, fuse=f)
+                          for f in (True, False)]), flush=True)
+        return
     name = STRONG[1] if args.strong else args.config
     fmt, M, K, N = CONFIGS[name]
     sweep_steps = max(20, args.steps // 4)
@@ -642,6 +650,7 @@ def main():
                 sweep.append(bench_config(sname, sweep_steps, args.warmup, dev))
         sweep.append(bench_layer((1, 2, 4, 8, 16, 32, 64, 128, 256, 512), ("q8_1", "fp8"), sweep_steps, args.warmup,
                                  dev))
+        sweep.append(bench_layer((1, 16, 128, 512), ("q8_1",), sweep_steps, args.warmup, dev, fuse=False))
         sweep.append(bench_msweep(sweep_steps, args.warmup, dev))
         sweep.extend(bench_fp8(("q8_0_4096x4096_m128", "q4_k_11008x4096_m128", "q6_k_28672x8192_m128",
                                 "q4_k_4096x4096_m1"), sweep_steps, args.warmup, dev))

@@ -1,10 +1,15 @@
 """Mixed-format (GGUF Q4_K_M) projection stack of a Llama block on the MMQ kernels.
 
 BASELINE.json configs[4] / SURVEY.md 8(f)4 (no reference counterpart).  Each projection is a
-packed GGUF weight of its own type (gguf.mix.q4_k_m_layer_types); projections that share an
-input (q/k/v, gate/up) quantize it once (gq_act_prepare) and run gq_mmq_prepared per
-weight -- the dispatch is by type, per matrix, with no repacking.  At decode sizes (N <= 4)
-every call is the one-launch fused decode kernel instead (its quantizer is in-kernel).
+packed GGUF weight of its own type (gguf.mix.q4_k_m_layer_types); the dispatch is by type,
+per matrix.  Projections that read the same input and have the same GGUF type (q/k, and v too
+when it is not the Q6_K one; gate/up) are fused once at construction: their packed rows are
+copied end to end into one device buffer (the bytes are unchanged -- a packed row is whole
+blocks), so each such set is ONE call (one activation quantization, one launch, the split-K
+plan of the taller matrix) whose (N, sum M) output is returned as per-projection column views.
+Sets that share an input but differ in type quantize the input once (gq_act_prepare) and run
+gq_mmq_prepared per weight; at decode sizes (N <= 4) every call is the one-launch fused decode
+kernel (its quantizer is in-kernel).
 """
 from __future__ import annotations
 
@@ -36,12 +41,37 @@ class LayerMix:
 
     GROUPS = (("attn_q", "attn_k", "attn_v"), ("attn_output",), ("ffn_gate", "ffn_up"), ("ffn_down",))
 
-    def __init__(self, linears: dict, act: str = "q8_1"):
-        self.lin = linears
+    def __init__(self, linears: dict, act: str = "q8_1", fuse: bool = True):
         self.act = act  # "q8_1" (the reference's activation quantization) or "fp8" (e4m3 variant)
+        self.lin = {}     # name -> GGUFLinear (unfused projections)
+        self.parts = {}   # name -> (fused key, first column, rows)
+        # per input group: the calls to make, each (key, GGUFLinear); fused keys join names by "+"
+        self.calls = []
+        for group in self.GROUPS:
+            by_type = {}
+            for n in group:
+                by_type.setdefault(linears[n].type_name, []).append(n)
+            calls = []
+            for names in by_type.values():
+                if fuse and len(names) > 1:
+                    L0 = linears[names[0]]
+                    A = torch.cat([linears[n].A.reshape(-1) for n in names])  # rows end to end
+                    M = sum(linears[n].M for n in names)
+                    key = "+".join(names)
+                    col = 0
+                    for n in names:
+                        self.parts[n] = (key, col, linears[n].M)
+                        col += linears[n].M
+                    calls.append((key, GGUFLinear(L0.type_name, A, M, L0.K)))
+                else:
+                    for n in names:
+                        self.lin[n] = linears[n]
+                        calls.append((n, linears[n]))
+            self.calls.append(calls)
+        self._fused_out = {}
 
     @classmethod
-    def from_gguf(cls, tensors: dict, layer: int, device="cuda", act: str = "q8_1"):
+    def from_gguf(cls, tensors: dict, layer: int, device="cuda", act: str = "q8_1", fuse: bool = True):
         """From read_gguf() tensors named blk.<layer>.<proj>.weight."""
         lins = {}
         for group in cls.GROUPS:
@@ -49,23 +79,41 @@ class LayerMix:
                 t = tensors[f"blk.{layer}.{name}.weight"]
                 M, K = t.shape
                 lins[name] = GGUFLinear(t.type_name, t.to_device(device), M, K)
-        return cls(lins, act)
+        return cls(lins, act, fuse)
+
+    def _out(self, key, L, N, dev, out):
+        """Output buffer of one call: the caller's for an unfused projection, else ours."""
+        if "+" not in key:
+            return None if out is None else out[key]
+        buf = self._fused_out.get(key)
+        if buf is None or buf.shape[0] != N or buf.device != dev:
+            buf = torch.empty((N, L.M), dtype=torch.float16, device=dev)
+            self._fused_out[key] = buf
+        return buf
 
     def forward(self, x: torch.Tensor, h: torch.Tensor, attn: torch.Tensor | None = None,
                 x_ffn: torch.Tensor | None = None, out: dict | None = None) -> dict:
+        """{name: (N, M) fp16}.  Fused projections come back as column views of their set's
+        (N, sum M) output (kept by the layer and rewritten by the next forward); `out` supplies
+        the buffers of unfused ones."""
         res = {}
         inputs = (x, x if attn is None else attn, x if x_ffn is None else x_ffn, h)
-        for group, inp in zip(self.GROUPS, inputs):
+        for calls, inp in zip(self.calls, inputs):
             N, K = inp.shape
-            if N <= 4 and self.act == "q8_1":  # decode: each call quantizes its tokens in LDS (one launch)
-                for n in group:
-                    L = self.lin[n]
-                    res[n] = _lib.mmq(L.gtype, L.A, inp, L.M, N, K, out=None if out is None else out[n])
-                continue
-            ws_bytes = max(self.lin[n].workspace_bytes(N, self.act) for n in group)
-            ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=inp.device)
-            _lib.act_prepare(inp, N, K, ws, act=self.act)
-            for n in group:
-                L = self.lin[n]
-                res[n] = _lib.mmq_prepared(L.gtype, L.A, ws, L.M, N, K, None if out is None else out[n], act=self.act)
+            if (N <= 4 and self.act == "q8_1") or len(calls) == 1:
+                # decode (each call quantizes its tokens in-kernel), or a single call
+                for key, L in calls:
+                    res[key] = _lib.mmq(L.gtype, L.A, inp, L.M, N, K, out=self._out(key, L, N, inp.device, out),
+                                        act=self.act)
+            else:
+                ws_bytes = max(L.workspace_bytes(N, self.act) for _, L in calls)
+                ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=inp.device)
+                _lib.act_prepare(inp, N, K, ws, act=self.act)
+                for key, L in calls:
+                    res[key] = _lib.mmq_prepared(L.gtype, L.A, ws, L.M, N, K, self._out(key, L, N, inp.device, out),
+                                                 act=self.act)
+        for n, (key, col, rows) in self.parts.items():
+            res[n] = res[key][:, col:col + rows]
+        for key in [k for k in res if "+" in k]:
+            del res[key]
         return res

@@ -262,10 +262,11 @@ def test_blas_path(fmt, M, N, K, force, monkeypatch):
     assert O.allclose(exact, got, 0.01)
 
 
-def test_layer_mix_from_gguf(tmp_path):
+@pytest.mark.parametrize("fuse", (True, False))
+def test_layer_mix_from_gguf(tmp_path, fuse):
     """Q4_K_M-typed layer read from a GGUF file; each projection group reads its own input
     (x for q/k/v, the attention output for attn_output, the FFN input for gate/up, h for
-    ffn_down), shared-input groups quantized once."""
+    ffn_down), shared-input groups quantized once; fused: q+k and gate+up as one call each."""
     from gguf import q4_k_m_layer_types, read_gguf, write_gguf
     from kernels.layer_mix import LayerMix
     types = q4_k_m_layer_types(0, 32)  # layer 0: attn_v / ffn_down in Q6_K
@@ -275,8 +276,8 @@ def test_layer_mix_from_gguf(tmp_path):
     p = tmp_path / "l.gguf"
     write_gguf(p, {f"blk.0.{n}.weight": (types[n], shapes[n], raw[n]) for n in shapes})
     _, tens = read_gguf(p)
-    layer = LayerMix.from_gguf(tens, 0, device=_dev())
-    for N in (1, 20):
+    layer = LayerMix.from_gguf(tens, 0, device=_dev(), fuse=fuse)
+    for N in (1, 3, 20, 128):
         x, a, y = (random_activations(N, 512, seed=N + 10 * i) for i in range(3))
         h = random_activations(N, 768, seed=N + 1)
         d = {k: torch.from_numpy(v).to(_dev()) for k, v in (("x", x), ("a", a), ("y", y), ("h", h))}

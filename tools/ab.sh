@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 STEP=""; if [ "$1" = "--step" ]; then STEP="--step"; shift; fi
 A=""
 for r in $(seq ${AB_R:-3}); do for s in "$@"; do A="$A $s"; done; done
-timeout -k 10 500 python tools/gemm_tune.py $STEP $A 2>&1 | grep kernel_us | python3 -c "
+timeout -k 10 500 python tools/gemm_tune.py ${AB_LIB:+--lib=$AB_LIB} $STEP $A 2>&1 | grep kernel_us | python3 -c "
 import sys, collections
 d = collections.OrderedDict()
 for l in sys.stdin:
