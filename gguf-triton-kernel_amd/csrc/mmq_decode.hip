@@ -38,7 +38,7 @@
 namespace gq {
 
 #ifdef GQ_DECODE_STAMPS // diagnostic build: per-wave s_memtime breakdown (never the product)
-__device__ unsigned long long g_dstamps[65536][8];
+__device__ unsigned long long g_dstamps[65536][12];
 #endif
 
 namespace {
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 #ifdef GQ_DECODE_STAMPS
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-    unsigned long long t_wait = 0;
+    unsigned long long t_wait = 0, t_w0 = 0, t_c0 = 0;
 #endif
     const int64_t tok0 = (int64_t)blockIdx.y * NT;
     const int nb = K / 32;
@@ -399,6 +399,8 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifdef GQ_DECODE_STAMPS
         t_wait += __builtin_amdgcn_s_memtime() - ta;
+        if (j == 0) t_w0 = __builtin_amdgcn_s_memtime();
+        if (j == 1) t_c0 = ta;
 #endif
 
         uint32_t st, len;
@@ -494,6 +496,10 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
         g_dstamps[gw_id][5] = t_q - t_start;
         g_dstamps[gw_id][6] = t_start;
         g_dstamps[gw_id][7] = t_end;
+        g_dstamps[gw_id][8] = t_w0;
+        g_dstamps[gw_id][9] = t_c0 ? t_c0 : t_end;
+        g_dstamps[gw_id][10] = t_pro;
+        g_dstamps[gw_id][11] = (unsigned long long)blockIdx.x;
     }
 #endif
 }

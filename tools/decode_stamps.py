@@ -23,7 +23,7 @@ for cfg in sys.argv[1:] or ["q6_k_28672x8192_m1"]:
     for i in range(8):
         r.step(i)
     torch.cuda.synchronize()
-    buf = np.zeros((65536, 8), np.uint64)
+    buf = np.zeros((65536, 12), np.uint64)
     assert kl.lib().gq_debug_decode_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes) == 0
     used = buf[buf[:, 3] > 0].astype(np.float64)
     pro, wait, loop, nt = used[:, 0], used[:, 1], used[:, 2], used[:, 3]
@@ -35,4 +35,12 @@ for cfg in sys.argv[1:] or ["q6_k_28672x8192_m1"]:
           f"compute/task={np.median((loop - wait) / nt):.0f}")
     print(f"   prologue: x-arrival med={np.median(xw):.0f}  quantized med={np.median(qd):.0f}  "
           f"barrier med={np.median(pro - qd):.0f}")
+    w0, c0, tp = used[:, 8], used[:, 9], used[:, 10]
+    T0 = t0.min()
+    print(f"   kernel span={t1.max() - T0:.0f}  wave starts: med={np.median(t0 - T0):.0f} max={(t0 - T0).max():.0f}  "
+          f"ends: med={np.median(t1 - T0):.0f}  first DMA landed after barrier: med={np.median(w0 - tp):.0f}  "
+          f"first task compute: med={np.median(c0 - w0):.0f}")
+    for q in (10, 50, 90):
+        print(f"   p{q}: start={np.percentile(t0 - T0, q):.0f} barrier={np.percentile(tp - T0, q):.0f} "
+              f"dma0={np.percentile(w0 - T0, q):.0f} end={np.percentile(t1 - T0, q):.0f}")
     del r
