@@ -140,7 +140,10 @@ struct Cfg {
 #ifndef GQ_GEMM_SMALL_NAS_CAP
 #define GQ_GEMM_SMALL_NAS_CAP 4
 #endif
-    static constexpr int NWS = NB <= 2 ? GQ_GEMM_SMALL_NWS : 2;
+#ifndef GQ_GEMM_NWS // weight-stage slots for 64- and 128-token tiles
+#define GQ_GEMM_NWS 2
+#endif
+    static constexpr int NWS = NB <= 2 ? GQ_GEMM_SMALL_NWS : GQ_GEMM_NWS;
     // padding DMAs (instruction counts not a multiple of the wave count) land in a scratch KiB
     static constexpr bool PAD = W_REAL % ISSUERS != 0 || A_REAL % ISSUERS != 0;
     static constexpr int NAS_FIT = (LDS_MAX - (PAD ? 1024 : 0) - NWS * W_SLOT) / A_SLOT;
@@ -256,7 +259,10 @@ constexpr uint32_t DUMMY = 0u;
 // A(4(w-NWS+1)+NAS-1), which is older than A(4w) iff NAS <= 4*NWS-4.  Past the end the indices are clamped (re-loads of identical
 // bytes into the same slot) so every wave issues the same sequence.
 // ABL: ablation bitmask for performance diagnosis (diagnostic build -DGQ_ABLATION only; 0 in
-// production): 1 = no MFMA, 2 = no weight DMA, 4 = no activation DMA, 8 = no dequantization.
+// production): 1 = no MFMA, 2 = no weight DMA, 4 = no activation DMA, 8 = no dequantization,
+// 16 = no epilogue, 32 = activation DMAs with the addresses of a sub-stage-blocked layout,
+// 64 = weight DMAs with the addresses of a stage-contiguous (tiled) layout, 128 = a quarter of
+// the activation fragment reads.
 // AF_I8 / AF_F8: X = codes [N][K], XD = block-major scales [K/32][ldd]; AF_F16: X = fp16 x~.
 template <int F, int NB, int RG, int ABL = 0, int AM = AF_F16, int NL = 0>
 __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *__restrict__ A, const void *__restrict__ X,
@@ -330,7 +336,10 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
         } else {
             const int r = p >> 3, q = p & 7;
             const int64_t tok = n0 + r < N ? n0 + r : N - 1;
-            av[i] = r < G::BN ? (uint32_t)(tok * K * 2) + act_voff<F>(q ^ act_swz(r)) : DUMMY;
+            if constexpr ((ABL & 32) != 0) // diagnostic: the access pattern of a sub-stage-blocked layout
+                av[i] = r < G::BN ? (uint32_t)(tok * 128) + 16u * (q ^ act_swz(r)) : DUMMY;
+            else
+                av[i] = r < G::BN ? (uint32_t)(tok * K * 2) + act_voff<F>(q ^ act_swz(r)) : DUMMY;
         }
     }
     const int myrow = 16 * RG * wave + l16; // the row this lane multiplies (row group 0)
@@ -342,7 +351,10 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
         for (int i = 0; i < G::NW; ++i) {
             const int k = iw + G::ISSUERS * i;
             uint32_t vo, so;
-            if constexpr (F == Q6_K) { // super-block image: pieces +16i (i < 13) and +194 (d at 222)
+            if constexpr ((ABL & 64) != 0) { // diagnostic: the stage as one contiguous run (a tiled layout)
+                vo = (uint32_t)(m0 * row_bytes) + 16u * (uint32_t)(64 * k + lane);
+                so = (uint32_t)(w * G::BM * G::RBW);
+            } else if constexpr (F == Q6_K) { // super-block image: pieces +16i (i < 13) and +194 (d at 222)
                 vo = wv[i] + (uint32_t)WStage<F>::SB * (uint32_t)w + (wpc[i] < 13 ? 16u * wpc[i] : 194u); // piece 14 = 13 again
                 so = 0;
             } else {
@@ -363,6 +375,8 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
                 const uint32_t e0 = act_soff<F>(a) / 2; // first element of the sub-stage
                 if (k < G::CI) dma16(ars, d, av[i], e0);
                 else dma16(drs, d, av[i], (uint32_t)((e0 / 32) * ldd * 4)); // scales of its two blocks
+            } else if constexpr ((ABL & 32) != 0) {
+                dma16(ars, d, av[i], (uint32_t)(a * N * 128));
             } else {
                 dma16(ars, d, av[i], act_soff<F>(a));
             }
@@ -487,6 +501,9 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
                                           __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(c.x, sc, true),
                                           __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(c.y, sc, false),
                                           __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(c.y, sc, true));
+                    } else if constexpr ((ABL & 128) != 0) { // diagnostic: a quarter of the fragment reads
+                        bfr[s][t] = t < NB / 4 || NB < 4 ? *(const f16x8 *)(xs + 128 * r + 16 * ((4 * s + g) ^ act_swz(r)))
+                                                         : bfr[s][t % (NB / 4)];
                     } else {
                         bfr[s][t] = *(const f16x8 *)(xs + 128 * r + 16 * ((4 * s + g) ^ act_swz(r)));
                     }
@@ -769,7 +786,8 @@ hipError_t launch_cfg(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P,
 #define GQ_ABL_CASE(v) \
     case v: gemm_kernel<F, NB, RG, v, AM, NL><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps, pl.pf16); break;
     switch (abl) {
-    GQ_ABL_CASE(1) GQ_ABL_CASE(6) GQ_ABL_CASE(8) GQ_ABL_CASE(15) GQ_ABL_CASE(16) GQ_ABL_CASE(31)
+    GQ_ABL_CASE(1) GQ_ABL_CASE(6) GQ_ABL_CASE(8) GQ_ABL_CASE(15) GQ_ABL_CASE(16) GQ_ABL_CASE(31) GQ_ABL_CASE(32)
+    GQ_ABL_CASE(33) GQ_ABL_CASE(2) GQ_ABL_CASE(4) GQ_ABL_CASE(64) GQ_ABL_CASE(68) GQ_ABL_CASE(96) GQ_ABL_CASE(128) GQ_ABL_CASE(134)
     default: gemm_kernel<F, NB, RG, 0, AM, NL><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps, pl.pf16); break;
     }
 #undef GQ_ABL_CASE
@@ -795,7 +813,9 @@ hipError_t launch_fmt(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P,
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
     if constexpr (F == Q4_K)
-        if (pl.rg == 2 && pl.nb == 8) return launch_cfg<F, 8, 2>(A, x, C, P, pl, M, N, K, ldc, s);
+        if (pl.rg == 2 && pl.nb == 8)
+            return pl.loaders == 4 ? launch_cfg<F, 8, 2, AF_F16, 4>(A, x, C, P, pl, M, N, K, ldc, s)
+                                   : launch_cfg<F, 8, 2>(A, x, C, P, pl, M, N, K, ldc, s);
     if constexpr (F == Q8_0)
         if (pl.act == AF_I8) switch (pl.nb) {
             case 1: return launch_cfg<F, 1, 1, AF_I8>(A, x, C, P, pl, M, N, K, ldc, s);
@@ -845,7 +865,7 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, int act)
     // Q6_K 28672x8192x128 116.5 -> 103.7 us, Q4_K 4096^2x128 17.4 -> 16.7, Q8_0 4096^2x128
     // 20.6 -> 20.1 (profiles/r02/loader_tune.txt); GQ_GEMM_LOADERS=0 restores all-wave issue
     p.loaders = p.act == AF_F16 && p.rg == 1 ? 4 : 0;
-    if (const char *env = getenv("GQ_GEMM_LOADERS")) p.loaders = p.act == AF_F16 && p.rg == 1 && atoi(env) == 4 ? 4 : 0;
+    if (const char *env = getenv("GQ_GEMM_LOADERS")) p.loaders = p.act == AF_F16 && atoi(env) == 4 ? 4 : 0;
     const int64_t nws = K / 256; // weight stages (super-blocks)
     if (nws == 0) return p;      // not a GEMM shape (gemm_supported() is false): nothing to plan
     const int64_t bm = 128 * p.rg;

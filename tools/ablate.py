@@ -7,7 +7,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "gguf-triton-kernel_amd")]
 import kernels._lib as kl  # noqa: E402
 
-kl.LIB_PATH = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gguf-triton-kernel_amd", "build", "abl",
+kl.LIB_PATH = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gguf-triton-kernel_amd", "lib",
                                                                    "libgguf_mmq_abl.so")
 import torch  # noqa: E402
 

@@ -1,0 +1,119 @@
+// probe_fill.hip -- per-CU LDS fill rate from an L2-resident buffer, the GEMM's activation
+// pattern (8 token rows x 128 B per 1 KiB wave instruction, rows 8 KiB apart), by
+//   mode 0: LDS-DMA (buffer_load_dwordx4 ... lds), 1 KiB per instruction
+//   mode 1: register staging (global_load_dwordx4 -> VGPRs -> ds_write_b128)
+// with L loader waves per CU, optionally beside R reader waves that stream ds_read_b128 over
+// the filled slots (the multiplying waves' fragment reads).  One workgroup per CU, 256 CUs.
+// Build: hipcc -O3 --offload-arch=gfx950 -o probe_fill tools/probes/probe_fill.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int SLOT = 16 * 1024, NSLOT = 4;
+
+template <int MODE, int L, int R>
+__global__ __launch_bounds__(64 * (L + R)) void fill_kernel(const unsigned char *__restrict__ src, int iters,
+                                                            unsigned *__restrict__ out)
+{
+    __shared__ __attribute__((aligned(1024))) unsigned char lds[NSLOT * SLOT];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)src, 0, 1 << 20, 0x00020000);
+    unsigned acc = 0;
+    if (wave < L) {
+        // instruction k of a slot: pieces p = 64k + lane: token p >> 3, piece p & 7
+        constexpr int NK = SLOT / 1024 / L;
+        auto off_of = [&](int it, int j) {
+            const unsigned base = (unsigned)((it * 128 + blockIdx.x * 4096) & ((1 << 19) - 1));
+            const int k = wave + L * j, p = 64 * k + lane, tok = p >> 3, q = p & 7;
+            return base + (unsigned)tok * 8192u % (1u << 19) + 16u * q;
+        };
+        if constexpr (MODE == 0) {
+            for (int it = 0; it < iters; ++it) {
+                unsigned char *slot = lds + (it % NSLOT) * SLOT;
+#pragma unroll
+                for (int j = 0; j < NK; ++j)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void *)(slot + 1024 * (wave + L * j)), 16,
+                                                             off_of(it, j), 0, 0, 0);
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NK) : "memory"); // 2 slots in flight
+            }
+        } else {
+            // two slots of loads in registers ahead of the LDS writes
+            u32x4 b0[NK], b1[NK];
+#pragma unroll
+            for (int j = 0; j < NK; ++j) b0[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off_of(0, j), 0, 0);
+#pragma unroll
+            for (int j = 0; j < NK; ++j) b1[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off_of(1, j), 0, 0);
+            for (int it = 0; it < iters; it += 2) {
+                unsigned char *slot = lds + (it % NSLOT) * SLOT;
+#pragma unroll
+                for (int j = 0; j < NK; ++j) *(u32x4 *)(slot + 1024 * (wave + L * j) + 16 * lane) = b0[j];
+#pragma unroll
+                for (int j = 0; j < NK; ++j) b0[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off_of(it + 2, j), 0, 0);
+                slot = lds + ((it + 1) % NSLOT) * SLOT;
+#pragma unroll
+                for (int j = 0; j < NK; ++j) *(u32x4 *)(slot + 1024 * (wave + L * j) + 16 * lane) = b1[j];
+#pragma unroll
+                for (int j = 0; j < NK; ++j) b1[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off_of(it + 3, j), 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        // readers: ds_read_b128 sweeps over the ring, iters * 16 KiB per wave (a GEMM
+        // sub-stage's fragment reads are the whole 16 KiB slot per wave)
+        const int n = iters * SLOT / 1024;
+        for (int i = 0; i < n; ++i) {
+            const u32x4 v = *(const u32x4 *)(lds + ((i * 1024 + 16 * lane) & (NSLOT * SLOT - 1)));
+            acc ^= v.x + v.w;
+        }
+    }
+    if (acc == 0x9e3779b9u) out[blockIdx.x] = acc;
+}
+
+template <int MODE, int L, int R>
+float run(const unsigned char *src, unsigned *out, int iters)
+{
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    fill_kernel<MODE, L, R><<<256, 64 * (L + R)>>>(src, iters, out);
+    hipDeviceSynchronize();
+    float best = 1e30f;
+    for (int t = 0; t < 5; ++t) {
+        hipEventRecord(a);
+        fill_kernel<MODE, L, R><<<256, 64 * (L + R)>>>(src, iters, out);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        if (ms < best) best = ms;
+    }
+    const double bytes = (double)iters * SLOT; // per CU
+    printf("mode %s loaders %d readers %d: %.1f us  %.1f GB/s per CU  %.1f B/cycle/CU (2.4 GHz)\n",
+           MODE == 0 ? "lds-dma " : "reg-stage", L, R, best * 1e3, bytes / (best * 1e-3) / 1e9,
+           bytes / (best * 1e-3) / 2.4e9);
+    return best;
+}
+
+int main()
+{
+    unsigned char *src;
+    unsigned *out;
+    hipMalloc(&src, 1 << 20);
+    hipMemset(src, 1, 1 << 20);
+    hipMalloc(&out, 4096);
+    const int iters = 400; // 6.4 MB per CU
+    run<0, 4, 0>(src, out, iters);
+    run<1, 4, 0>(src, out, iters);
+    run<0, 4, 8>(src, out, iters);
+    run<1, 4, 8>(src, out, iters);
+    run<0, 8, 0>(src, out, iters);
+    run<1, 8, 0>(src, out, iters);
+    run<0, 2, 0>(src, out, iters);
+    run<1, 2, 0>(src, out, iters);
+    run<0, 1, 0>(src, out, iters);
+    return 0;
+}
