@@ -193,4 +193,6 @@ def test_split_k_partials_huge_cancelling_sums(partial, monkeypatch):
     assert np.isfinite(got).all()
     first = np.abs(O.mmq_from_fp16("q8_0", half.reshape(-1), x, M, N, K // 2, O.IDEAL).astype(np.float32)).max()
     assert first == np.inf or first > 65504  # the half sums overflow fp16 (so do the split partials)
-    assert np.abs(got).max() <= 1e-4 * 65504
+    # the split partials reach ~1e8 (fp32 ulp 8): what is left is a few ulps of the reduce's
+    # fp32 summation order (the halves cancel split by split only up to that order)
+    assert np.abs(got).max() <= 256
