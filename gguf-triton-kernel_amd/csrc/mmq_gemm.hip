@@ -229,7 +229,13 @@ __device__ __forceinline__ void stage_frags<Q6_K>(const uint8_t *wr, int g, int 
     }
 }
 
-// Q8_0 sub-stage u: blocks 2u, 2u+1 of the stage's 8.
+// Q8_0 sub-stage u: blocks 2u, 2u+1 of the stage's 8.  The 8 code bytes of a lane start 2, 4
+// or 6 bytes past an 8-byte boundary (34-byte blocks): unaligned ds_read_b64 stall the LDS
+// (SQ_LDS_UNALIGNED_STALL), so two aligned 8-byte reads and a byte shift (the offset is the
+// same for every lane of the sub-stage) are used instead (GQ_Q8_UNALIGNED=1: the direct read).
+#ifndef GQ_Q8_UNALIGNED
+#define GQ_Q8_UNALIGNED 0
+#endif
 template <>
 __device__ __forceinline__ void stage_frags<Q8_0>(const uint8_t *wr, int g, int u, f16x8 (&frag)[2])
 {
@@ -238,7 +244,19 @@ __device__ __forceinline__ void stage_frags<Q8_0>(const uint8_t *wr, int g, int 
     for (int b = 0; b < 2; ++b) {
         const uint8_t *blk = wr + 34 * (2 * u + b);
         const h2 d = splat(h2f(*(const uint16_t *)blk));
+#if GQ_Q8_UNALIGNED
         const u32x2 q = *(const u32x2 *)(blk + 2 + 8 * g); // 2-byte aligned: gfx950 LDS runs unaligned
+#else
+        // wr is 16-byte aligned (RBW = 272): the shift depends on u and b only
+        const int off = 34 * (2 * u + b) + 2, sh = off & 7;
+        const uint8_t *al = wr + (off & ~7) + 8 * g;
+        const u32x2 lo = *(const u32x2 *)al, hi = *(const u32x2 *)(al + 8);
+        u32x2 q;
+        if (sh == 0) q = lo;
+        else if (sh < 4) q = (u32x2){__builtin_amdgcn_alignbyte(lo.y, lo.x, sh), __builtin_amdgcn_alignbyte(hi.x, lo.y, sh)};
+        else if (sh == 4) q = (u32x2){lo.y, hi.x};
+        else q = (u32x2){__builtin_amdgcn_alignbyte(hi.x, lo.y, sh - 4), __builtin_amdgcn_alignbyte(hi.y, hi.x, sh - 4)};
+#endif
         const uint32_t c0 = q.x ^ 0x80808080u, c1 = q.y ^ 0x80808080u;
         frag[b] = frag4((pair02(c0) + bias) * d, (pair13(c0) + bias) * d, (pair02(c1) + bias) * d,
                         (pair13(c1) + bias) * d);

@@ -15,6 +15,11 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int SLOT = 16 * 1024, NSLOT = 4;
 
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, unsigned char *dst, unsigned off)
+{
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void *)dst, 16, off, 0, 0, 0);
+}
+
 template <int MODE, int L, int R>
 __global__ __launch_bounds__(64 * (L + R)) void fill_kernel(const unsigned char *__restrict__ src, int iters,
                                                             unsigned *__restrict__ out)
@@ -36,9 +41,8 @@ __global__ __launch_bounds__(64 * (L + R)) void fill_kernel(const unsigned char 
                 unsigned char *slot = lds + (it % NSLOT) * SLOT;
 #pragma unroll
                 for (int j = 0; j < NK; ++j)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void *)(slot + 1024 * (wave + L * j)), 16,
-                                                             off_of(it, j), 0, 0, 0);
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NK) : "memory"); // 2 slots in flight
+                    dma16(rs, slot + 1024 * (wave + L * j), off_of(it, j));
+                __builtin_amdgcn_s_waitcnt(0x0f70 | ((2 * NK) & 15) | (((2 * NK) >> 4) << 14)); // vmcnt(2NK): 2 slots in flight
             }
         } else {
             // two slots of loads in registers ahead of the LDS writes
