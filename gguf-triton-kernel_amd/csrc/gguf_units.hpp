@@ -34,6 +34,21 @@ __device__ __forceinline__ void act_blocks(int u, int &b0, int &b1)
 template <int F> struct UnitLoad;
 template <int F> struct UnitRaw;
 
+// N dwords starting at a 2-byte aligned LDS address p, read as dword-aligned words and shifted
+// into place: an LDS read that is not dword-aligned stalls the LDS pipeline
+// (SQ_LDS_UNALIGNED_STALL was ~90% of the Q6_K/Q8_0 decode kernels' LDS cycles).
+template <int N>
+__device__ __forceinline__ void lds_words(const uint8_t *p, uint32_t (&o)[N])
+{
+    const uint32_t *a = (const uint32_t *)((uintptr_t)p & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(uintptr_t)p & 3u;
+    uint32_t w[N + 1];
+#pragma unroll
+    for (int k = 0; k <= N; ++k) w[k] = a[k];
+#pragma unroll
+    for (int k = 0; k < N; ++k) o[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+}
+
 // ---- Q8_0: two blocks ----
 template <> struct UnitLoad<Q8_0> {
     uint32_t d0b, d1b;
@@ -50,6 +65,24 @@ template <> struct UnitLoad<Q8_0> {
         a1 = ld16(p0 + 18);
         a2 = ld16(p1 + 2);
         a3 = ld16(p1 + 18);
+    }
+    // from LDS (the decode ring): the block pair as 17 dword-aligned words (p is 4-byte
+    // aligned there); a missing second block reads bytes of no consequence (its d is zeroed)
+    __device__ __forceinline__ void load_lds(const uint8_t *__restrict__ rowp, int u, int64_t /*nb32*/)
+    {
+        const uint32_t *w = (const uint32_t *)(rowp + 68 * u);
+        uint32_t x[17];
+#pragma unroll
+        for (int k = 0; k < 17; ++k) x[k] = w[k];
+        d0b = x[0] & 0xffffu;
+        d1b = x[8] >> 16;
+        uint32_t c[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) c[k] = __builtin_amdgcn_alignbyte(x[k + 1], x[k], 2);
+        a0 = (u32x4){c[0], c[1], c[2], c[3]};
+        a1 = (u32x4){c[4], c[5], c[6], c[7]};
+        a2 = (u32x4){x[9], x[10], x[11], x[12]};
+        a3 = (u32x4){x[13], x[14], x[15], x[16]};
     }
 };
 
@@ -125,6 +158,22 @@ template <> struct UnitLoad<Q6_K> {
         g1 = ld16(p + 144 + 32 * h);
         sc8 = ld8(p + 192 + 8 * h);
         dbits = ld2(p + 208);
+    }
+    // from LDS (the decode ring): every field has the block's 2-byte misalignment
+    __device__ __forceinline__ void load_lds(const uint8_t *__restrict__ rowp, int u, int64_t /*nb32*/)
+    {
+        const int sb = u >> 2, h = (u >> 1) & 1, v = u & 1;
+        const uint8_t *p = rowp + 210 * (int64_t)sb;
+        uint32_t l[8], g[8], s[2];
+        lds_words<8>(p + 64 * h + 32 * v, l);
+        lds_words<8>(p + 128 + 32 * h, g);
+        lds_words<2>(p + 192 + 8 * h, s);
+        l0 = (u32x4){l[0], l[1], l[2], l[3]};
+        l1 = (u32x4){l[4], l[5], l[6], l[7]};
+        g0 = (u32x4){g[0], g[1], g[2], g[3]};
+        g1 = (u32x4){g[4], g[5], g[6], g[7]};
+        sc8 = (u32x2){s[0], s[1]};
+        dbits = *(const uint16_t *)(p + 208);
     }
 };
 

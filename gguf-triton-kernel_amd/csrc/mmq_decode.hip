@@ -356,6 +356,8 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
             // because direct reads here made the waitcnt pass add a vmcnt(0) before them, i.e.
             // wait for the task DMA just issued -- tools/check_waits.py)
             UnitLoad<Q6_K> l0, l1;
+            // (plain 2-byte aligned reads: the dword-aligned form, UnitLoad::load_lds, cut the
+            // unaligned-LDS stalls but measured 7-10% slower here -- profiles/r02/decode_lds_align_ab.txt)
             l0.load(rowp, 2 * c, nb);
             l1.load(rowp, 2 * c + 1, nb);
             unit(l0, 2 * c, 2 * i, acc);
@@ -369,7 +371,10 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
         ((uint32_t *)&l)[0] = (uint32_t)(uintptr_t)rowp + u;
         ((uint32_t *)&l)[3] = (uint32_t)u * 77u;
 #else
-        l.load(rowp, u, nb);
+        // Q8_0: dword-aligned reads and a 2-byte shift (4096^2 decode 6.6 -> 5.6 us); Q4_K
+        // blocks are 16-byte aligned in the ring; Q6_K: see above
+        if constexpr (F == Q8_0) l.load_lds(rowp, u, nb);
+        else l.load(rowp, u, nb);
 #endif
 #ifdef GQ_ABL_NODOT
         const uint32_t *w = (const uint32_t *)&l;
