@@ -39,8 +39,6 @@ struct GemmPlan {
     int act = AF_F16;          // activation form (AF_I8: Q8_0 only)
     int loaders = 0;           // 4: four dedicated DMA-issuing waves beside the 8 multiplying ones
     int pf16 = 0;              // split-K partials stored as fp16 (else fp32)
-    int lsplit = 0;            // split loader waves (2 weight + 2 activation) with a 3-stage weight ring
-    int wreg = 0;              // weights loaded to registers per wave (fp16 form, loader waves, 128-row tiles)
     size_t partial_bytes = 0;  // fp32 partial slabs needed when splits > 1
 };
 // Activations as the GEMM reads them: fp16 x~ (act_quant DEQ) or, for the code forms, codes +

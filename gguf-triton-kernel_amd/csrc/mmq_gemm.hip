@@ -113,26 +113,21 @@ __device__ __forceinline__ uint32_t act_voff(int p) // byte offset of piece p (8
 
 constexpr int NWAVE = 8; // 512 threads: two waves per SIMD
 
-template <int F, int NB, int RG = 1, int AM = AF_F16, int NL = 0, int WR = 0, int LS = 0>
+template <int F, int NB, int RG = 1, int AM = AF_F16, int NL = 0>
 struct Cfg {
     // 128*RG weight rows x 16*NB tokens; wave w owns rows 16*(RG*w + rg) + [0, 16), rg < RG.
     // NL > 0: NL more waves that only issue the DMAs (loader waves); 0: every wave issues its share
     static constexpr int BN = 16 * NB, BM = 16 * NWAVE * RG;
-    // LS > 0 (split loaders): LS loader waves issue only the weight stages and NL - LS only the
-    // activation sub-stages, so each stream is counted by its own waves' vmcnt (an in-order
-    // count would make every activation wait for the weight stages issued before it)
     static constexpr int ISSUERS = NL > 0 ? NL : NWAVE, THREADS = 64 * (NWAVE + NL);
-    static constexpr int WISS = LS > 0 ? LS : ISSUERS, AISS = LS > 0 ? NL - LS : ISSUERS;
     static constexpr int RBW = WStage<F>::RBW, NPW = RBW / 16;
-    // WR: the weights go to registers (per-wave loads), no weight DMA and no weight slots
-    static constexpr int W_REAL = WR ? 0 : BM * NPW / 64;                     // DMA instructions per stage
+    static constexpr int W_REAL = BM * NPW / 64;                              // DMA instructions per stage
     // code-form (AF_I8 / AF_F8) activation sub-stage: BN x 64 code bytes (CI instructions), then
     // one instruction for the tile's scales of the sub-stage's two blocks (2 x BN floats)
     static constexpr bool CODES = AM != AF_F16;
     static constexpr int CI = BN * 64 / 1024 > 0 ? BN * 64 / 1024 : 1;
     static constexpr int A_REAL = CODES ? CI + 1 : (BN * 8 / 64 > 0 ? BN * 8 / 64 : 1);
     static constexpr int D_OFF = CI * 1024; // code forms: byte offset of the scales in a slot
-    static constexpr int NW = (W_REAL + WISS - 1) / WISS, NA = (A_REAL + AISS - 1) / AISS; // per issuer
+    static constexpr int NW = (W_REAL + ISSUERS - 1) / ISSUERS, NA = (A_REAL + ISSUERS - 1) / ISSUERS; // per issuer
     static constexpr int W_SLOT = W_REAL * 1024, A_SLOT = A_REAL * 1024;
     // activation sub-stage ring: as deep as the LDS allows, at most 4*NWS-4 slots (W(w) must
     // be issued before A(4w): see the pipeline note below) and GQ_GEMM_NAS_CAP.  Two weight
@@ -148,21 +143,15 @@ struct Cfg {
 #ifndef GQ_GEMM_NWS // weight-stage slots for 64- and 128-token tiles
 #define GQ_GEMM_NWS 2
 #endif
-#ifndef GQ_GEMM_LS_NWS // weight-stage slots with split loaders
-#define GQ_GEMM_LS_NWS 3
-#endif
-    static constexpr int NWS = WR ? 0 : (LS > 0 ? GQ_GEMM_LS_NWS : (NB <= 2 ? GQ_GEMM_SMALL_NWS : GQ_GEMM_NWS));
+    static constexpr int NWS = NB <= 2 ? GQ_GEMM_SMALL_NWS : GQ_GEMM_NWS;
     // padding DMAs (instruction counts not a multiple of the wave count) land in a scratch KiB
-    static constexpr bool PAD = W_REAL % WISS != 0 || A_REAL % AISS != 0;
+    static constexpr bool PAD = W_REAL % ISSUERS != 0 || A_REAL % ISSUERS != 0;
     static constexpr int NAS_FIT = (LDS_MAX - (PAD ? 1024 : 0) - NWS * W_SLOT) / A_SLOT;
 #ifndef GQ_GEMM_NAS_CAP // activation ring depth cap: 4 measured best (Q4_K 4096^2 x128: 6 slots
 #define GQ_GEMM_NAS_CAP 4  // 19.6 us, 4 slots 18.8, 3 slots 19.4; Q6_K x128: 3 slots +15%)
 #endif
     static constexpr int NAS_CAP = NB <= 2 ? GQ_GEMM_SMALL_NAS_CAP : GQ_GEMM_NAS_CAP;
-#ifndef GQ_GEMM_WR_NAS_CAP // activation ring cap when the weights bypass LDS
-#define GQ_GEMM_WR_NAS_CAP 8
-#endif
-    static constexpr int NAS_MAX = WR || LS ? GQ_GEMM_WR_NAS_CAP : (4 * NWS - 4 < NAS_CAP ? 4 * NWS - 4 : NAS_CAP);
+    static constexpr int NAS_MAX = 4 * NWS - 4 < NAS_CAP ? 4 * NWS - 4 : NAS_CAP;
     static constexpr int NAS = NAS_FIT < NAS_MAX ? NAS_FIT : NAS_MAX;
     static constexpr int A_BASE = NWS * W_SLOT, SCRATCH = A_BASE + NAS * A_SLOT; // dummy DMAs land there
     static constexpr int LDS_BYTES = SCRATCH + (PAD ? 1024 : 0);
@@ -171,9 +160,7 @@ struct Cfg {
     static_assert(!CODES || BN <= 128, "code forms: <= 128 tokens per tile");
     static_assert(LDS_BYTES <= LDS_MAX, "LDS budget");
     static_assert(NAS >= 3, "activation ring depth");
-    static_assert((LS > 0 ? (NAS - 2) * NA : (NAS - 2) * NA + 2 * NW) <= 63, "vmcnt range");
-    static_assert(LS == 0 || (NL > LS && NWS >= 2 && !WR), "split loaders");
-    static_assert(!WR || (NL > 0 && RG == 1 && AM == AF_F16), "register weights: loader waves, 128-row tiles, fp16 form");
+    static_assert((NAS - 2) * NA + 2 * NW <= 63, "vmcnt range");
 };
 
 // ---------------------------------------------------------------------------------------
@@ -263,128 +250,6 @@ __device__ __forceinline__ void stage_frags<Q8_0>(const uint8_t *wr, int g, int 
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// Register weights (WR): every wave loads its own 16 rows' bytes of a super-block stage
-// straight into registers (a wave's A operand is private to it: nothing to share through LDS).
-// Lane (l16, g) takes 16 contiguous bytes per load; the K order inside a stage is permuted so
-// that those bytes are exactly the lane's MFMA elements (the activation DMA applies the same
-// permutation: act_soff_wr / act_voff_wr).  Per stage and lane:
-//   Q4_K: header 16 B + qs [64p + 16g, +16) for p = 0, 1.  Sub-stage s4 = 2p + t, k-step s:
-//         nibble t of bytes 8s.. of the pair-p load = elements 128p + 32t + 64(g>>1) +
-//         16(g&1) + 8s + [0,8), sub-block 4p + 2(g>>1) + t.
-//   Q8_0: per pair c (= sub-stage): block b = 2c + (g>>1), codes [16(g&1), +16) and its d.
-//         k-step s: codes 16(g&1) + 8s.. = elements 64c + 32(g>>1) + 16(g&1) + 8s + [0,8).
-//   Q6_K: ql [64h + 16g, +16), qh [128 + 32h + 16(g&1), +16) for h = 0, 1, scales, d.
-//         Sub-stage s4 = 2h + q, k-step s (nibble): elements 128h + 64s + 16g + 8q + [0,8),
-//         qh shift 2(g>>1) + 4s, scale 8h + 4s + g.
-template <int F> struct WRegs;
-template <> struct WRegs<Q4_K> { u32x4 hdr, q[2]; };
-template <> struct WRegs<Q8_0> { u32x4 c[4]; uint32_t d[4]; };
-template <> struct WRegs<Q6_K> { u32x4 ql[2], qh[2], sc; uint32_t d; };
-
-template <int F>
-__device__ __forceinline__ void load_wregs(WRegs<F> &r, const uint8_t *row, int64_t w, int g)
-{
-    if constexpr (F == Q4_K) {
-        const uint8_t *b = row + 144 * w;
-        r.hdr = ld16(b);
-        r.q[0] = ld16(b + 16 + 16 * g);
-        r.q[1] = ld16(b + 80 + 16 * g);
-    } else if constexpr (F == Q8_0) {
-        const uint8_t *b = row + 272 * w + 34 * (g >> 1);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            r.c[c] = ld16(b + 68 * c + 2 + 16 * (g & 1));
-            r.d[c] = ld2(b + 68 * c);
-        }
-    } else {
-        const uint8_t *b = row + 210 * w;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            r.ql[h] = ld16(b + 64 * h + 16 * g);
-            r.qh[h] = ld16(b + 128 + 32 * h + 16 * (g & 1));
-        }
-        r.sc = ld16(b + 192);
-        r.d = ld2(b + 208);
-    }
-}
-
-template <int F>
-__device__ __forceinline__ void reg_frags(const WRegs<F> &r, int g, int s4, f16x8 (&frag)[2])
-{
-    if constexpr (F == Q4_K) {
-        const int p = s4 >> 1, t = s4 & 1, j = 2 * (g >> 1) + t; // sub-block 4p + j
-        const float d = h2f(r.hdr.x & 0xffffu), dmin = h2f(r.hdr.x >> 16);
-        const uint32_t sh = 8 * j;
-        int sc, m;
-        if (p == 0) { // get_scale_min_k4, j < 4
-            sc = (int)((r.hdr.y >> sh) & 63u);
-            m = (int)((r.hdr.z >> sh) & 63u);
-        } else {
-            const uint32_t hi = (r.hdr.w >> sh) & 0xffu;
-            sc = (int)((hi & 0x0fu) | (((r.hdr.y >> sh) & 0xc0u) >> 2));
-            m = (int)((hi >> 4) | (((r.hdr.z >> sh) & 0xc0u) >> 2));
-        }
-        const h2 ds = splat(d * (float)sc), ndm = splat(-(dmin * (float)m));
-        const h2 bias = splat(-1024.f);
-        const u32x4 q = r.q[p];
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const uint32_t x0 = (s ? q.z : q.x) >> (4 * t), x1 = (s ? q.w : q.y) >> (4 * t);
-            frag[s] = frag4(__builtin_elementwise_fma(magic(x0, 0x000f000fu) + bias, ds, ndm),
-                            __builtin_elementwise_fma(magic(x0 >> 8, 0x000f000fu) + bias, ds, ndm),
-                            __builtin_elementwise_fma(magic(x1, 0x000f000fu) + bias, ds, ndm),
-                            __builtin_elementwise_fma(magic(x1 >> 8, 0x000f000fu) + bias, ds, ndm));
-        }
-    } else if constexpr (F == Q8_0) {
-        const h2 bias = splat(-1152.f);
-        const h2 d = splat(h2f(r.d[s4]));
-        const u32x4 c = r.c[s4];
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const uint32_t c0 = (s ? c.z : c.x) ^ 0x80808080u, c1 = (s ? c.w : c.y) ^ 0x80808080u;
-            frag[s] = frag4((pair02(c0) + bias) * d, (pair13(c0) + bias) * d, (pair02(c1) + bias) * d,
-                            (pair13(c1) + bias) * d);
-        }
-    } else {
-        const int h = s4 >> 1, q = s4 & 1;
-        const float d = h2f(r.d);
-        const u32x4 L = r.ql[h], H = r.qh[h];
-        const uint32_t l0 = q ? L.z : L.x, l1 = q ? L.w : L.y, q0 = q ? H.z : H.x, q1 = q ? H.w : H.y;
-        const uint32_t scw[4] = {r.sc.x, r.sc.y, r.sc.z, r.sc.w};
-        const h2 bias = splat(-1056.f); // 1024 + 32
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int sq = 2 * (g >> 1) + 4 * s;
-            const float scv = (float)(int8_t)((scw[2 * h + s] >> (8 * g)) & 0xffu);
-            const h2 dsc = splat(d * scv);
-            const uint32_t c0 = ((l0 >> (4 * s)) & 0x0f0f0f0fu) | (((q0 >> sq) & 0x03030303u) << 4);
-            const uint32_t c1 = ((l1 >> (4 * s)) & 0x0f0f0f0fu) | (((q1 >> sq) & 0x03030303u) << 4);
-            frag[s] = frag4((pair02(c0) + bias) * dsc, (pair13(c0) + bias) * dsc, (pair02(c1) + bias) * dsc,
-                            (pair13(c1) + bias) * dsc);
-        }
-    }
-}
-
-// activation sub-stage a of the register-weight order: its first element (x2 bytes) and
-// piece j = 4s + g's element offset (x2 bytes) in it
-template <int F>
-__device__ __forceinline__ uint32_t act_soff_wr(int64_t a)
-{
-    const uint32_t sb = (uint32_t)(256 * (a >> 2)), s4 = (uint32_t)(a & 3);
-    if constexpr (F == Q4_K) return 2u * (sb + 128u * (s4 >> 1) + 32u * (s4 & 1));
-    if constexpr (F == Q8_0) return 2u * (sb + 64u * s4);
-    return 2u * (sb + 128u * (s4 >> 1) + 8u * (s4 & 1));
-}
-template <int F>
-__device__ __forceinline__ uint32_t act_voff_wr(int j)
-{
-    const uint32_t s = (uint32_t)(j >> 2), g = (uint32_t)(j & 3);
-    if constexpr (F == Q4_K) return 2u * (64u * (g >> 1) + 16u * (g & 1) + 8u * s);
-    if constexpr (F == Q8_0) return 2u * (32u * (g >> 1) + 16u * (g & 1) + 8u * s);
-    return 2u * (64u * s + 16u * g);
-}
-
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, uint8_t *lds_dst, uint32_t voff, uint32_t soff)
 {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void *)lds_dst, 16, voff, soff, 0, 0);
@@ -417,13 +282,13 @@ constexpr uint32_t DUMMY = 0u;
 // 64 = weight DMAs with the addresses of a stage-contiguous (tiled) layout, 128 = a quarter of
 // the activation fragment reads.
 // AF_I8 / AF_F8: X = codes [N][K], XD = block-major scales [K/32][ldd]; AF_F16: X = fp16 x~.
-template <int F, int NB, int RG, int ABL = 0, int AM = AF_F16, int NL = 0, int WR = 0, int LS = 0>
+template <int F, int NB, int RG, int ABL = 0, int AM = AF_F16, int NL = 0>
 __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *__restrict__ A, const void *__restrict__ X,
                                                    const float *__restrict__ XD, uint16_t *__restrict__ C,
                                                    float *__restrict__ P, int64_t M, int64_t N, int64_t K,
                                                    int64_t ldc, int64_t ldd, int wstages_per_split, int pf16)
 {
-    using G = Cfg<F, NB, RG, AM, NL, WR, LS>;
+    using G = Cfg<F, NB, RG, AM, NL>;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[G::LDS_BYTES];
 #ifdef GQ_GEMM_STAMPS
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
@@ -435,8 +300,6 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
     // DMA issuer index: loader waves NWAVE.. (NL > 0), else every wave
     const bool loader = NL > 0 && wave >= NWAVE;
     const int iw = NL > 0 ? wave - NWAVE : wave;
-    const bool wloader = LS > 0 && loader && iw < LS; // split loaders: this wave issues the weights
-    const int iww = iw, iwa = LS > 0 ? iw - LS : iw;  // issuer index within each stream
     const int g = lane >> 4, l16 = lane & 15;
     const int64_t m0 = (int64_t)blockIdx.x * G::BM;
     const int64_t n0 = (int64_t)blockIdx.y * G::BN;
@@ -459,11 +322,11 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
         (void *)XD, 0, G::CODES ? (int)(uint32_t)(((K / 32 - 1) * ldd + N) * 4) : 0, 0x00020000);
 
     // weight DMA: instruction k = wave + 8i moves pieces p = 64k + lane: row p / NPW, piece p % NPW
-    uint32_t wv[G::NW > 0 ? G::NW : 1];
-    int wpc[G::NW > 0 ? G::NW : 1];
+    uint32_t wv[G::NW];
+    int wpc[G::NW];
 #pragma unroll
     for (int i = 0; i < G::NW; ++i) {
-        const int p = 64 * (iww + G::WISS * i) + lane, r = p / G::NPW;
+        const int p = 64 * (iw + G::ISSUERS * i) + lane, r = p / G::NPW;
         wpc[i] = p - r * G::NPW;
         const int64_t row = m0 + r < M ? m0 + r : M - 1;
         wv[i] = r < G::BM ? (uint32_t)(row * row_bytes) : DUMMY;
@@ -476,7 +339,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
     uint32_t av[G::NA];
 #pragma unroll
     for (int i = 0; i < G::NA; ++i) {
-        const int k = iwa + G::AISS * i, p = 64 * k + lane;
+        const int k = iw + G::ISSUERS * i, p = 64 * k + lane;
         if constexpr (G::CODES) {
             if (k < G::CI) {
                 const int r = p >> 2, q = p & 3, qs = q ^ i8_swz(r);
@@ -494,18 +357,17 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
             if constexpr ((ABL & 32) != 0) // diagnostic: the access pattern of a sub-stage-blocked layout
                 av[i] = r < G::BN ? (uint32_t)(tok * 128) + 16u * (q ^ act_swz(r)) : DUMMY;
             else
-                av[i] = r < G::BN ? (uint32_t)(tok * K * 2) + (WR ? act_voff_wr<F>(q ^ act_swz(r)) : act_voff<F>(q ^ act_swz(r)))
-                                  : DUMMY;
+                av[i] = r < G::BN ? (uint32_t)(tok * K * 2) + act_voff<F>(q ^ act_swz(r)) : DUMMY;
         }
     }
     const int myrow = 16 * RG * wave + l16; // the row this lane multiplies (row group 0)
 
     auto issue_w = [&](int64_t w) {
-        if constexpr ((ABL & 2) != 0 || WR != 0) return;
-        uint8_t *dst = lds + (int)(w % (G::NWS > 0 ? G::NWS : 1)) * G::W_SLOT;
+        if constexpr (ABL & 2) return;
+        uint8_t *dst = lds + (int)(w % G::NWS) * G::W_SLOT;
 #pragma unroll
         for (int i = 0; i < G::NW; ++i) {
-            const int k = iww + G::WISS * i;
+            const int k = iw + G::ISSUERS * i;
             uint32_t vo, so;
             if constexpr ((ABL & 64) != 0) { // diagnostic: the stage as one contiguous run (a tiled layout)
                 vo = (uint32_t)(m0 * row_bytes) + 16u * (uint32_t)(64 * k + lane);
@@ -525,7 +387,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
         uint8_t *dst = lds + G::A_BASE + (int)(a % G::NAS) * G::A_SLOT;
 #pragma unroll
         for (int i = 0; i < G::NA; ++i) {
-            const int k = iwa + G::AISS * i;
+            const int k = iw + G::ISSUERS * i;
             uint8_t *d = k < G::A_REAL ? dst + 1024 * k : lds + G::SCRATCH;
             if constexpr (G::CODES) {
                 const uint32_t e0 = act_soff<F>(a) / 2; // first element of the sub-stage
@@ -534,7 +396,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
             } else if constexpr ((ABL & 32) != 0) {
                 dma16(ars, d, av[i], (uint32_t)(a * N * 128));
             } else {
-                dma16(ars, d, av[i], WR ? act_soff_wr<F>(a) : act_soff<F>(a));
+                dma16(ars, d, av[i], act_soff<F>(a));
             }
         }
     };
@@ -563,81 +425,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
 #ifdef GQ_GEMM_STAMPS
     const unsigned long long t_setup = __builtin_amdgcn_s_memtime() - t_start;
 #endif
-    if constexpr (WR) {
-        if (w0 >= w1) {
-        } else if (loader) { // activation sub-stages only: A(a) landed = all but the NAS-2 after it
-            const int64_t a0 = 4 * w0, a1 = 4 * w1;
-#pragma unroll
-            for (int i = 0; i < G::NAS - 1; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
-            for (int64_t a = a0; a < a1; ++a) {
-                asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((G::NAS - 2) * G::NA) : "memory");
-                issue_a(a + G::NAS - 1 < a1 ? a + G::NAS - 1 : a1 - 1);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            return;
-        } else {
-            // this wave's 16 rows; the next stage's bytes are loaded while this one multiplies
-            const int64_t row = m0 + 16 * wave + l16 < M ? m0 + 16 * wave + l16 : M - 1;
-            const uint8_t *rowp = A + row * row_bytes;
-            WRegs<F> cur, nxt;
-            load_wregs<F>(cur, rowp, w0, g);
-            load_wregs<F>(nxt, rowp, w0 + 1 < w1 ? w0 + 1 : w1 - 1, g);
-            for (int64_t w = w0; w < w1; ++w) {
-#pragma unroll
-                for (int s4 = 0; s4 < 4; ++s4) {
-                    const int64_t a = 4 * w + s4;
-                    asm volatile("s_barrier" ::: "memory"); // the loaders' wait for A(a)
-                    const uint8_t *xs = lds + G::A_BASE + (int)(a % G::NAS) * G::A_SLOT;
-                    f16x8 bfr[2][NB];
-#pragma unroll
-                    for (int s = 0; s < 2; ++s)
-#pragma unroll
-                        for (int t = 0; t < NB; ++t) {
-                            const int r = 16 * t + l16;
-                            bfr[s][t] = *(const f16x8 *)(xs + 128 * r + 16 * ((4 * s + g) ^ act_swz(r)));
-                        }
-                    f16x8 af[2];
-                    reg_frags<F>(cur, g, s4, af);
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int s = 0; s < 2; ++s)
-#pragma unroll
-                        for (int t = 0; t < NB; ++t)
-                            acc[0][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s], bfr[s][t], acc[0][t], 0, 0, 0);
-                }
-                cur = nxt;
-                load_wregs<F>(nxt, rowp, w + 2 < w1 ? w + 2 : w1 - 1, g);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-    } else if (LS > 0 && loader) { // split loaders: one stream per wave, one barrier per sub-stage
-        if (w0 < w1) {
-            const int64_t a0 = 4 * w0, a1 = 4 * w1;
-            if (wloader) {
-                // W(w) landed = all but the NWS-2 stages issued after it; W(w+NWS-1) refills the
-                // slot of stage w-1, which every multiplying wave left at barrier 4w
-#pragma unroll
-                for (int i = 0; i < G::NWS - 1; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
-                for (int64_t a = a0; a < a1; ++a) {
-                    if ((a & 3) == 0) {
-                        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((G::NWS - 2) * G::NW) : "memory");
-                        issue_w((a >> 2) + G::NWS - 1 < w1 ? (a >> 2) + G::NWS - 1 : w1 - 1);
-                    } else {
-                        asm volatile("s_barrier" ::: "memory");
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < G::NAS - 1; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
-                for (int64_t a = a0; a < a1; ++a) {
-                    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((G::NAS - 2) * G::NA) : "memory");
-                    issue_a(a + G::NAS - 1 < a1 ? a + G::NAS - 1 : a1 - 1);
-                }
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        return;
-    } else if (loader) { // loader waves: the DMA schedule of the pipeline note, no multiply
+    if (loader) { // loader waves: the DMA schedule of the pipeline note, no multiply
         if (w0 < w1) {
             const int64_t a0 = 4 * w0, a1 = 4 * w1;
 #pragma unroll
@@ -653,7 +441,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
         }
         return;
     }
-    if (!WR && w0 < w1) {
+    if (w0 < w1) {
         const int64_t a0 = 4 * w0, a1 = 4 * w1;
 #pragma unroll
         for (int i = 0; i < G::NWS - 1 && NL == 0; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
@@ -682,7 +470,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
                 if (s4 == 0) issue_w(w + G::NWS - 1 < w1 ? w + G::NWS - 1 : w1 - 1);
             }
 
-            const uint8_t *wr = lds + (int)(w % (G::NWS > 0 ? G::NWS : 1)) * G::W_SLOT + G::RBW * myrow;
+            const uint8_t *wr = lds + (int)(w % G::NWS) * G::W_SLOT + G::RBW * myrow;
             const uint8_t *xs = lds + G::A_BASE + (int)(a % G::NAS) * G::A_SLOT;
             if constexpr (AM == AF_I8) {
                 // int8 form: per block b of the sub-stage one i8 MFMA per token tile, the int32
@@ -1002,11 +790,11 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restric
     }
 }
 
-template <int F, int NB, int RG, int AM = AF_F16, int NL = 0, int WR = 0, int LS = 0>
+template <int F, int NB, int RG, int AM = AF_F16, int NL = 0>
 hipError_t launch_cfg(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P, const GemmPlan &pl, int64_t M,
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
-    using G = Cfg<F, NB, RG, AM, NL, WR, LS>;
+    using G = Cfg<F, NB, RG, AM, NL>;
     dim3 grid((unsigned)((M + G::BM - 1) / G::BM), (unsigned)((N + G::BN - 1) / G::BN), (unsigned)pl.splits);
     float *PP = pl.splits > 1 ? P : nullptr;
     const int cps = pl.chunks_per_split;
@@ -1014,15 +802,15 @@ hipError_t launch_cfg(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P,
 #ifdef GQ_ABLATION
     const int abl = getenv("GQ_ABLATE") ? atoi(getenv("GQ_ABLATE")) : 0;
 #define GQ_ABL_CASE(v) \
-    case v: gemm_kernel<F, NB, RG, v, AM, NL, WR, LS><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps, pl.pf16); break;
+    case v: gemm_kernel<F, NB, RG, v, AM, NL><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps, pl.pf16); break;
     switch (abl) {
     GQ_ABL_CASE(1) GQ_ABL_CASE(6) GQ_ABL_CASE(8) GQ_ABL_CASE(15) GQ_ABL_CASE(16) GQ_ABL_CASE(31) GQ_ABL_CASE(32)
     GQ_ABL_CASE(33) GQ_ABL_CASE(2) GQ_ABL_CASE(4) GQ_ABL_CASE(64) GQ_ABL_CASE(68) GQ_ABL_CASE(96) GQ_ABL_CASE(128) GQ_ABL_CASE(134)
-    default: gemm_kernel<F, NB, RG, 0, AM, NL, WR, LS><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps, pl.pf16); break;
+    default: gemm_kernel<F, NB, RG, 0, AM, NL><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps, pl.pf16); break;
     }
 #undef GQ_ABL_CASE
 #else
-    gemm_kernel<F, NB, RG, 0, AM, NL, WR, LS><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps, pl.pf16);
+    gemm_kernel<F, NB, RG, 0, AM, NL><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps, pl.pf16);
 #endif
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || pl.splits == 1) return e;
@@ -1058,18 +846,6 @@ hipError_t launch_fmt(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P,
         case 2: return launch_cfg<F, 2, 1, AF_F8>(A, x, C, P, pl, M, N, K, ldc, s);
         case 4: return launch_cfg<F, 4, 1, AF_F8>(A, x, C, P, pl, M, N, K, ldc, s);
         default: return launch_cfg<F, 8, 1, AF_F8>(A, x, C, P, pl, M, N, K, ldc, s);
-        }
-    if (pl.loaders == 4 && pl.lsplit == 2 && pl.rg == 1) switch (pl.nb) {
-        case 1: return launch_cfg<F, 1, 1, AF_F16, 4, 0, 2>(A, x, C, P, pl, M, N, K, ldc, s);
-        case 2: return launch_cfg<F, 2, 1, AF_F16, 4, 0, 2>(A, x, C, P, pl, M, N, K, ldc, s);
-        case 4: return launch_cfg<F, 4, 1, AF_F16, 4, 0, 2>(A, x, C, P, pl, M, N, K, ldc, s);
-        default: return launch_cfg<F, 8, 1, AF_F16, 4, 0, 2>(A, x, C, P, pl, M, N, K, ldc, s);
-        }
-    if (pl.loaders == 4 && pl.wreg && pl.rg == 1) switch (pl.nb) {
-        case 1: return launch_cfg<F, 1, 1, AF_F16, 4, 1>(A, x, C, P, pl, M, N, K, ldc, s);
-        case 2: return launch_cfg<F, 2, 1, AF_F16, 4, 1>(A, x, C, P, pl, M, N, K, ldc, s);
-        case 4: return launch_cfg<F, 4, 1, AF_F16, 4, 1>(A, x, C, P, pl, M, N, K, ldc, s);
-        default: return launch_cfg<F, 8, 1, AF_F16, 4, 1>(A, x, C, P, pl, M, N, K, ldc, s);
         }
     if (pl.loaders == 4) switch (pl.nb) {
         case 1: return launch_cfg<F, 1, 1, AF_F16, 4>(A, x, C, P, pl, M, N, K, ldc, s);
@@ -1108,12 +884,6 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, int act)
     // 20.6 -> 20.1 (profiles/r02/loader_tune.txt); GQ_GEMM_LOADERS=0 restores all-wave issue
     p.loaders = p.act == AF_F16 && p.rg == 1 ? 4 : 0;
     if (const char *env = getenv("GQ_GEMM_LOADERS")) p.loaders = p.act == AF_F16 && atoi(env) == 4 ? 4 : 0;
-    // split loaders with a deeper weight ring (GQ_GEMM_LSPLIT=2: 2 weight + 2 activation loaders)
-    p.lsplit = 0;
-    if (const char *env = getenv("GQ_GEMM_LSPLIT")) p.lsplit = p.loaders == 4 && p.rg == 1 ? atoi(env) : 0;
-    // weights loaded to registers by each wave (no weight DMA through LDS): GQ_GEMM_WREG=1
-    p.wreg = 0;
-    if (const char *env = getenv("GQ_GEMM_WREG")) p.wreg = p.loaders == 4 && p.rg == 1 && atoi(env) == 1;
     const int64_t nws = K / 256; // weight stages (super-blocks)
     if (nws == 0) return p;      // not a GEMM shape (gemm_supported() is false): nothing to plan
     const int64_t bm = 128 * p.rg;
