@@ -88,13 +88,23 @@ __device__ __forceinline__ h2 pair13(uint32_t c) { return as_h2(__builtin_amdgcn
 // Per format: RBW = LDS bytes per row per weight stage (pieces NPW = RBW / 16), SB = packed
 // bytes per stage.  Q6_K rows are only 2-byte aligned: its window starts at floor16 of the
 // stage's first byte and the reader adds that misalignment (delta, per row and stage).
+// SPW = activation sub-stages per weight stage (4: one super-block).  GQ_GEMM_Q8_FINE=1 builds
+// Q8_0 with one 64-element sub-stage per weight stage (68 B per row as 5 pieces from its
+// 4-byte aligned first byte, 5 slots), so the first sub-stage waits for a quarter of the
+// weight bytes: parity-green but no faster (Q8_0 4096^2 x16..x256 within 1%,
+// profiles/r02/q8_0_fine_stages_ab.txt) -- the first wait is not the weight bytes.
+#ifndef GQ_GEMM_Q8_FINE
+#define GQ_GEMM_Q8_FINE 0
+#endif
 template <int F> struct WStage;
-template <> struct WStage<Q4_K> { static constexpr int RBW = 144, SB = 144; };
+template <> struct WStage<Q4_K> { static constexpr int RBW = 144, SB = 144, SPW = 4; };
 // Q6_K rows are padded to 240 B (15 pieces, the last a repeat of the d piece): a 224-B stride
 // (56 dwords) put rows l and l+8 of a 16-lane fragment read on the same banks (2-way
 // conflicts, ~half of the LDS cycles measured); 60 dwords spread 16 rows over distinct banks.
-template <> struct WStage<Q6_K> { static constexpr int RBW = 240, SB = 210; };
-template <> struct WStage<Q8_0> { static constexpr int RBW = 272, SB = 272; };
+template <> struct WStage<Q6_K> { static constexpr int RBW = 240, SB = 210, SPW = 4; };
+template <> struct WStage<Q8_0> {
+    static constexpr int SPW = GQ_GEMM_Q8_FINE ? 1 : 4, RBW = GQ_GEMM_Q8_FINE ? 80 : 272, SB = SPW * 68;
+};
 
 // Activation sub-stage c (64 elements) = sub-stage s4 = c & 3 of super-block c >> 2: the K
 // elements whose weights the k-steps read (Q6_K: two 32-element runs, see frags below).
@@ -119,7 +129,7 @@ struct Cfg {
     // NL > 0: NL more waves that only issue the DMAs (loader waves); 0: every wave issues its share
     static constexpr int BN = 16 * NB, BM = 16 * NWAVE * RG;
     static constexpr int ISSUERS = NL > 0 ? NL : NWAVE, THREADS = 64 * (NWAVE + NL);
-    static constexpr int RBW = WStage<F>::RBW, NPW = RBW / 16;
+    static constexpr int RBW = WStage<F>::RBW, NPW = RBW / 16, SPW = WStage<F>::SPW;
     static constexpr int W_REAL = BM * NPW / 64;                              // DMA instructions per stage
     // code-form (AF_I8 / AF_F8) activation sub-stage: BN x 64 code bytes (CI instructions), then
     // one instruction for the tile's scales of the sub-stage's two blocks (2 x BN floats)
@@ -143,7 +153,10 @@ struct Cfg {
 #ifndef GQ_GEMM_NWS // weight-stage slots for 64- and 128-token tiles
 #define GQ_GEMM_NWS 2
 #endif
-    static constexpr int NWS = NB <= 2 ? GQ_GEMM_SMALL_NWS : GQ_GEMM_NWS;
+#ifndef GQ_GEMM_FINE_NWS // weight-stage slots with one-sub-stage weight stages
+#define GQ_GEMM_FINE_NWS 5
+#endif
+    static constexpr int NWS = SPW == 1 ? GQ_GEMM_FINE_NWS : (NB <= 2 ? GQ_GEMM_SMALL_NWS : GQ_GEMM_NWS);
     // padding DMAs (instruction counts not a multiple of the wave count) land in a scratch KiB
     static constexpr bool PAD = W_REAL % ISSUERS != 0 || A_REAL % ISSUERS != 0;
     static constexpr int NAS_FIT = (LDS_MAX - (PAD ? 1024 : 0) - NWS * W_SLOT) / A_SLOT;
@@ -151,7 +164,7 @@ struct Cfg {
 #define GQ_GEMM_NAS_CAP 4  // 19.6 us, 4 slots 18.8, 3 slots 19.4; Q6_K x128: 3 slots +15%)
 #endif
     static constexpr int NAS_CAP = NB <= 2 ? GQ_GEMM_SMALL_NAS_CAP : GQ_GEMM_NAS_CAP;
-    static constexpr int NAS_MAX = 4 * NWS - 4 < NAS_CAP ? 4 * NWS - 4 : NAS_CAP;
+    static constexpr int NAS_MAX = SPW * (NWS - 1) < NAS_CAP ? SPW * (NWS - 1) : NAS_CAP;
     static constexpr int NAS = NAS_FIT < NAS_MAX ? NAS_FIT : NAS_MAX;
     static constexpr int A_BASE = NWS * W_SLOT, SCRATCH = A_BASE + NAS * A_SLOT; // dummy DMAs land there
     static constexpr int LDS_BYTES = SCRATCH + (PAD ? 1024 : 0);
@@ -160,7 +173,7 @@ struct Cfg {
     static_assert(!CODES || BN <= 128, "code forms: <= 128 tokens per tile");
     static_assert(LDS_BYTES <= LDS_MAX, "LDS budget");
     static_assert(NAS >= 3, "activation ring depth");
-    static_assert((NAS - 2) * NA + 2 * NW <= 63, "vmcnt range");
+    static_assert((NAS - 2) * NA + ((NAS - 1 + SPW - 1) / SPW) * NW <= 63, "vmcnt range");
 };
 
 // ---------------------------------------------------------------------------------------
@@ -266,16 +279,17 @@ __device__ __forceinline__ int i8_swz(int r) { return (r >> 2) & 3; }
 constexpr uint32_t DUMMY = 0u;
 
 // ---------------------------------------------------------------------------------------
-// Pipeline (per wave; a = activation sub-stage, w = a >> 2 = weight stage, NAS activation
+// Pipeline (per wave; a = activation sub-stage, w = a / SPW = weight stage, NAS activation
 // slots, NWS weight slots):
 //   prologue  W(0) .. W(NWS-2) A(0) .. A(NAS-2)
-//   iteration a: wait until A(a) (and so W(a>>2)) landed -> barrier -> A(a+NAS-1) ->
-//                [a&3 == 0: W(w+NWS-1)] -> multiply sub-stage a from W slot w%NWS, A slot a%NAS.
+//   iteration a: wait until A(a) (and so W(a/SPW)) landed -> barrier -> A(a+NAS-1) ->
+//                [a%SPW == 0: W(w+NWS-1)] -> multiply sub-stage a from W slot w%NWS, A slot a%NAS.
 // vmcnt counts in issue order, so "A(a) landed" = all but the ops issued after it: the NAS-2
 // younger activation sub-stages and the W(.) issued in iterations a-NAS+1 .. a-1 with
-// index % 4 == 0 (after their A).  W(w) is issued in iteration 4(w-NWS+1), after
-// A(4(w-NWS+1)+NAS-1), which is older than A(4w) iff NAS <= 4*NWS-4.  Past the end the indices are clamped (re-loads of identical
-// bytes into the same slot) so every wave issues the same sequence.
+// index % SPW == 0 (after their A).  W(w) is issued in iteration SPW(w-NWS+1), after
+// A(SPW(w-NWS+1)+NAS-1), which is older than A(SPW w) iff NAS <= SPW(NWS-1).  Past the end the
+// indices are clamped (re-loads of identical bytes into the same slot) so every wave issues
+// the same sequence.
 // ABL: ablation bitmask for performance diagnosis (diagnostic build -DGQ_ABLATION only; 0 in
 // production): 1 = no MFMA, 2 = no weight DMA, 4 = no activation DMA, 8 = no dequantization,
 // 16 = no epilogue, 32 = activation DMAs with the addresses of a sub-stage-blocked layout,
@@ -303,9 +317,12 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
     const int g = lane >> 4, l16 = lane & 15;
     const int64_t m0 = (int64_t)blockIdx.x * G::BM;
     const int64_t n0 = (int64_t)blockIdx.y * G::BN;
-    const int64_t nw_total = K / 256;
-    const int64_t w0 = (int64_t)blockIdx.z * wstages_per_split;
-    const int64_t w1 = w0 + wstages_per_split < nw_total ? w0 + wstages_per_split : nw_total;
+    // the split's super-blocks [sb0, sb1) = sub-stages [a0, a1) = weight stages [w0, w1)
+    const int64_t nsb = K / 256;
+    const int64_t sb0 = (int64_t)blockIdx.z * wstages_per_split;
+    const int64_t sb1 = sb0 + wstages_per_split < nsb ? sb0 + wstages_per_split : nsb;
+    constexpr int SPW = G::SPW;
+    const int64_t w0 = 4 * sb0 / SPW, w1 = 4 * sb1 / SPW;
     const int64_t row_bytes = (K / Layout<F>::QK) * Layout<F>::BYTES;
 
     // buffer descriptors (byte offsets are 32-bit: tensors < 4 GiB, checked on the host).  The
@@ -375,6 +392,9 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
             } else if constexpr (F == Q6_K) { // super-block image: pieces +16i (i < 13) and +194 (d at 222)
                 vo = wv[i] + (uint32_t)WStage<F>::SB * (uint32_t)w + (wpc[i] < 13 ? 16u * wpc[i] : 194u); // piece 14 = 13 again
                 so = 0;
+            } else if constexpr (F == Q8_0 && SPW == 1) { // 5 pieces from the stage's first byte (4-byte aligned)
+                vo = wv[i] + 68u * (uint32_t)w + 16u * wpc[i];
+                so = 0;
             } else {
                 vo = wv[i] + 16u * wpc[i];
                 so = (uint32_t)(WStage<F>::SB * w);
@@ -402,19 +422,23 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
     };
     // vmcnt for "A(a) landed": (NAS-2) younger A's + the W's issued after A(a)
     // rel = a - a0: W issues in iterations [max(0, rel-NAS+1), rel-1] that are multiples of 4
+    // rel = a - a0: W issues in iterations [max(0, rel-NAS+1), rel-1] that are multiples of SPW
     auto wait_a = [&](int rel) {
         constexpr int na = ABL & 4 ? 0 : G::NA, nw = ABL & 2 ? 0 : G::NW; // (ablated streams issue nothing)
         constexpr int base = (G::NAS - 2) * na;
         const int lo = rel - G::NAS + 1 > 0 ? rel - G::NAS + 1 : 0, hi = rel - 1;
-        const int w_after = hi >= lo ? hi / 4 - (lo + 3) / 4 + 1 : 0;
+        const int w_after = hi >= lo ? hi / SPW - (lo + SPW - 1) / SPW + 1 : 0;
         if constexpr ((ABL & 6) == 6) asm volatile("s_barrier" ::: "memory");
-        else if constexpr (ABL & 4) { // weights only: W(w) must land by sub-stage 4w
-            if ((rel & 3) == 0) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(nw) : "memory");
+        else if constexpr (ABL & 4) { // weights only: W(w) must land by sub-stage SPW w
+            if (rel % SPW == 0) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(nw) : "memory");
             else asm volatile("s_barrier" ::: "memory");
-        } else if (w_after >= 2) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(base + 2 * nw) : "memory");
+        } else if (w_after >= 4) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(base + 4 * nw) : "memory");
+        else if (w_after == 3) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(base + 3 * nw) : "memory");
+        else if (w_after == 2) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(base + 2 * nw) : "memory");
         else if (w_after == 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(base + nw) : "memory");
         else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(base) : "memory");
     };
+    static_assert((G::NAS - 1 + SPW - 1) / SPW <= 4, "W issues after an A: at most 4");
 
     f32x4 acc[RG][NB];
 #pragma unroll
@@ -427,7 +451,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
 #endif
     if (loader) { // loader waves: the DMA schedule of the pipeline note, no multiply
         if (w0 < w1) {
-            const int64_t a0 = 4 * w0, a1 = 4 * w1;
+            const int64_t a0 = 4 * sb0, a1 = 4 * sb1;
 #pragma unroll
             for (int i = 0; i < G::NWS - 1; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
 #pragma unroll
@@ -435,14 +459,14 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
             for (int64_t a = a0; a < a1; ++a) {
                 wait_a((int)(a - a0)); // A(a) landed -> barrier: the compute waves take sub-stage a
                 issue_a(a + G::NAS - 1 < a1 ? a + G::NAS - 1 : a1 - 1);
-                if ((a & 3) == 0) issue_w((a >> 2) + G::NWS - 1 < w1 ? (a >> 2) + G::NWS - 1 : w1 - 1);
+                if (a % SPW == 0) issue_w(a / SPW + G::NWS - 1 < w1 ? a / SPW + G::NWS - 1 : w1 - 1);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         return;
     }
     if (w0 < w1) {
-        const int64_t a0 = 4 * w0, a1 = 4 * w1;
+        const int64_t a0 = 4 * sb0, a1 = 4 * sb1;
 #pragma unroll
         for (int i = 0; i < G::NWS - 1 && NL == 0; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
 #pragma unroll
@@ -451,7 +475,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
         t_issued = __builtin_amdgcn_s_memtime() - t_start;
 #endif
         for (int64_t a = a0; a < a1; ++a) {
-            const int s4 = (int)(a & 3);
+            const int s4 = (int)(a % SPW); // sub-stage within the weight stage
 #ifdef GQ_GEMM_STAMPS
             const unsigned long long tw = __builtin_amdgcn_s_memtime();
 #endif
@@ -464,7 +488,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
                 else t_wait += tn - tw;
             }
 #endif
-            const int64_t w = a >> 2;
+            const int64_t w = a / SPW;
             if constexpr (NL == 0) {
                 issue_a(a + G::NAS - 1 < a1 ? a + G::NAS - 1 : a1 - 1);
                 if (s4 == 0) issue_w(w + G::NWS - 1 < w1 ? w + G::NWS - 1 : w1 - 1);
@@ -564,7 +588,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
             g_gstamps[id][1] = t_wait;
             g_gstamps[id][2] = t_loop;
             g_gstamps[id][3] = __builtin_amdgcn_s_memtime() - t_start;
-            g_gstamps[id][4] = (unsigned long long)(w1 - w0) * 4;
+            g_gstamps[id][4] = (unsigned long long)(sb1 - sb0) * 4;
             g_gstamps[id][5] = 1 + t_setup;
             g_gstamps[id][6] = t_start;
             g_gstamps[id][7] = t_issued;
