@@ -535,6 +535,14 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p)
     p.nt = 4;
     for (int i = 0; i < 3; ++i)
         if (nts[i] >= N) { p.nt = nts[i]; break; }
+    // Q6_K at 3-4 tokens with K >= 8192: two 2-token groups (super-block-half lanes; the second
+    // group re-reads the weights, largely from the Infinity Cache) beat one 4-token group (unit
+    // lanes): 28672x8192 x4 79.5 -> 69.4 us, 1024x8192 13.3 -> 8.1; at K = 4096 the 4-token
+    // group wins (4096^2 11.1 vs 14.3, 14336x4096 27.4 vs 29.7) -- profiles/r02/decode_maxnt_ab.txt.
+    // By K, not by size: row shards of one matrix take the same path (bit-identical results).
+    int nt_cap = fmt == Q6_K && K >= 8192 ? 2 : 4;
+    if (const char *env = getenv("GQ_DECODE_MAXNT")) nt_cap = atoi(env); // tuning override
+    while (p.nt > 1 && p.nt > nt_cap) p.nt >>= 1;
     while ((size_t)RING + act_lds(fmt, p.nt, K) > (size_t)LDS_CAP) {
         if (p.nt == 1) return false;
         p.nt >>= 1;

@@ -196,3 +196,24 @@ def test_split_k_partials_huge_cancelling_sums(partial, monkeypatch):
     # the split partials reach ~1e8 (fp32 ulp 8): what is left is a few ulps of the reduce's
     # fp32 summation order (the halves cancel split by split only up to that order)
     assert np.abs(got).max() <= 256
+
+
+@pytest.mark.parametrize("N", (3, 4))
+def test_q6_k_decode_two_token_groups(N):
+    """Q6_K at 3-4 tokens with K >= 8192 runs as two 2-token groups (mmq_decode.hip pick()):
+    against the oracle, and row shards of the matrix give the same bits (the choice depends on
+    K only)."""
+    from kernels._lib import TYPES, mmq
+    dev = _dev()
+    M, K = 192, 8192
+    qA = random_blocks("q6_k", M, K, seed=40 + N)
+    B = random_activations(N, K, seed=41 + N)
+    A_t = torch.from_numpy(qA.view(np.int8)).to(dev)
+    B_t = torch.from_numpy(B).to(dev)
+    C = mmq(TYPES["q6_k"], A_t, B_t, M, N, K)
+    half = qA.size // 2
+    C2 = mmq(TYPES["q6_k"], A_t[half:], B_t, M // 2, N, K)
+    torch.cuda.synchronize()
+    ideal = O.mmq_from_fp16("q6_k", qA, B, M, N, K, O.IDEAL)
+    assert O.max_rel_err(C.cpu().numpy(), ideal) <= TIGHT_GEMV
+    assert torch.equal(C2.view(torch.int16), C[:, M // 2:].contiguous().view(torch.int16))
