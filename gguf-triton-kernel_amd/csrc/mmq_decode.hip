@@ -511,6 +511,7 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
 
 struct Pick {
     int nt, itc;
+    bool lds_split = false; // fewer tokens per workgroup than wanted: the activations do not fit LDS
     size_t lds;
     DecodeGeom geo;
     int grid;
@@ -546,6 +547,7 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p)
     while ((size_t)RING + act_lds(fmt, p.nt, K) > (size_t)LDS_CAP) {
         if (p.nt == 1) return false;
         p.nt >>= 1;
+        p.lds_split = true;
     }
     p.lds = (size_t)RING + act_lds(fmt, p.nt, K);
     const int64_t RB = row_bytes(fmt, K);
@@ -648,8 +650,12 @@ hipError_t launch_f(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *
 bool decode_fused_ok(int fmt, int64_t N, int64_t K)
 {
     Pick p;
-    // 32-bit buffer offsets: the packed tensor must stay below 2 GiB (the C ABI splits larger ones)
-    return N <= 8 && pick(fmt, 1, N, K, p);
+    // 32-bit buffer offsets: the packed tensor must stay below 2 GiB (the C ABI splits larger ones).
+    // When the tokens' activations do not fit LDS beside the ring (long K: every extra token
+    // group streams the weights again), the GEMV path (activations quantized once to global,
+    // weights streamed once) is taken instead: Q6_K 8192x28672 x4 140 -> 82 us, x2 74 -> 67,
+    // Q4_K 4096x14336 x4 26.7 -> 22.6 (profiles/r02/decode_vs_gemv_long_k.txt)
+    return N <= 8 && pick(fmt, 1, N, K, p) && !p.lds_split;
 }
 
 hipError_t launch_decode_fused(int fmt, const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, int64_t M,
