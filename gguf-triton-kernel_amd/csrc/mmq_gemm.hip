@@ -86,8 +86,9 @@ __device__ __forceinline__ h2 pair13(uint32_t c) { return as_h2(__builtin_amdgcn
 // the row's contiguous bytes (16-byte pieces from a 16-byte aligned window: full cache lines,
 // the shape HBM streams at its full rate).  Activation sub-stages are 64 elements.
 // Per format: RBW = LDS bytes per row per weight stage (pieces NPW = RBW / 16), SB = packed
-// bytes per stage.  Q6_K rows are only 2-byte aligned: its window starts at floor16 of the
-// stage's first byte and the reader adds that misalignment (delta, per row and stage).
+// bytes per stage.  Q6_K super-blocks are only 2-byte aligned: each is moved as 16-byte pieces
+// read from its own first byte (2-byte aligned DMA sources) into a 240-B image whose every
+// field is aligned (the d piece repeated at 208..223, d at 222).
 // SPW = activation sub-stages per weight stage (4: one super-block).  GQ_GEMM_Q8_FINE=1 builds
 // Q8_0 with one 64-element sub-stage per weight stage (68 B per row as 5 pieces from its
 // 4-byte aligned first byte, 5 slots), so the first sub-stage waits for a quarter of the
