@@ -584,8 +584,9 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p)
     // units and 1 token (K <= 28672: the 70B ffn_down rows) -- no spills (kernel-resource-usage)
     const int64_t itc = (cpr + (1 << g.lp2) - 1) >> g.lp2, units = itc * (upr / cpr);
     p.itc = ((p.nt <= 2 && units <= (fmt == Q6_K ? 2 : 4)) || (p.nt == 1 && units <= 8)) ? (int)itc : 0;
-    // four tokens, one unit per lane (Q4_K / Q8_0, K <= 4096): cached too (GQ_DECODE_NT4_CACHE=0: off)
-    if (p.nt == 4 && fmt != Q6_K && units == 1 && !(getenv("GQ_DECODE_NT4_CACHE") && getenv("GQ_DECODE_NT4_CACHE")[0] == '0'))
+    // four tokens, one unit per lane (K <= 4096): cached too (Q6_K 14336x4096 x4 27.7 -> 20.7 us,
+    // profiles/r02/decode_nt4_cache_ab.txt; GQ_DECODE_NT4_CACHE=0: off)
+    if (p.nt == 4 && units == 1 && !(getenv("GQ_DECODE_NT4_CACHE") && getenv("GQ_DECODE_NT4_CACHE")[0] == '0'))
         p.itc = 1;
     const int64_t waves = g.ngroups < W ? g.ngroups : W;
     p.grid = (int)((waves + DW - 1) / DW);
@@ -623,6 +624,7 @@ hipError_t launch_f(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *
         case 16: return GQ_LT(2, 0);
         case 17: return GQ_LT(2, 1);
         case 32: return GQ_LT(4, 0);
+        case 33: return GQ_LT(4, 1);
         default: return hipErrorInvalidValue;
         }
     } else {
