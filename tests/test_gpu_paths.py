@@ -217,3 +217,18 @@ def test_q6_k_decode_two_token_groups(N):
     ideal = O.mmq_from_fp16("q6_k", qA, B, M, N, K, O.IDEAL)
     assert O.max_rel_err(C.cpu().numpy(), ideal) <= TIGHT_GEMV
     assert torch.equal(C2.view(torch.int16), C[:, M // 2:].contiguous().view(torch.int16))
+
+
+@pytest.mark.parametrize("fmt,K,N", [("q6_k", 28672, 2), ("q6_k", 28672, 4), ("q4_k", 11008, 4), ("q8_0", 14336, 4)])
+def test_long_k_small_n_routes(fmt, K, N):
+    """2-4 tokens whose q8_1 image does not fit LDS beside the decode ring (long K) take the
+    GEMV path (mmq_decode.hip decode_fused_ok); against the oracle."""
+    from kernels._lib import TYPES, mmq
+    dev = _dev()
+    M = 96
+    qA = random_blocks(fmt, M, K, seed=K + N)
+    B = random_activations(N, K, seed=K - N)
+    C = mmq(TYPES[fmt], torch.from_numpy(qA.view(np.int8)).to(dev), torch.from_numpy(B).to(dev), M, N, K)
+    torch.cuda.synchronize()
+    ideal = O.mmq_from_fp16(fmt, qA, B, M, N, K, O.IDEAL)
+    assert O.max_rel_err(C.cpu().numpy(), ideal) <= TIGHT_GEMV
