@@ -39,6 +39,7 @@ struct GemmPlan {
     int act = AF_F16;          // activation form (AF_I8: Q8_0 only)
     int loaders = 0;           // 4: four dedicated DMA-issuing waves beside the 8 multiplying ones
     int pf16 = 0;              // split-K partials stored as fp16 (else fp32)
+    int aq = 0;                // activations quantized in-kernel from raw fp16 (GemmAct::xraw)
     size_t partial_bytes = 0;  // fp32 partial slabs needed when splits > 1
 };
 // Activations as the GEMM reads them: fp16 x~ (act_quant DEQ) or, for the code forms, codes +
@@ -48,7 +49,11 @@ struct GemmAct {
     const int8_t *xq = nullptr;
     const float *xd = nullptr;
     int64_t ldd = 0; // row length of the block-major scale array (all the call's tokens)
+    const uint16_t *xraw = nullptr; // aq: the fp16 activations themselves, rows ldx apart
+    int64_t ldx = 0;
 };
+// plan.aq is allowed (in-kernel q8_1 of a 16/32-token tile's split, GemmPlan::aq)
+bool gemm_aq_ok(const GemmPlan &p);
 // The MFMA GEMM needs K in whole 256-element stages (always true for Q4_K/Q6_K).
 bool gemm_supported(int fmt, int64_t K);
 // act: the activation form (AF_I8 is honoured for Q8_0 only).

@@ -294,6 +294,23 @@ int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int6
         if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (decode): %s", hipGetErrorString(e));
         return GQ_OK;
     }
+    if (!r.gemv && !r.blas && act == GQ_ACT_Q8_1 && r.form == gq::AF_F16 && gemm_rows_per_launch(t, M, K) >= M &&
+        gemm_toks_per_launch(N, K) >= N) {
+        // 16/32-token tiles whose split fits LDS: the GEMM quantizes the activations itself (no
+        // act_quant launch; bit-identical to the DEQ form it would read)
+        gq::GemmPlan plan = gq::plan_gemm(t, M, N, K, r.form);
+        if (gq::gemm_aq_ok(plan)) {
+            plan.aq = 1;
+            gq::GemmAct x;
+            x.xraw = (const uint16_t *)B;
+            x.ldx = ldb;
+            Carved c = carve(act, workspace, N, K);
+            hipError_t e = gq::launch_gemm(t, (const uint8_t *)A, x, (uint16_t *)C, c.partials, plan, M, N, K, ldc,
+                                           (hipStream_t)stream);
+            if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (mmq): %s", hipGetErrorString(e));
+            return GQ_OK;
+        }
+    }
     rc = prepare(act, B, N, K, ldb, workspace, workspace_bytes, (hipStream_t)stream, r.form == gq::AF_I8 ? 2 : 1);
     if (rc != GQ_OK) return rc;
     return compute(t, act, A, workspace, workspace_bytes, C, M, N, K, ldc, (hipStream_t)stream);

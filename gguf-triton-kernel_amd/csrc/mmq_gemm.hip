@@ -49,6 +49,7 @@
 
 #include "gguf_blocks.hpp"
 #include "gguf_internal.hpp"
+#include "gguf_q8_1.hpp"
 
 namespace gq {
 
@@ -124,7 +125,16 @@ __device__ __forceinline__ uint32_t act_voff(int p) // byte offset of piece p (8
 
 constexpr int NWAVE = 8; // 512 threads: two waves per SIMD
 
-template <int F, int NB, int RG = 1, int AM = AF_F16, int NL = 0>
+// AQ (in-kernel activation quantization, 16- and 32-token tiles): the loader waves q8_1-quantize
+// the tile's fp16 activations for the whole split into LDS (every sub-stage resident, AQ_SUB at
+// most), so the call needs no act_quant launch and no activation DMA.
+#ifndef GQ_GEMM_AQ_SUB
+#define GQ_GEMM_AQ_SUB 24
+#endif
+template <int NB> constexpr int aq_sub() { return NB == 1 ? GQ_GEMM_AQ_SUB : GQ_GEMM_AQ_SUB / 2; }
+int aq_sub_of(int nb) { return nb == 1 ? GQ_GEMM_AQ_SUB : (nb == 2 ? GQ_GEMM_AQ_SUB / 2 : 0); }
+
+template <int F, int NB, int RG = 1, int AM = AF_F16, int NL = 0, int AQ = 0>
 struct Cfg {
     // 128*RG weight rows x 16*NB tokens; wave w owns rows 16*(RG*w + rg) + [0, 16), rg < RG.
     // NL > 0: NL more waves that only issue the DMAs (loader waves); 0: every wave issues its share
@@ -166,7 +176,7 @@ struct Cfg {
 #endif
     static constexpr int NAS_CAP = NB <= 2 ? GQ_GEMM_SMALL_NAS_CAP : GQ_GEMM_NAS_CAP;
     static constexpr int NAS_MAX = SPW * (NWS - 1) < NAS_CAP ? SPW * (NWS - 1) : NAS_CAP;
-    static constexpr int NAS = NAS_FIT < NAS_MAX ? NAS_FIT : NAS_MAX;
+    static constexpr int NAS = AQ ? aq_sub<NB>() : (NAS_FIT < NAS_MAX ? NAS_FIT : NAS_MAX);
     static constexpr int A_BASE = NWS * W_SLOT, SCRATCH = A_BASE + NAS * A_SLOT; // dummy DMAs land there
     static constexpr int LDS_BYTES = SCRATCH + (PAD ? 1024 : 0);
     static_assert((BM * NPW % 64 == 0 && (BN * 8) % 64 == 0) || BN * 8 < 64, "whole DMA instructions");
@@ -174,7 +184,8 @@ struct Cfg {
     static_assert(!CODES || BN <= 128, "code forms: <= 128 tokens per tile");
     static_assert(LDS_BYTES <= LDS_MAX, "LDS budget");
     static_assert(NAS >= 3, "activation ring depth");
-    static_assert((NAS - 2) * NA + ((NAS - 1 + SPW - 1) / SPW) * NW <= 63, "vmcnt range");
+    static_assert(!AQ || (NB <= 2 && NL > 0 && RG == 1 && AM == AF_F16), "in-kernel quantization: small tiles, loaders");
+    static_assert(AQ || (NAS - 2) * NA + ((NAS - 1 + SPW - 1) / SPW) * NW <= 63, "vmcnt range");
 };
 
 // ---------------------------------------------------------------------------------------
@@ -297,13 +308,13 @@ constexpr uint32_t DUMMY = 0u;
 // 64 = weight DMAs with the addresses of a stage-contiguous (tiled) layout, 128 = a quarter of
 // the activation fragment reads.
 // AF_I8 / AF_F8: X = codes [N][K], XD = block-major scales [K/32][ldd]; AF_F16: X = fp16 x~.
-template <int F, int NB, int RG, int ABL = 0, int AM = AF_F16, int NL = 0>
+template <int F, int NB, int RG, int ABL = 0, int AM = AF_F16, int NL = 0, int AQ = 0>
 __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *__restrict__ A, const void *__restrict__ X,
                                                    const float *__restrict__ XD, uint16_t *__restrict__ C,
                                                    float *__restrict__ P, int64_t M, int64_t N, int64_t K,
                                                    int64_t ldc, int64_t ldd, int wstages_per_split, int pf16)
 {
-    using G = Cfg<F, NB, RG, AM, NL>;
+    using G = Cfg<F, NB, RG, AM, NL, AQ>;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[G::LDS_BYTES];
 #ifdef GQ_GEMM_STAMPS
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
@@ -333,7 +344,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
     const __amdgpu_buffer_rsrc_t wrs =
         __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, (int)(uint32_t)((M * row_bytes + 15) & ~(int64_t)15), 0x00020000);
     const __amdgpu_buffer_rsrc_t ars =
-        __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, (int)(uint32_t)(N * K * (G::CODES ? 1 : 2)), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, (int)(uint32_t)(AQ ? ((N - 1) * ldd + K) * 2 : N * K * (G::CODES ? 1 : 2)), 0x00020000);
     // code forms: scales [K/32][ldd] from XD (this launch's first token), the last block's run
     // holding this launch's N tokens
     const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
@@ -439,7 +450,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
         else if (w_after == 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(base + nw) : "memory");
         else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(base) : "memory");
     };
-    static_assert((G::NAS - 1 + SPW - 1) / SPW <= 4, "W issues after an A: at most 4");
+    static_assert(AQ || (G::NAS - 1 + SPW - 1) / SPW <= 4, "W issues after an A: at most 4");
 
     f32x4 acc[RG][NB];
 #pragma unroll
@@ -450,7 +461,74 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
 #ifdef GQ_GEMM_STAMPS
     const unsigned long long t_setup = __builtin_amdgcn_s_memtime() - t_start;
 #endif
-    if (loader) { // loader waves: the DMA schedule of the pipeline note, no multiply
+    if (AQ && loader) { // weights by DMA; the split's activations quantized straight into LDS
+        if (w0 < w1) {
+            const int64_t a0 = 4 * sb0, a1 = 4 * sb1;
+#pragma unroll
+            for (int i = 0; i < G::NWS - 1; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
+            // 4 lanes per 32-element block (8 fp16 each), 64 blocks per pass over the 4 loader
+            // waves; loads unconditional (clamped) and all issued before the first quantization
+            constexpr int PMAX = (G::NAS * G::BN * 2 + 63) / 64;
+            const int nbk = 2 * (int)(a1 - a0), nblk = G::BN * nbk;
+            const __amdgpu_buffer_rsrc_t xr = ars; // raw fp16 activations [N][ldd]
+            u32x4 xv[PMAX];
+#pragma unroll
+            for (int q = 0; q < PMAX; ++q) {
+                int b = 64 * q + 16 * iw + (lane >> 2);
+                if (b >= nblk) b = 0;
+                const int r = b / nbk, kb = b - r * nbk;
+                const int64_t tok = n0 + r < N ? n0 + r : N - 1;
+                const uint32_t k = (uint32_t)(64 * a0 + 32 * kb + 8 * (lane & 3));
+                xv[q] = __builtin_amdgcn_raw_buffer_load_b128(xr, (uint32_t)(tok * ldd) * 2u + 2u * k, 0, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < PMAX; ++q) {
+                const Q81Quad qq = q8_1_quad(xv[q]); // every lane: DPP quad groups
+                const int b = 64 * q + 16 * iw + (lane >> 2);
+                if (b < nblk) {
+                    const int r = b / nbk, kb = b - r * nbk;
+                    const int k = 32 * kb + 8 * (lane & 3); // element offset from 64 * a0
+                    // x~ = fp16(d*q), 4-groups stored (0,2,1,3) as act_quant's DEQ form
+                    uint32_t o[4];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        float v4[4];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) v4[i] = qq.d * (float)(int8_t)((qq.codes[h] >> (8 * i)) & 0xff);
+                        o[2 * h] = (uint32_t)f2h_bits(v4[0]) | ((uint32_t)f2h_bits(v4[2]) << 16);
+                        o[2 * h + 1] = (uint32_t)f2h_bits(v4[1]) | ((uint32_t)f2h_bits(v4[3]) << 16);
+                    }
+                    // where the GEMM's fragment reads expect these 8 elements: sub-stage a (its
+                    // region a - a0), piece j of the 8 (Q6_K: the permuted run order of act_soff)
+                    int ar, j;
+                    if constexpr (F == Q6_K) {
+                        const int sbk = k >> 8, wsb = k & 255, h = wsb >> 7, n = (wsb >> 6) & 1, v = (wsb >> 5) & 1;
+                        ar = 4 * sbk + 2 * h + v;
+                        j = 4 * n + ((wsb >> 3) & 3);
+                    } else {
+                        ar = k >> 6;
+                        j = (k & 63) >> 3;
+                    }
+                    *(u32x4 *)(lds + G::A_BASE + ar * G::A_SLOT + 128 * r + 16 * (j ^ act_swz(r))) =
+                        (u32x4){o[0], o[1], o[2], o[3]};
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < PMAX; ++q) asm volatile("" ::"v"(xv[q].x), "v"(xv[q].y), "v"(xv[q].z), "v"(xv[q].w));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the image is complete before barrier a0
+            for (int64_t a = a0; a < a1; ++a) {
+                if ((a & 3) == 0) { // W(w) landed = all but the NWS-2 stages issued after it
+                    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((G::NWS - 2) * G::NW) : "memory");
+                    issue_w((a >> 2) + G::NWS - 1 < w1 ? (a >> 2) + G::NWS - 1 : w1 - 1);
+                } else {
+                    asm volatile("s_barrier" ::: "memory");
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        return;
+    }
+    if (!AQ && loader) { // loader waves: the DMA schedule of the pipeline note, no multiply
         if (w0 < w1) {
             const int64_t a0 = 4 * sb0, a1 = 4 * sb1;
 #pragma unroll
@@ -496,7 +574,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
             }
 
             const uint8_t *wr = lds + (int)(w % G::NWS) * G::W_SLOT + G::RBW * myrow;
-            const uint8_t *xs = lds + G::A_BASE + (int)(a % G::NAS) * G::A_SLOT;
+            const uint8_t *xs = lds + G::A_BASE + (int)(AQ ? a - a0 : a % G::NAS) * G::A_SLOT;
             if constexpr (AM == AF_I8) {
                 // int8 form: per block b of the sub-stage one i8 MFMA per token tile, the int32
                 // tile scaled by dA[row] * dB[token] into the fp32 accumulators
@@ -815,27 +893,28 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restric
     }
 }
 
-template <int F, int NB, int RG, int AM = AF_F16, int NL = 0>
+template <int F, int NB, int RG, int AM = AF_F16, int NL = 0, int AQ = 0>
 hipError_t launch_cfg(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P, const GemmPlan &pl, int64_t M,
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
-    using G = Cfg<F, NB, RG, AM, NL>;
+    using G = Cfg<F, NB, RG, AM, NL, AQ>;
     dim3 grid((unsigned)((M + G::BM - 1) / G::BM), (unsigned)((N + G::BN - 1) / G::BN), (unsigned)pl.splits);
     float *PP = pl.splits > 1 ? P : nullptr;
     const int cps = pl.chunks_per_split;
-    const void *X = G::CODES ? (const void *)x.xq : (const void *)x.xdeq;
+    const void *X = AQ ? (const void *)x.xraw : (G::CODES ? (const void *)x.xq : (const void *)x.xdeq);
+    const int64_t ldd = AQ ? x.ldx : x.ldd;
 #ifdef GQ_ABLATION
     const int abl = getenv("GQ_ABLATE") ? atoi(getenv("GQ_ABLATE")) : 0;
 #define GQ_ABL_CASE(v) \
-    case v: gemm_kernel<F, NB, RG, v, AM, NL><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps, pl.pf16); break;
+    case v: gemm_kernel<F, NB, RG, v, AM, NL, AQ><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, ldd, cps, pl.pf16); break;
     switch (abl) {
     GQ_ABL_CASE(1) GQ_ABL_CASE(6) GQ_ABL_CASE(8) GQ_ABL_CASE(15) GQ_ABL_CASE(16) GQ_ABL_CASE(31) GQ_ABL_CASE(32)
     GQ_ABL_CASE(33) GQ_ABL_CASE(2) GQ_ABL_CASE(4) GQ_ABL_CASE(64) GQ_ABL_CASE(68) GQ_ABL_CASE(96) GQ_ABL_CASE(128) GQ_ABL_CASE(134)
-    default: gemm_kernel<F, NB, RG, 0, AM, NL><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps, pl.pf16); break;
+    default: gemm_kernel<F, NB, RG, 0, AM, NL, AQ><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, ldd, cps, pl.pf16); break;
     }
 #undef GQ_ABL_CASE
 #else
-    gemm_kernel<F, NB, RG, 0, AM, NL><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, x.ldd, cps, pl.pf16);
+    gemm_kernel<F, NB, RG, 0, AM, NL, AQ><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, ldd, cps, pl.pf16);
 #endif
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || pl.splits == 1) return e;
@@ -872,6 +951,11 @@ hipError_t launch_fmt(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P,
         case 4: return launch_cfg<F, 4, 1, AF_F8>(A, x, C, P, pl, M, N, K, ldc, s);
         default: return launch_cfg<F, 8, 1, AF_F8>(A, x, C, P, pl, M, N, K, ldc, s);
         }
+    if (pl.aq && pl.loaders == 4 && pl.rg == 1 && pl.act == AF_F16) switch (pl.nb) {
+        case 1: return launch_cfg<F, 1, 1, AF_F16, 4, 1>(A, x, C, P, pl, M, N, K, ldc, s);
+        case 2: return launch_cfg<F, 2, 1, AF_F16, 4, 1>(A, x, C, P, pl, M, N, K, ldc, s);
+        default: return hipErrorInvalidValue;
+        }
     if (pl.loaders == 4) switch (pl.nb) {
         case 1: return launch_cfg<F, 1, 1, AF_F16, 4>(A, x, C, P, pl, M, N, K, ldc, s);
         case 2: return launch_cfg<F, 2, 1, AF_F16, 4>(A, x, C, P, pl, M, N, K, ldc, s);
@@ -891,6 +975,17 @@ int pick_nb(int64_t N) { return N > 64 ? 8 : (N > 32 ? 4 : (N > 16 ? 2 : 1)); }
 } // namespace
 
 bool gemm_supported(int /*fmt*/, int64_t K) { return K > 0 && K % 256 == 0; }
+
+bool gemm_aq_ok(const GemmPlan &p)
+{
+    if (const char *env = getenv("GQ_GEMM_AQ"))
+        if (env[0] == '0') return false;
+    // splits of at most two super-blocks: the quantization (a few passes of the loader waves)
+    // then hides under the first weight stage; longer splits measured neutral to 2% slower
+    // (Q4_K 4096x11008 x16), shorter ones 4-9% faster (profiles/r02/gemm_aq_ab.txt)
+    return p.act == AF_F16 && p.loaders == 4 && p.rg == 1 && p.nb <= 2 && p.chunks_per_split <= 2 &&
+           4 * p.chunks_per_split <= aq_sub_of(p.nb);
+}
 
 GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, int act)
 {

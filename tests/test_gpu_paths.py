@@ -232,3 +232,26 @@ def test_long_k_small_n_routes(fmt, K, N):
     torch.cuda.synchronize()
     ideal = O.mmq_from_fp16(fmt, qA, B, M, N, K, O.IDEAL)
     assert O.max_rel_err(C.cpu().numpy(), ideal) <= TIGHT_GEMV
+
+
+@pytest.mark.parametrize("fmt", ("q8_0", "q4_k", "q6_k"))
+@pytest.mark.parametrize("M,N,K", [(512, 5, 1024), (300, 16, 2048), (1024, 17, 4096), (640, 32, 1536), (128, 9, 512)])
+def test_gemm_in_kernel_quantization_bit_identical(fmt, M, N, K, monkeypatch):
+    """16/32-token tiles quantize their activations inside the GEMM (no act_quant launch): the
+    result is the same bits as the act_quant (DEQ) + GEMM path, and matches the oracle."""
+    from kernels._lib import TYPES, mmq
+    dev = _dev()
+    qA = random_blocks(fmt, M, K, seed=M + N)
+    B = random_activations(N, K, seed=K + 2 * N)
+    A_t = torch.from_numpy(qA.view(np.int8)).to(dev)
+    # a strided activation view (ldb > K) exercises the row stride of the in-kernel loads
+    Bw = torch.zeros(N, K + 64, dtype=torch.float16, device=dev)
+    Bw[:, :K] = torch.from_numpy(B).to(dev)
+    B_t = Bw[:, :K]
+    fused = mmq(TYPES[fmt], A_t, B_t, M, N, K)
+    monkeypatch.setenv("GQ_GEMM_AQ", "0")
+    staged = mmq(TYPES[fmt], A_t, B_t, M, N, K)
+    torch.cuda.synchronize()
+    assert torch.equal(fused.view(torch.int16), staged.view(torch.int16))
+    ideal = O.mmq_from_fp16(fmt, qA, B, M, N, K, O.IDEAL)
+    assert O.max_rel_err(fused.cpu().numpy(), ideal) <= TIGHT_GEMM
