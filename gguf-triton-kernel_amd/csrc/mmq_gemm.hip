@@ -131,8 +131,8 @@ constexpr int NWAVE = 8; // 512 threads: two waves per SIMD
 #ifndef GQ_GEMM_AQ_SUB
 #define GQ_GEMM_AQ_SUB 24
 #endif
-template <int NB> constexpr int aq_sub() { return NB == 1 ? GQ_GEMM_AQ_SUB : GQ_GEMM_AQ_SUB / 2; }
-int aq_sub_of(int nb) { return nb == 1 ? GQ_GEMM_AQ_SUB : (nb == 2 ? GQ_GEMM_AQ_SUB / 2 : 0); }
+template <int NB> constexpr int aq_sub() { return NB == 1 ? GQ_GEMM_AQ_SUB : (NB == 2 ? GQ_GEMM_AQ_SUB / 2 : 8); }
+int aq_sub_of(int nb) { return nb == 1 ? GQ_GEMM_AQ_SUB : (nb == 2 ? GQ_GEMM_AQ_SUB / 2 : (nb == 4 ? 8 : 0)); }
 
 template <int F, int NB, int RG = 1, int AM = AF_F16, int NL = 0, int AQ = 0>
 struct Cfg {
@@ -184,7 +184,7 @@ struct Cfg {
     static_assert(!CODES || BN <= 128, "code forms: <= 128 tokens per tile");
     static_assert(LDS_BYTES <= LDS_MAX, "LDS budget");
     static_assert(NAS >= 3, "activation ring depth");
-    static_assert(!AQ || (NB <= 2 && NL > 0 && RG == 1 && AM == AF_F16), "in-kernel quantization: small tiles, loaders");
+    static_assert(!AQ || (NB <= 4 && NL > 0 && RG == 1 && AM == AF_F16), "in-kernel quantization: small tiles, loaders");
     static_assert(AQ || (NAS - 2) * NA + ((NAS - 1 + SPW - 1) / SPW) * NW <= 63, "vmcnt range");
 };
 
@@ -954,6 +954,7 @@ hipError_t launch_fmt(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P,
     if (pl.aq && pl.loaders == 4 && pl.rg == 1 && pl.act == AF_F16) switch (pl.nb) {
         case 1: return launch_cfg<F, 1, 1, AF_F16, 4, 1>(A, x, C, P, pl, M, N, K, ldc, s);
         case 2: return launch_cfg<F, 2, 1, AF_F16, 4, 1>(A, x, C, P, pl, M, N, K, ldc, s);
+        case 4: return launch_cfg<F, 4, 1, AF_F16, 4, 1>(A, x, C, P, pl, M, N, K, ldc, s);
         default: return hipErrorInvalidValue;
         }
     if (pl.loaders == 4) switch (pl.nb) {
@@ -983,7 +984,10 @@ bool gemm_aq_ok(const GemmPlan &p)
     // splits of at most two super-blocks: the quantization (a few passes of the loader waves)
     // then hides under the first weight stage; longer splits measured neutral to 2% slower
     // (Q4_K 4096x11008 x16), shorter ones 4-9% faster (profiles/r02/gemm_aq_ab.txt)
-    return p.act == AF_F16 && p.loaders == 4 && p.rg == 1 && p.nb <= 2 && p.chunks_per_split <= 2 &&
+    // 64-token tiles (GQ_GEMM_AQ_NB4=1) measured 11-14% slower: the loader waves' quantization
+    // (32 blocks per lane) no longer hides under the first weight stage
+    const int max_nb = getenv("GQ_GEMM_AQ_NB4") && getenv("GQ_GEMM_AQ_NB4")[0] == '1' ? 4 : 2;
+    return p.act == AF_F16 && p.loaders == 4 && p.rg == 1 && p.nb <= max_nb && p.chunks_per_split <= 2 &&
            4 * p.chunks_per_split <= aq_sub_of(p.nb);
 }
 

@@ -235,7 +235,7 @@ def test_long_k_small_n_routes(fmt, K, N):
 
 
 @pytest.mark.parametrize("fmt", ("q8_0", "q4_k", "q6_k"))
-@pytest.mark.parametrize("M,N,K", [(512, 5, 1024), (300, 16, 2048), (1024, 17, 4096), (640, 32, 1536), (128, 9, 512)])
+@pytest.mark.parametrize("M,N,K", [(512, 5, 1024), (300, 16, 2048), (1024, 17, 4096), (640, 32, 1536), (128, 9, 512), (384, 64, 1024), (256, 40, 2048)])
 def test_gemm_in_kernel_quantization_bit_identical(fmt, M, N, K, monkeypatch):
     """16/32-token tiles quantize their activations inside the GEMM (no act_quant launch): the
     result is the same bits as the act_quant (DEQ) + GEMM path, and matches the oracle."""
