@@ -73,7 +73,8 @@ hipError_t launch_one(const uint8_t *A, const int8_t *xq, const float *xd, const
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
     const int64_t groups = (M + 4 * R - 1) / (4 * R);
-    const int64_t cap = 2048;
+    int64_t cap = 2048;
+    if (const char *env = getenv("GQ_GEMV_CAP")) cap = atoll(env); // tuning
     dim3 grid((unsigned)(groups < cap ? groups : cap), (unsigned)((N + NT - 1) / NT)), block(256);
     gemv_kernel<F, NT, R><<<grid, block, 0, s>>>(A, xq, xd, xs, C, M, N, K, ldc);
     return hipGetLastError();
@@ -83,9 +84,19 @@ template <int F>
 hipError_t launch_fmt(const uint8_t *A, const int8_t *xq, const float *xd, const float *xs, uint16_t *C, int64_t M,
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
-    if (N == 1) return launch_one<F, 1, 4>(A, xq, xd, xs, C, M, N, K, ldc, s);
-    if (N == 2) return launch_one<F, 2, 4>(A, xq, xd, xs, C, M, N, K, ldc, s);
-    return launch_one<F, 4, 2>(A, xq, xd, xs, C, M, N, K, ldc, s);
+    // rows per wave: 4 (1-2 tokens) / 2 (3-4 tokens); Q6_K the other way round (8192x28672 x2
+    // 64.9 -> 58.3 us, x4 81.7 -> 72.9: profiles/r02/gemv_rows_tune.txt); GQ_GEMV_R overrides
+    int r = F == Q6_K ? (N <= 2 ? 2 : 4) : 0;
+    if (const char *env = getenv("GQ_GEMV_R")) r = atoi(env);
+    if (N == 1) return r == 8 ? launch_one<F, 1, 8>(A, xq, xd, xs, C, M, N, K, ldc, s)
+                              : r == 2 ? launch_one<F, 1, 2>(A, xq, xd, xs, C, M, N, K, ldc, s)
+                                       : launch_one<F, 1, 4>(A, xq, xd, xs, C, M, N, K, ldc, s);
+    if (N == 2) return r == 8 ? launch_one<F, 2, 8>(A, xq, xd, xs, C, M, N, K, ldc, s)
+                              : r == 2 ? launch_one<F, 2, 2>(A, xq, xd, xs, C, M, N, K, ldc, s)
+                                       : launch_one<F, 2, 4>(A, xq, xd, xs, C, M, N, K, ldc, s);
+    return r == 4 ? launch_one<F, 4, 4>(A, xq, xd, xs, C, M, N, K, ldc, s)
+                  : r == 1 ? launch_one<F, 4, 1>(A, xq, xd, xs, C, M, N, K, ldc, s)
+                           : launch_one<F, 4, 2>(A, xq, xd, xs, C, M, N, K, ldc, s);
 }
 
 } // namespace
