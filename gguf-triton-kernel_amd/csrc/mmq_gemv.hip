@@ -84,9 +84,10 @@ template <int F>
 hipError_t launch_fmt(const uint8_t *A, const int8_t *xq, const float *xd, const float *xs, uint16_t *C, int64_t M,
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
-    // rows per wave: 4 (1-2 tokens) / 2 (3-4 tokens); Q6_K the other way round (8192x28672 x2
-    // 64.9 -> 58.3 us, x4 81.7 -> 72.9: profiles/r02/gemv_rows_tune.txt); GQ_GEMV_R overrides
-    int r = F == Q6_K ? (N <= 2 ? 2 : 4) : 0;
+    // rows per wave (profiles/r02/gemv_rows_tune.txt): 1-2 tokens Q8_0 4, Q4_K / Q6_K 2
+    // (Q4_K 4096x28672 x2 30.3 -> 23.9 us, Q6_K 8192x28672 x2 64.9 -> 58.3); 3-4 tokens 2,
+    // Q6_K 4 (x4 81.7 -> 72.9); GQ_GEMV_R overrides
+    int r = N <= 2 ? (F == Q8_0 ? 4 : 2) : (F == Q6_K ? 4 : 2);
     if (const char *env = getenv("GQ_GEMV_R")) r = atoi(env);
     if (N == 1) return r == 8 ? launch_one<F, 1, 8>(A, xq, xd, xs, C, M, N, K, ldc, s)
                               : r == 2 ? launch_one<F, 1, 2>(A, xq, xd, xs, C, M, N, K, ldc, s)
