@@ -40,6 +40,8 @@ struct GemmPlan {
     int loaders = 0;           // 4: four dedicated DMA-issuing waves beside the 8 multiplying ones
     int pf16 = 0;              // split-K partials stored as fp16 (else fp32)
     int aq = 0;                // activations quantized in-kernel from raw fp16 (GemmAct::xraw)
+    int fused_reduce = 0;      // fp16 split-K partials summed by each row group's last-arriving wave
+                               // (no reduce launch); 0: gemm_reduce_f16_kernel
     size_t partial_bytes = 0;  // fp32 partial slabs needed when splits > 1
 };
 // Activations as the GEMM reads them: fp16 x~ (act_quant DEQ) or, for the code forms, codes +

@@ -255,3 +255,35 @@ def test_gemm_in_kernel_quantization_bit_identical(fmt, M, N, K, monkeypatch):
     assert torch.equal(fused.view(torch.int16), staged.view(torch.int16))
     ideal = O.mmq_from_fp16(fmt, qA, B, M, N, K, O.IDEAL)
     assert O.max_rel_err(fused.cpu().numpy(), ideal) <= TIGHT_GEMM
+
+
+@pytest.mark.parametrize("fmt", ("q8_0", "q4_k", "q6_k"))
+@pytest.mark.parametrize("M,N,K,splits", [(4096, 128, 4096, None), (300, 100, 2048, "3"), (1000, 77, 1280, "5"),
+                                          (8192, 128, 2048, "2"), (520, 17, 4096, "11"), (256, 5, 4096, "16"),
+                                          (384, 40, 3072, "12")])
+def test_fused_split_k_reduce_bit_identical(fmt, M, N, K, splits, monkeypatch):
+    """Split-K partials summed inside the GEMM by each row group's last-arriving wave
+    (GQ_GEMM_FUSED_REDUCE=1, mmq_gemm.hip GemmPlan::fused_reduce; measured slower, so opt-in)
+    give the same bits as the separate
+    gemm_reduce_f16_kernel launch, call after call (the arrival counters reset themselves),
+    and match the oracle.  Covers every tile width, 128- and 256-row tiles (Q4_K at 8192 rows),
+    split counts that are not multiples of 8, ragged M/N."""
+    from kernels._lib import TYPES, mmq
+    dev = _dev()
+    if splits:
+        monkeypatch.setenv("GQ_GEMM_SPLITS", splits)
+    qA = random_blocks(fmt, M, K, seed=M + 7 * N)
+    B = random_activations(N, K, seed=K + 5 * N)
+    A_t = torch.from_numpy(qA.view(np.int8)).to(dev)
+    B_t = torch.from_numpy(B).to(dev)
+    monkeypatch.setenv("GQ_GEMM_FUSED_REDUCE", "1")
+    fused = [mmq(TYPES[fmt], A_t, B_t, M, N, K) for _ in range(3)]
+    monkeypatch.setenv("GQ_GEMM_FUSED_REDUCE", "0")
+    staged = mmq(TYPES[fmt], A_t, B_t, M, N, K)
+    torch.cuda.synchronize()
+    for f in fused:
+        assert torch.equal(f.view(torch.int16), staged.view(torch.int16))
+    rows = np.arange(0, M, max(1, M // 256))
+    sub = qA.reshape(M, -1)[rows].reshape(-1)
+    ideal = O.mmq_from_fp16(fmt, sub, B, len(rows), N, K, O.IDEAL)
+    assert O.max_rel_err(fused[0].cpu().numpy()[:, rows], ideal) <= TIGHT_GEMM
