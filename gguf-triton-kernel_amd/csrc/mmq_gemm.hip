@@ -144,7 +144,11 @@ __device__ __forceinline__ uint32_t act_voff(int p) // byte offset of piece p (8
     return 16u * p;
 }
 
-constexpr int NWAVE = 8; // 512 threads: two waves per SIMD
+#ifndef GQ_GEMM_NWAVE // multiplying waves per workgroup (experiment: 4 = one per SIMD, two row groups each)
+#define GQ_GEMM_NWAVE 8
+#endif
+constexpr int NWAVE = GQ_GEMM_NWAVE; // 8: 512 threads, two waves per SIMD
+constexpr int R1 = 8 / NWAVE;        // row groups per wave of a 128-row tile
 
 // AQ (in-kernel activation quantization, 16- and 32-token tiles): the loader waves q8_1-quantize
 // the tile's fp16 activations for the whole split into LDS (every sub-stage resident, AQ_SUB at
@@ -205,7 +209,7 @@ struct Cfg {
     static_assert(!CODES || BN <= 128, "code forms: <= 128 tokens per tile");
     static_assert(LDS_BYTES <= LDS_MAX, "LDS budget");
     static_assert(NAS >= 3, "activation ring depth");
-    static_assert(!AQ || (NB <= 4 && NL > 0 && RG == 1 && AM == AF_F16), "in-kernel quantization: small tiles, loaders");
+    static_assert(!AQ || (NB <= 4 && NL > 0 && RG == R1 && AM == AF_F16), "in-kernel quantization: small tiles, loaders");
     static_assert(AQ || (NAS - 2) * NA + ((NAS - 1 + SPW - 1) / SPW) * NW <= 63, "vmcnt range");
 };
 
@@ -1065,9 +1069,9 @@ hipError_t launch_fmt(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P,
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
     if constexpr (F == Q4_K)
-        if (pl.rg == 2 && pl.nb == 8)
-            return pl.loaders == 4 ? launch_cfg<F, 8, 2, AF_F16, 4>(A, x, C, P, pl, M, N, K, ldc, s)
-                                   : launch_cfg<F, 8, 2>(A, x, C, P, pl, M, N, K, ldc, s);
+        if (pl.rg == 2 * R1 && pl.nb == 8)
+            return pl.loaders == 4 ? launch_cfg<F, 8, 2 * R1, AF_F16, 4>(A, x, C, P, pl, M, N, K, ldc, s)
+                                   : launch_cfg<F, 8, 2 * R1>(A, x, C, P, pl, M, N, K, ldc, s);
     if constexpr (F == Q8_0)
         if (pl.act == AF_I8) switch (pl.nb) {
             case 1: return launch_cfg<F, 1, 1, AF_I8>(A, x, C, P, pl, M, N, K, ldc, s);
@@ -1081,23 +1085,23 @@ hipError_t launch_fmt(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P,
         case 4: return launch_cfg<F, 4, 1, AF_F8>(A, x, C, P, pl, M, N, K, ldc, s);
         default: return launch_cfg<F, 8, 1, AF_F8>(A, x, C, P, pl, M, N, K, ldc, s);
         }
-    if (pl.aq && pl.loaders == 4 && pl.rg == 1 && pl.act == AF_F16) switch (pl.nb) {
-        case 1: return launch_cfg<F, 1, 1, AF_F16, 4, 1>(A, x, C, P, pl, M, N, K, ldc, s);
-        case 2: return launch_cfg<F, 2, 1, AF_F16, 4, 1>(A, x, C, P, pl, M, N, K, ldc, s);
-        case 4: return launch_cfg<F, 4, 1, AF_F16, 4, 1>(A, x, C, P, pl, M, N, K, ldc, s);
+    if (pl.aq && pl.loaders == 4 && pl.rg == R1 && pl.act == AF_F16) switch (pl.nb) {
+        case 1: return launch_cfg<F, 1, R1, AF_F16, 4, 1>(A, x, C, P, pl, M, N, K, ldc, s);
+        case 2: return launch_cfg<F, 2, R1, AF_F16, 4, 1>(A, x, C, P, pl, M, N, K, ldc, s);
+        case 4: return launch_cfg<F, 4, R1, AF_F16, 4, 1>(A, x, C, P, pl, M, N, K, ldc, s);
         default: return hipErrorInvalidValue;
         }
     if (pl.loaders == 4) switch (pl.nb) {
-        case 1: return launch_cfg<F, 1, 1, AF_F16, 4>(A, x, C, P, pl, M, N, K, ldc, s);
-        case 2: return launch_cfg<F, 2, 1, AF_F16, 4>(A, x, C, P, pl, M, N, K, ldc, s);
-        case 4: return launch_cfg<F, 4, 1, AF_F16, 4>(A, x, C, P, pl, M, N, K, ldc, s);
-        default: return launch_cfg<F, 8, 1, AF_F16, 4>(A, x, C, P, pl, M, N, K, ldc, s);
+        case 1: return launch_cfg<F, 1, R1, AF_F16, 4>(A, x, C, P, pl, M, N, K, ldc, s);
+        case 2: return launch_cfg<F, 2, R1, AF_F16, 4>(A, x, C, P, pl, M, N, K, ldc, s);
+        case 4: return launch_cfg<F, 4, R1, AF_F16, 4>(A, x, C, P, pl, M, N, K, ldc, s);
+        default: return launch_cfg<F, 8, R1, AF_F16, 4>(A, x, C, P, pl, M, N, K, ldc, s);
         }
     switch (pl.nb) {
-    case 1: return launch_cfg<F, 1, 1>(A, x, C, P, pl, M, N, K, ldc, s);
-    case 2: return launch_cfg<F, 2, 1>(A, x, C, P, pl, M, N, K, ldc, s);
-    case 4: return launch_cfg<F, 4, 1>(A, x, C, P, pl, M, N, K, ldc, s);
-    default: return launch_cfg<F, 8, 1>(A, x, C, P, pl, M, N, K, ldc, s);
+    case 1: return launch_cfg<F, 1, R1>(A, x, C, P, pl, M, N, K, ldc, s);
+    case 2: return launch_cfg<F, 2, R1>(A, x, C, P, pl, M, N, K, ldc, s);
+    case 4: return launch_cfg<F, 4, R1>(A, x, C, P, pl, M, N, K, ldc, s);
+    default: return launch_cfg<F, 8, R1>(A, x, C, P, pl, M, N, K, ldc, s);
     }
 }
 
@@ -1117,7 +1121,7 @@ bool gemm_aq_ok(const GemmPlan &p)
     // 64-token tiles (GQ_GEMM_AQ_NB4=1) measured 11-14% slower: the loader waves' quantization
     // (32 blocks per lane) no longer hides under the first weight stage
     const int max_nb = getenv("GQ_GEMM_AQ_NB4") && getenv("GQ_GEMM_AQ_NB4")[0] == '1' ? 4 : 2;
-    return p.act == AF_F16 && p.loaders == 4 && p.rg == 1 && p.nb <= max_nb && p.chunks_per_split <= 2 &&
+    return p.act == AF_F16 && p.loaders == 4 && p.rg == R1 && p.nb <= max_nb && p.chunks_per_split <= 2 &&
            4 * p.chunks_per_split <= aq_sub_of(p.nb);
 }
 
@@ -1130,17 +1134,17 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, int act)
     // two 16-row groups per wave (256-row tiles: half the activation traffic per weight) for
     // tall matrices at full token tiles
     // (Q4_K only: Q6_K's padded 240-B rows and Q8_0's 272-B rows do not fit 256 rows twice)
-    p.rg = (fmt == Q4_K && p.nb == 8 && M >= 8192) ? 2 : 1; // measured: 11008 rows 5% faster
-    if (const char *env = getenv("GQ_GEMM_RG")) p.rg = (fmt == Q4_K && p.nb == 8 && atoi(env) == 2) ? 2 : 1;
+    p.rg = (fmt == Q4_K && p.nb == 8 && M >= 8192) ? 2 * R1 : R1; // measured: 11008 rows 5% faster
+    if (const char *env = getenv("GQ_GEMM_RG")) p.rg = (fmt == Q4_K && p.nb == 8 && atoi(env) == 2) ? 2 * R1 : R1;
     if (p.act != AF_F16) p.rg = 1; // the code forms run 128-row tiles
     // four loader waves (DMA issue off the multiplying waves' path) for the 128-row fp16 form:
     // Q6_K 28672x8192x128 116.5 -> 103.7 us, Q4_K 4096^2x128 17.4 -> 16.7, Q8_0 4096^2x128
     // 20.6 -> 20.1 (profiles/r02/loader_tune.txt); GQ_GEMM_LOADERS=0 restores all-wave issue
-    p.loaders = p.act == AF_F16 && p.rg == 1 ? 4 : 0;
+    p.loaders = p.act == AF_F16 && p.rg == R1 ? 4 : 0;
     if (const char *env = getenv("GQ_GEMM_LOADERS")) p.loaders = p.act == AF_F16 && atoi(env) == 4 ? 4 : 0;
     const int64_t nws = K / 256; // weight stages (super-blocks)
     if (nws == 0) return p;      // not a GEMM shape (gemm_supported() is false): nothing to plan
-    const int64_t bm = 128 * p.rg;
+    const int64_t bm = 16 * NWAVE * p.rg;
     const int64_t tiles = ((M + bm - 1) / bm) * ((N + 16 * p.nb - 1) / (16 * p.nb));
     // one workgroup per CU (LDS-bound): the largest split that keeps tiles * S <= 256 CUs, so no
     // second wave of workgroups (258 workgroups ran 25% slower than 172 at 11008 x 4096 x 128)
