@@ -2,9 +2,13 @@
 // path selection (decode GEMV vs MFMA GEMM) and launches.  Stateless and re-entrant.
 #include <climits>
 #include <cstdio>
+#include <dlfcn.h>
+#include <mutex>
 #include <cstdarg>
 #include <cstdlib>
 #include <string>
+
+#include <rccl/rccl.h> // types only: the entry point is resolved at run time (shard_allgather)
 
 #include "../../include/gguf_mmq.h"
 #include "gguf_blocks.hpp"
@@ -139,6 +143,74 @@ size_t ws_bytes(int t, int act, int64_t M, int64_t N, int64_t K)
         b += align_up(p);
     }
     return b;
+}
+
+// ---- row sharding (gq_mmq_sharded) ----
+constexpr int64_t kShardAlign = 64; // dist/row_shard.py shard_rows(align=64)
+
+void shard_geom(int64_t M, int world, int rank, int64_t &row0, int64_t &rows, int64_t &R)
+{
+    R = (M + world - 1) / world;
+    R = (R + kShardAlign - 1) / kShardAlign * kShardAlign;
+    row0 = (int64_t)rank * R < M ? (int64_t)rank * R : M;
+    const int64_t end = row0 + R < M ? row0 + R : M;
+    rows = end - row0;
+}
+
+// C[n][m] = G[m / R][n][m % R]; VEC = 8: 8 columns (16 bytes) per thread (R % 8 == 0, so a
+// group never straddles two shards; used when C's rows and M allow 16-byte stores)
+template <int VEC>
+__global__ __launch_bounds__(256) void assemble_kernel(const uint16_t *__restrict__ G, uint16_t *__restrict__ C,
+                                                       int64_t N, int64_t R, int64_t M, int64_t ldc)
+{
+    const int64_t groups = (M + VEC - 1) / VEC;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N * groups;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t n = i / groups, m = (i - n * groups) * VEC;
+        const int64_t g = m / R, r = m - g * R;
+        const uint16_t *src = G + (g * N + n) * R + r;
+        uint16_t *dst = C + n * ldc + m;
+        if constexpr (VEC == 8) {
+            *(uint4 *)dst = *(const uint4 *)src;
+        } else {
+            *dst = *src;
+        }
+    }
+}
+
+hipError_t launch_assemble(const uint16_t *G, uint16_t *C, int64_t N, int64_t R, int64_t M, int64_t ldc,
+                           hipStream_t s)
+{
+    const bool vec = M % 8 == 0 && ldc % 8 == 0 && ((uintptr_t)C & 15) == 0 && ((uintptr_t)G & 15) == 0;
+    const int64_t items = N * (vec ? M / 8 : M);
+    const int64_t blocks = (items + 255) / 256 < 4096 ? (items + 255) / 256 : 4096;
+    if (vec) assemble_kernel<8><<<dim3((unsigned)blocks), dim3(256), 0, s>>>(G, C, N, R, M, ldc);
+    else assemble_kernel<1><<<dim3((unsigned)blocks), dim3(256), 0, s>>>(G, C, N, R, M, ldc);
+    return hipGetLastError();
+}
+
+// RCCL's all-gather, looked up in the process (the caller's RCCL, whose communicator we are
+// handed); librccl.so.1 is opened by soname only if nothing in the process exports it
+using AllGatherFn = decltype(&ncclAllGather);
+AllGatherFn shard_allgather()
+{
+    static AllGatherFn fn = nullptr;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *sym = dlsym(RTLD_DEFAULT, "ncclAllGather");
+        if (!sym) {
+            if (void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL)) sym = dlsym(h, "ncclAllGather");
+        }
+        fn = (AllGatherFn)sym;
+    });
+    return fn;
+}
+
+size_t sharded_ws(int t, int64_t M, int64_t N, int64_t K, int world)
+{
+    int64_t row0, rows, R;
+    shard_geom(M, world, 0, row0, rows, R); // rank 0 holds the most rows
+    return align_up((size_t)N * R * 2) + align_up((size_t)world * N * R * 2) + ws_bytes(t, GQ_ACT_Q8_1, rows, N, K);
 }
 
 } // namespace
@@ -399,6 +471,81 @@ int gq_quantize_fp8(const void *X, void *codes, void *scales, int64_t rows, int6
     hipError_t e = gq::launch_act_quant(gq::ACT_F8, (const uint16_t *)X, ldx, rows, K, codes, scales, nullptr,
                                         (hipStream_t)stream);
     if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed: %s", hipGetErrorString(e));
+    return GQ_OK;
+}
+
+int gq_shard_rows(int64_t M, int world, int rank, int64_t *row0, int64_t *rows, int64_t *R)
+{
+    g_err.clear();
+    if (M < 0 || world < 1 || rank < 0 || rank >= world)
+        return fail(GQ_EINVAL, "bad shard (M=%lld world=%d rank=%d)", (long long)M, world, rank);
+    if (!row0 || !rows || !R) return fail(GQ_EINVAL, "null output pointer");
+    shard_geom(M, world, rank, *row0, *rows, *R);
+    return GQ_OK;
+}
+
+int gq_assemble_shards(const void *gathered, void *C, int world, int64_t N, int64_t R, int64_t M, int64_t ldc,
+                       void *stream)
+{
+    g_err.clear();
+    if (world < 1 || N < 0 || R < 0 || M < 0) return fail(GQ_EINVAL, "negative size or world < 1");
+    if (M > (int64_t)world * R) return fail(GQ_EINVAL, "M=%lld > world*R=%lld", (long long)M, (long long)world * R);
+    if (R % 8 != 0) return fail(GQ_EINVAL, "R=%lld is not a multiple of 8", (long long)R);
+    if (ldc < M) return fail(GQ_EINVAL, "ldc=%lld < M=%lld", (long long)ldc, (long long)M);
+    if (N == 0 || M == 0) return GQ_OK;
+    if (!gathered || !C) return fail(GQ_EINVAL, "null pointer");
+    hipError_t e = launch_assemble((const uint16_t *)gathered, (uint16_t *)C, N, R, M, ldc, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (assemble): %s", hipGetErrorString(e));
+    return GQ_OK;
+}
+
+size_t gq_mmq_sharded_workspace_size(gq_type t, int64_t M, int64_t N, int64_t K, int world)
+{
+    if (N <= 0 || K <= 0 || M < 0 || world < 1) return 0;
+    return sharded_ws(t, M, N, K, world);
+}
+
+int gq_mmq_sharded(gq_type t, const void *A_shard, const void *B, void *C, int64_t M, int64_t N, int64_t K,
+                   int64_t ldb, int64_t ldc, int world, int rank, void *nccl_comm, void *workspace,
+                   size_t workspace_bytes, void *stream)
+{
+    g_err.clear();
+    int rc = check_common(t, M, N, K);
+    if (rc != GQ_OK) return rc;
+    if (world < 1 || rank < 0 || rank >= world) return fail(GQ_EINVAL, "bad rank %d of world %d", rank, world);
+    if (world > 1 && !nccl_comm) return fail(GQ_EINVAL, "world=%d needs an RCCL communicator", world);
+    if (M == 0 || N == 0) return GQ_OK;
+    if (K == 0) return fail(GQ_EINVAL, "K must be positive");
+    if (!B || !C) return fail(GQ_EINVAL, "null pointer (B=%p C=%p)", B, C);
+    if (ldc < M) return fail(GQ_EINVAL, "ldc=%lld < M=%lld", (long long)ldc, (long long)M);
+    const size_t need = sharded_ws(t, M, N, K, world);
+    if (!workspace || workspace_bytes < need)
+        return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace ? workspace_bytes : (size_t)0, need);
+    int64_t row0, rows, R;
+    shard_geom(M, world, rank, row0, rows, R);
+    if (rows > 0 && !A_shard) return fail(GQ_EINVAL, "null A_shard for %lld rows", (long long)rows);
+    uint8_t *ws = (uint8_t *)workspace;
+    uint16_t *slab = (uint16_t *)ws;                                  // (N, R)
+    uint16_t *gathered = (uint16_t *)(ws + align_up((size_t)N * R * 2)); // (world, N, R)
+    uint8_t *mws = (uint8_t *)gathered + align_up((size_t)world * N * R * 2);
+    const size_t mws_bytes = workspace_bytes - (size_t)(mws - ws);
+    hipStream_t s = (hipStream_t)stream;
+    if (rows > 0) {
+        rc = gq_mmq(t, A_shard, B, slab, rows, N, K, ldb, R, mws, mws_bytes, stream);
+        if (rc != GQ_OK) return rc;
+    }
+    if (world == 1 && !nccl_comm) { // the slab is the output
+        hipError_t e = launch_assemble(slab, (uint16_t *)C, N, R, M, ldc, s);
+        if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (assemble): %s", hipGetErrorString(e));
+        return GQ_OK;
+    }
+    AllGatherFn ag = shard_allgather();
+    if (!ag) return fail(GQ_EUNSUPPORTED, "RCCL (ncclAllGather) not found in the process");
+    // (a short or empty last shard sends its slab's pad columns too: assemble never reads them)
+    const ncclResult_t nr = ag(slab, gathered, (size_t)N * R, ncclFloat16, (ncclComm_t)nccl_comm, s);
+    if (nr != ncclSuccess) return fail(GQ_EHIP, "ncclAllGather failed (%d)", (int)nr);
+    hipError_t e = launch_assemble(gathered, (uint16_t *)C, N, R, M, ldc, s);
+    if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (assemble): %s", hipGetErrorString(e));
     return GQ_OK;
 }
 

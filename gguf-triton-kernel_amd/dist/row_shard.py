@@ -7,7 +7,8 @@ R = ceil(M / world) rounded up to `align` (the last shard may be short or empty)
 activations are replicated.  Each rank writes its (N, R) output into a padded slab and one
 all_gather_into_tensor (backend "nccl" = RCCL on ROCm; "gloo" in the CPU tests) collects
 (world, N, R); the (N, M) result is that slab viewed with the rank axis moved inside each
-token row -- for N = 1 (decode) a free reshape, otherwise one permute copy.
+token row -- for N = 1 (decode) a free reshape, otherwise one device copy kernel
+(gq_assemble_shards, the C ABI's form of this step; gq_mmq_sharded is the whole step in C).
 
 There is no reference counterpart (the reference is single-GPU); this is the north_star's
 "N partitioned across up to 8 GPUs of one node with RCCL all-gather".
@@ -94,12 +95,20 @@ class RowShardedMMQ:
                                            async_op=async_op)
         return out, work
 
-    def assemble(self, gathered: torch.Tensor) -> torch.Tensor:
-        """(world, N, R) -> (N, M)."""
+    def assemble(self, gathered: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """(world, N, R) -> (N, M): a free view at N = 1; otherwise on a ROCm device the C ABI's
+        gq_assemble_shards kernel (into `out` when given), on the CPU (gloo tests) a permute."""
         W, N, R = gathered.shape
-        if N == 1:
+        if N == 1 and out is None:
             return gathered.view(1, W * R)[:, :self.M]
-        return gathered.permute(1, 0, 2).reshape(N, W * R)[:, :self.M]
+        if gathered.is_cuda:
+            from kernels._lib import assemble_shards
+            return assemble_shards(gathered, self.M, out=out)
+        C = gathered.permute(1, 0, 2).reshape(N, W * R)[:, :self.M]
+        if out is not None:
+            out.copy_(C)
+            return out
+        return C
 
     def __call__(self, B: torch.Tensor, N: int) -> torch.Tensor:
         slab = self.local(B, N)

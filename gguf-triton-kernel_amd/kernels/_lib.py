@@ -38,6 +38,11 @@ SIGNATURES = {
     "gq_act_prepare_ex": ([_I, _P, _I64, _I64, _I64, _P, _SZ, _P], _I),
     "gq_mmq_prepared_ex": ([_I, _I, _P, _P, _SZ, _P, _I64, _I64, _I64, _I64, _P], _I),
     "gq_quantize_fp8": ([_P, _P, _P, _I64, _I64, _I64, _P], _I),
+    "gq_shard_rows": ([_I64, _I, _I, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                       ctypes.POINTER(ctypes.c_int64)], _I),
+    "gq_assemble_shards": ([_P, _P, _I, _I64, _I64, _I64, _I64, _P], _I),
+    "gq_mmq_sharded_workspace_size": ([_I, _I64, _I64, _I64, _I], _SZ),
+    "gq_mmq_sharded": ([_I, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _I, _P, _P, _SZ, _P], _I),
     "gq_last_error": ([], ctypes.c_char_p),
     "gq_version": ([], _I),
 }
@@ -211,3 +216,40 @@ def quantize_fp8_device(X: torch.Tensor):
         _check(lib().gq_quantize_fp8(X2.data_ptr(), codes.data_ptr(), scales.data_ptr(), rows, K, X2.stride(0),
                                      stream))
     return codes, scales
+
+
+def shard_rows(M: int, world: int, rank: int):
+    """(row0, rows, R) of rank `rank` (gq_shard_rows; the rule of dist/row_shard.shard_rows)."""
+    r0, rows, R = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    _check(lib().gq_shard_rows(M, world, rank, ctypes.byref(r0), ctypes.byref(rows), ctypes.byref(R)))
+    return r0.value, rows.value, R.value
+
+
+def assemble_shards(gathered: torch.Tensor, M: int, out: torch.Tensor | None = None) -> torch.Tensor:
+    """(world, N, R) fp16 slabs -> (N, M) on the device (gq_assemble_shards)."""
+    _require_device(gathered, "gathered")
+    if gathered.dtype != torch.float16 or gathered.dim() != 3 or not gathered.is_contiguous():
+        raise RuntimeError("gathered must be a contiguous (world, N, R) fp16 tensor")
+    W, N, R = gathered.shape
+    C = _check_out(out, N, M, gathered.device)
+    with torch.cuda.device(gathered.device):
+        stream = torch.cuda.current_stream(gathered.device).cuda_stream
+        _check(lib().gq_assemble_shards(gathered.data_ptr(), C.data_ptr(), W, N, R, M, C.stride(0), stream))
+    return C
+
+
+def mmq_sharded_single(gtype: int, A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int) -> torch.Tensor:
+    """gq_mmq_sharded at world 1 (no communicator): the C-ABI sharded entry point end to end on
+    one device (multi-rank callers pass their own RCCL communicator through the C ABI)."""
+    _require_device(A, "A")
+    _check_weights(gtype, A, M, K)
+    B = _check_acts(B, N, K)
+    C = _check_out(None, N, M, A.device)
+    need = int(lib().gq_mmq_sharded_workspace_size(gtype, M, N, K, 1))
+    ws = torch.empty(max(need, 1), dtype=torch.uint8, device=A.device)
+    with torch.cuda.device(A.device):
+        stream = torch.cuda.current_stream(A.device).cuda_stream
+        _check(lib().gq_mmq_sharded(gtype, A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, B.stride(0), C.stride(0),
+                                    1, 0, None, ws.data_ptr(), ws.numel(), stream))
+    return C
+

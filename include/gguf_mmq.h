@@ -114,6 +114,37 @@ int gq_quantize_q8_1(const void *X, void *Y, int64_t rows, int64_t K, int64_t ld
  */
 int gq_quantize_fp8(const void *X, void *codes, void *scales, int64_t rows, int64_t K, int64_t ldx, void *stream);
 
+/*
+ * Row-sharded MMQ over the GPUs of one node (SURVEY.md 8(b) "gq_mmq_sharded", 8(e)).  The
+ * reference is single-GPU and has no counterpart; this is the C form of dist/row_shard.py.
+ *
+ * gq_shard_rows: rank `rank` of `world` owns weight rows [*row0, *row0 + *rows) of M, padded
+ * shard size *R = ceil(M / world) rounded up to 64 (the last shards may be short or empty).
+ * Its packed bytes are A + row0 * (K / gq_block_elems(t)) * gq_block_bytes(t): no repacking.
+ */
+int gq_shard_rows(int64_t M, int world, int rank, int64_t *row0, int64_t *rows, int64_t *R);
+
+/*
+ * (world, N, R) fp16 slabs, as an all-gather leaves them -> C (N rows of ldc), columns [0, M):
+ * C[n][m] = gathered[m / R][n][m % R].  One device copy kernel on `stream`.
+ */
+int gq_assemble_shards(const void *gathered, void *C, int world, int64_t N, int64_t R, int64_t M, int64_t ldc,
+                       void *stream);
+
+/*
+ * One rank's row-sharded MMQ: the local gq_mmq of this rank's rows (A_shard, from
+ * gq_shard_rows) into an (N, R) slab, an RCCL all-gather of the slabs over `nccl_comm` (an
+ * ncclComm_t of this rank, world ranks; RCCL is resolved at run time from the process, so the
+ * caller's own RCCL is the one used), and gq_assemble_shards into C (N, ldc) -- every rank ends
+ * with the whole output.  All on `stream`, no host sync (graph-capturable as RCCL allows).
+ * world == 1 needs no communicator (NULL: no collective; a 1-rank communicator is used as given).  Workspace: at least
+ * gq_mmq_sharded_workspace_size(t, M, N, K, world) bytes.
+ */
+size_t gq_mmq_sharded_workspace_size(gq_type t, int64_t M, int64_t N, int64_t K, int world);
+int gq_mmq_sharded(gq_type t, const void *A_shard, const void *B, void *C, int64_t M, int64_t N, int64_t K,
+                   int64_t ldb, int64_t ldc, int world, int rank, void *nccl_comm, void *workspace,
+                   size_t workspace_bytes, void *stream);
+
 /* Text of the last error on this thread ("" if none). */
 const char *gq_last_error(void);
 

@@ -115,3 +115,28 @@ def test_dropin_k_assertions():
         mmq_q4_k(torch.zeros(144, dtype=torch.int8), B, 1, 1, 128)
     with pytest.raises(AssertionError):
         mmq_q6_k(torch.zeros(210, dtype=torch.int8), B, 1, 1, 300)
+
+
+def test_shard_rows_matches_row_shard_rule():
+    """gq_shard_rows (C ABI, host-only) gives dist/row_shard.py's split for every rank."""
+    import kernels._lib as kl
+    from dist.row_shard import shard_rows
+    for M in (0, 1, 63, 64, 65, 4096, 8192, 11008, 28672, 28673):
+        for world in (1, 2, 3, 4, 8):
+            for rank in range(world):
+                assert kl.shard_rows(M, world, rank) == shard_rows(M, world, rank), (M, world, rank)
+    with pytest.raises(RuntimeError):
+        kl.shard_rows(64, 2, 2)
+    with pytest.raises(RuntimeError):
+        kl.shard_rows(64, 0, 0)
+
+
+def test_sharded_host_argument_checks():
+    import kernels._lib as kl
+    L = kl.lib()
+    assert L.gq_mmq_sharded(0, None, None, None, 64, 1, 4096, 4096, 64, 2, 0, None, None, 0, None) != 0
+    assert b"communicator" in L.gq_last_error()
+    assert L.gq_mmq_sharded(0, None, None, None, 64, 1, 4096, 4096, 64, 2, 2, None, None, 0, None) != 0
+    assert L.gq_assemble_shards(None, None, 2, 4, 60, 100, 100, None) != 0  # R % 8
+    assert L.gq_assemble_shards(None, None, 2, 4, 64, 129, 200, None) != 0  # M > world * R
+    assert L.gq_mmq_sharded_workspace_size(0, 4096, 128, 4096, 8) > 8 * 128 * 512 * 2

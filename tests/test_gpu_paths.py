@@ -287,3 +287,69 @@ def test_fused_split_k_reduce_bit_identical(fmt, M, N, K, splits, monkeypatch):
     sub = qA.reshape(M, -1)[rows].reshape(-1)
     ideal = O.mmq_from_fp16(fmt, sub, B, len(rows), N, K, O.IDEAL)
     assert O.max_rel_err(fused[0].cpu().numpy()[:, rows], ideal) <= TIGHT_GEMM
+
+
+@pytest.mark.parametrize("W,N,R,M,pad", [(2, 5, 64, 100, 0), (8, 128, 3584, 28672, 0), (4, 3, 64, 250, 7),
+                                         (3, 17, 128, 384, 0), (8, 1, 1024, 8192, 0)])
+def test_assemble_shards_kernel(W, N, R, M, pad):
+    """gq_assemble_shards (the all-gather's (world, N, R) -> (N, M) step) against torch's
+    permute, vector (16-byte) and scalar (odd M / ldc) forms."""
+    from kernels._lib import assemble_shards
+    dev = _dev()
+    g = torch.randn(W, N, R, generator=torch.Generator().manual_seed(W * N + R)).to(torch.float16).to(dev)
+    want = g.permute(1, 0, 2).reshape(N, W * R)[:, :M]
+    out = torch.full((N, M + pad), -1.0, dtype=torch.float16, device=dev)[:, :M]
+    got = assemble_shards(g, M, out=out)
+    torch.cuda.synchronize()
+    assert torch.equal(got.view(torch.int16), want.view(torch.int16))
+
+
+@pytest.mark.parametrize("fmt,M,N,K", [("q6_k", 1000, 1, 8192), ("q4_k", 4096, 128, 4096), ("q8_0", 300, 16, 1024)])
+def test_mmq_sharded_entry_point_world1(fmt, M, N, K):
+    """gq_mmq_sharded through the C ABI at world 1 (no communicator): the same bits as gq_mmq."""
+    from kernels._lib import TYPES, mmq, mmq_sharded_single
+    dev = _dev()
+    qA = random_blocks(fmt, M, K, seed=M + N)
+    B = random_activations(N, K, seed=K + N)
+    A_t = torch.from_numpy(qA.view(np.int8)).to(dev)
+    B_t = torch.from_numpy(B).to(dev)
+    want = mmq(TYPES[fmt], A_t, B_t, M, N, K)
+    got = mmq_sharded_single(TYPES[fmt], A_t, B_t, M, N, K)
+    torch.cuda.synchronize()
+    assert torch.equal(got.view(torch.int16), want.view(torch.int16))
+
+
+def test_mmq_sharded_entry_point_rccl_one_rank():
+    """gq_mmq_sharded with a real 1-rank RCCL communicator (created here through RCCL's own C
+    API): the run-time-resolved ncclAllGather leg and the assemble give gq_mmq's bits."""
+    import ctypes
+    import kernels._lib as kl
+    dev = _dev()
+    rccl = ctypes.CDLL("librccl.so.1")
+
+    class UniqueId(ctypes.Structure):
+        _fields_ = [("internal", ctypes.c_char * 128)]
+
+    uid = UniqueId()
+    assert rccl.ncclGetUniqueId(ctypes.byref(uid)) == 0
+    comm = ctypes.c_void_p()
+    rccl.ncclCommInitRank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, UniqueId, ctypes.c_int]
+    torch.cuda.set_device(dev)
+    assert rccl.ncclCommInitRank(ctypes.byref(comm), 1, uid, 0) == 0
+    try:
+        fmt, M, N, K = "q6_k", 1000, 8, 2048
+        qA = random_blocks(fmt, M, K, seed=5)
+        B = random_activations(N, K, seed=6)
+        A_t = torch.from_numpy(qA.view(np.int8)).to(dev)
+        B_t = torch.from_numpy(B).to(dev)
+        want = kl.mmq(kl.TYPES[fmt], A_t, B_t, M, N, K)
+        C = torch.empty(N, M, dtype=torch.float16, device=dev)
+        need = int(kl.lib().gq_mmq_sharded_workspace_size(kl.TYPES[fmt], M, N, K, 1))
+        ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        kl._check(kl.lib().gq_mmq_sharded(kl.TYPES[fmt], A_t.data_ptr(), B_t.data_ptr(), C.data_ptr(), M, N, K, K, M,
+                                          1, 0, comm, ws.data_ptr(), need, stream))
+        torch.cuda.synchronize()
+        assert torch.equal(C.view(torch.int16), want.view(torch.int16))
+    finally:
+        rccl.ncclCommDestroy(comm)
