@@ -300,9 +300,16 @@ __device__ __forceinline__ void stage_frags<Q8_0>(const uint8_t *wr, int g, int 
     }
 }
 
+// AUX = cache policy of the DMA (2 = nt).  GQ_GEMM_WNT=1 sets nt on the weight stream: equal
+// on Q8_0, 2-7% slower on Q4_K/Q6_K with weights rotated over 1 GiB (profiles/r02/
+// gemm_weight_nt_ab_rejected.txt), so the default policy stays
+#ifndef GQ_GEMM_WNT
+#define GQ_GEMM_WNT 0
+#endif
+template <int AUX = 0>
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, uint8_t *lds_dst, uint32_t voff, uint32_t soff)
 {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void *)lds_dst, 16, voff, soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void *)lds_dst, 16, voff, soff, 0, AUX);
 }
 
 __device__ __forceinline__ int act_swz(int r) { return (r >> 1) & 7; }
@@ -437,7 +444,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
                 vo = wv[i] + 16u * wpc[i];
                 so = (uint32_t)(WStage<F>::SB * w);
             }
-            dma16(wrs, k < G::W_REAL ? dst + 1024 * k : lds + G::SCRATCH, vo, so);
+            dma16<GQ_GEMM_WNT ? 2 : 0>(wrs, k < G::W_REAL ? dst + 1024 * k : lds + G::SCRATCH, vo, so);
         }
     };
     auto issue_a = [&](int64_t a) {
