@@ -27,6 +27,9 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
+if os.environ.get("GQ_TUNE_ROTATE"):  # weight-rotation bytes (default bench.ROTATE_BYTES, 1 GiB: cold)
+    bench.ROTATE_BYTES = int(os.environ["GQ_TUNE_ROTATE"])
+
 dev = torch.device("cuda:0")
 KEYS = ("GQ_ABLATE", "GQ_GEMV_R", "GQ_GEMV_CAP", "GQ_GEMM_AQ_NB4", "GQ_GEMM_AQ", "GQ_DECODE_NT4_CACHE", "GQ_DECODE_MAXNT", "GQ_DECODE_WIDE_ROWS", "GQ_GEMM_I8", "GQ_GEMM_LOADERS", "GQ_GEMM_PARTIAL", "GQ_GEMM_RG", "GQ_GEMM_NB", "GQ_GEMM_SPLITS", "GQ_DECODE_CAP", "GQ_NO_FUSED_DECODE", "GQ_DECODE_NI", "GQ_DECODE_NS", "GQ_BLAS_MIN_TOKENS")
 for spec in args:
