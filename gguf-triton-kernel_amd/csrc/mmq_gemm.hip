@@ -306,6 +306,11 @@ __device__ __forceinline__ void stage_frags<Q8_0>(const uint8_t *wr, int g, int 
 #ifndef GQ_GEMM_WNT
 #define GQ_GEMM_WNT 0
 #endif
+// GQ_GEMM_AFIRST=1: the prologue issues the activation sub-stages before the first weight stage
+// (the first sub-stage then waits for everything issued: vmcnt(0))
+#ifndef GQ_GEMM_AFIRST
+#define GQ_GEMM_AFIRST 0
+#endif
 template <int AUX = 0>
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, uint8_t *lds_dst, uint32_t voff, uint32_t soff)
 {
@@ -470,6 +475,10 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
     // rel = a - a0: W issues in iterations [max(0, rel-NAS+1), rel-1] that are multiples of SPW
     auto wait_a = [&](int rel) {
         constexpr int na = ABL & 4 ? 0 : G::NA, nw = ABL & 2 ? 0 : G::NW; // (ablated streams issue nothing)
+        if (GQ_GEMM_AFIRST && rel == 0) { // prologue A(0..NAS-2) then W(w0): sub-stage 0 needs all of it
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+            return;
+        }
         constexpr int base = (G::NAS - 2) * na;
         const int lo = rel - G::NAS + 1 > 0 ? rel - G::NAS + 1 : 0, hi = rel - 1;
         const int w_after = hi >= lo ? hi / SPW - (lo + SPW - 1) / SPW + 1 : 0;
@@ -564,10 +573,17 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
     if (!AQ && loader) { // loader waves: the DMA schedule of the pipeline note, no multiply
         if (w0 < w1) {
             const int64_t a0 = 4 * sb0, a1 = 4 * sb1;
+            if constexpr (GQ_GEMM_AFIRST) {
 #pragma unroll
-            for (int i = 0; i < G::NWS - 1; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
+                for (int i = 0; i < G::NAS - 1; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
 #pragma unroll
-            for (int i = 0; i < G::NAS - 1; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
+                for (int i = 0; i < G::NWS - 1; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
+            } else {
+#pragma unroll
+                for (int i = 0; i < G::NWS - 1; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
+#pragma unroll
+                for (int i = 0; i < G::NAS - 1; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
+            }
             for (int64_t a = a0; a < a1; ++a) {
                 wait_a((int)(a - a0)); // A(a) landed -> barrier: the compute waves take sub-stage a
                 issue_a(a + G::NAS - 1 < a1 ? a + G::NAS - 1 : a1 - 1);
@@ -579,10 +595,17 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
     }
     if (w0 < w1) {
         const int64_t a0 = 4 * sb0, a1 = 4 * sb1;
+        if constexpr (GQ_GEMM_AFIRST) {
 #pragma unroll
-        for (int i = 0; i < G::NWS - 1 && NL == 0; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
+            for (int i = 0; i < G::NAS - 1 && NL == 0; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
 #pragma unroll
-        for (int i = 0; i < G::NAS - 1 && NL == 0; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
+            for (int i = 0; i < G::NWS - 1 && NL == 0; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
+        } else {
+#pragma unroll
+            for (int i = 0; i < G::NWS - 1 && NL == 0; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
+#pragma unroll
+            for (int i = 0; i < G::NAS - 1 && NL == 0; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
+        }
 #ifdef GQ_GEMM_STAMPS
         t_issued = __builtin_amdgcn_s_memtime() - t_start;
 #endif
