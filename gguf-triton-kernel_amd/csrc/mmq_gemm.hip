@@ -1143,6 +1143,7 @@ bool gemm_supported(int /*fmt*/, int64_t K) { return K > 0 && K % 256 == 0; }
 
 bool gemm_aq_ok(const GemmPlan &p)
 {
+    if (GQ_GEMM_Q8_FINE) return false; // the in-kernel quantizer's loader schedule assumes super-block weight stages
     if (const char *env = getenv("GQ_GEMM_AQ"))
         if (env[0] == '0') return false;
     // splits of at most two super-blocks: the quantization (a few passes of the loader waves)
