@@ -311,6 +311,11 @@ __device__ __forceinline__ void stage_frags<Q8_0>(const uint8_t *wr, int g, int 
 #ifndef GQ_GEMM_AFIRST
 #define GQ_GEMM_AFIRST 0
 #endif
+// GQ_GEMM_PSER=1: the loader waves let the first weight stage land before issuing the
+// prologue's activation sub-stages (the two streams in flight together are super-additive)
+#ifndef GQ_GEMM_PSER
+#define GQ_GEMM_PSER 0
+#endif
 template <int AUX = 0>
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, uint8_t *lds_dst, uint32_t voff, uint32_t soff)
 {
@@ -581,6 +586,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
             } else {
 #pragma unroll
                 for (int i = 0; i < G::NWS - 1; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
+                if constexpr (GQ_GEMM_PSER) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // weights landed first
 #pragma unroll
                 for (int i = 0; i < G::NAS - 1; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
             }
