@@ -5,6 +5,40 @@
 
 namespace gq {
 
+// Tuning overrides of the measured defaults.  Read ONCE per process from GQ_* environment
+// variables (gq_capi.hip, std::call_once) -- the launch path never calls getenv -- and changed
+// at run time only through the debug entry point gq_debug_set_tuning (tests, A/B tools; not
+// thread-safe against concurrent launches).  0 / -1 = "the default the code measured".
+struct Tuning {
+    long long blas_min_tokens = 768;          // GQ_BLAS_MIN_TOKENS: library GEMM from this many tokens (<= 0: never)
+    long long gemm_max_bytes = 1LL << 31;     // GQ_GEMM_MAX_BYTES: weight / activation bytes per GEMM launch
+    int gemm_i8 = 0;                          // GQ_GEMM_I8: Q8_0 int8-MFMA form
+    int fused_decode = 1;                     // GQ_NO_FUSED_DECODE=1 -> 0
+    int decode_maxnt = 0;                     // GQ_DECODE_MAXNT: token-group cap of the fused decode (0: auto)
+    int decode_nt4_cache = 1;                 // GQ_DECODE_NT4_CACHE
+    int gemm_aq = 1;                          // GQ_GEMM_AQ: in-kernel quantization of 16/32-token tiles
+    int gemm_aq_nb4 = 0;                      // GQ_GEMM_AQ_NB4
+    int gemm_nb = 0;                          // GQ_GEMM_NB: 16-token groups per tile, 1/2/4/8 (0: auto)
+    int gemm_rg = 0;                          // GQ_GEMM_RG: 1 or 2 (0: auto)
+    int gemm_loaders = -1;                    // GQ_GEMM_LOADERS: 0 or 4 (-1: auto)
+    long long gemm_splits = 0;                // GQ_GEMM_SPLITS: split-K factor (0: auto)
+    int gemm_partial_f32 = 0;                 // GQ_GEMM_PARTIAL=f32
+    int gemm_fused_reduce = 0;                // GQ_GEMM_FUSED_REDUCE
+    long long gemv_cap = 0;                   // GQ_GEMV_CAP (0: auto)
+    int gemv_r = 0;                           // GQ_GEMV_R: rows per wave, 1/2/4 (0: auto)
+    int wgemm = -1;                           // GQ_WGEMM: weight-register GEMM 0 off / 1 on (-1: auto)
+    int wgemm_rg = 0;                         // GQ_WGEMM_RG: 1 or 2 (0: auto)
+    int wgemm_nb = 0;                         // GQ_WGEMM_NB: 2/4/8 (0: auto)
+    int wgemm_splits = 0;                     // GQ_WGEMM_SPLITS (0: auto)
+    int ablate = 0;                           // GQ_ABLATE (GQ_ABLATION diagnostic builds only)
+};
+const Tuning &tuning();
+// key = the environment variable's name ("GQ_GEMM_SPLITS", ...); value validated (an override
+// that no kernel is instantiated for is rejected).  Returns 0, or -1 for an unknown key or a
+// value out of range.  reset: back to the environment's values.
+int set_tuning(const char *key, long long value);
+void reset_tuning();
+
 enum ActMode : int { ACT_AOS = 0, ACT_SOA = 1, ACT_DEQ = 2, ACT_I8 = 3, ACT_F8 = 4 };
 // Activation form the MFMA GEMM reads (mmq_gemm.hip): fp16 x~, q8_1 codes (Q8_0 int8 MFMA),
 // or the fp8 variant's e4m3 codes.
@@ -62,6 +96,20 @@ bool gemm_supported(int fmt, int64_t K);
 GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, int act = AF_F16);
 hipError_t launch_gemm(int fmt, const uint8_t *A, const GemmAct &x, uint16_t *C, float *partials,
                        const GemmPlan &plan, int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
+
+// Weight-register GEMM (mmq_wgemm.hip): weights streamed into VGPRs a super-block ahead,
+// activations (fp16 x~, act_quant DEQ form) register-staged into a two-slot LDS ring; 128*rg
+// rows x 16*nb tokens per workgroup, split-K `splits` ways (fp16 partials + wreduce_kernel).
+struct WGemmPlan {
+    int rg = 2, nb = 8;
+    int tiles_m = 0, tiles_n = 0;
+    int splits = 1, sb_per_split = 1;
+    size_t partial_bytes = 0;
+};
+// rg / nb: tile shape (rg in {1, 2}, nb in {2, 4, 8}); splits <= 0: as many as fill 256 CUs
+WGemmPlan plan_wgemm(int fmt, int64_t M, int64_t N, int64_t K, int rg, int nb, int splits);
+hipError_t launch_wgemm(int fmt, const uint8_t *A, const uint16_t *X, uint16_t *C, void *partials,
+                        const WGemmPlan &plan, int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
 
 // Dequantization and the library GEMM (mmq_dequant.hip).  perm: store 4-groups as (0,2,1,3),
 // matching act_quant's DEQ form.  blas_gemm returns 0 or a negative code.

@@ -14,6 +14,112 @@
 #include "gguf_blocks.hpp"
 #include "gguf_internal.hpp"
 
+namespace gq {
+namespace {
+
+Tuning g_tuning;
+std::once_flag g_tuning_once;
+
+bool parse_key(Tuning &t, const char *key, long long v)
+{
+    auto in = [&](std::initializer_list<long long> ok) {
+        for (long long o : ok)
+            if (v == o) return true;
+        return false;
+    };
+    const std::string k = key;
+    if (k == "GQ_BLAS_MIN_TOKENS") t.blas_min_tokens = v;
+    else if (k == "GQ_GEMM_MAX_BYTES") {
+        if (v <= 0) return false;
+        t.gemm_max_bytes = v < (1LL << 31) ? v : (1LL << 31);
+    } else if (k == "GQ_GEMM_I8") t.gemm_i8 = v != 0;
+    else if (k == "GQ_NO_FUSED_DECODE") t.fused_decode = v == 0;
+    else if (k == "GQ_DECODE_MAXNT") {
+        if (v < 0 || v > 8) return false;
+        t.decode_maxnt = (int)v;
+    } else if (k == "GQ_DECODE_NT4_CACHE") t.decode_nt4_cache = v != 0;
+    else if (k == "GQ_GEMM_AQ") t.gemm_aq = v != 0;
+    else if (k == "GQ_GEMM_AQ_NB4") t.gemm_aq_nb4 = v != 0;
+    else if (k == "GQ_GEMM_NB") {
+        if (!in({0, 1, 2, 4, 8})) return false;
+        t.gemm_nb = (int)v;
+    } else if (k == "GQ_GEMM_RG") {
+        if (!in({0, 1, 2})) return false;
+        t.gemm_rg = (int)v;
+    } else if (k == "GQ_GEMM_LOADERS") {
+        if (!in({-1, 0, 4})) return false;
+        t.gemm_loaders = (int)v;
+    } else if (k == "GQ_GEMM_SPLITS") {
+        if (v < 0) return false;
+        t.gemm_splits = v;
+    } else if (k == "GQ_GEMM_PARTIAL") t.gemm_partial_f32 = v != 0; // 1 = f32
+    else if (k == "GQ_GEMM_FUSED_REDUCE") t.gemm_fused_reduce = v != 0;
+    else if (k == "GQ_GEMV_CAP") {
+        if (v < 0) return false;
+        t.gemv_cap = v;
+    } else if (k == "GQ_GEMV_R") {
+        if (!in({0, 1, 2, 4})) return false;
+        t.gemv_r = (int)v;
+    } else if (k == "GQ_WGEMM") {
+        if (!in({-1, 0, 1})) return false;
+        t.wgemm = (int)v;
+    } else if (k == "GQ_WGEMM_RG") {
+        if (!in({0, 1, 2})) return false;
+        t.wgemm_rg = (int)v;
+    } else if (k == "GQ_WGEMM_NB") {
+        if (!in({0, 2, 4, 8})) return false;
+        t.wgemm_nb = (int)v;
+    } else if (k == "GQ_WGEMM_SPLITS") {
+        if (v < 0 || v > 4096) return false;
+        t.wgemm_splits = (int)v;
+    } else if (k == "GQ_ABLATE") t.ablate = (int)v;
+    else return false;
+    return true;
+}
+
+void tuning_from_env(Tuning &t)
+{
+    t = Tuning{};
+    static const char *const keys[] = {"GQ_BLAS_MIN_TOKENS", "GQ_GEMM_MAX_BYTES", "GQ_GEMM_I8", "GQ_NO_FUSED_DECODE",
+                                       "GQ_DECODE_MAXNT", "GQ_DECODE_NT4_CACHE", "GQ_GEMM_AQ", "GQ_GEMM_AQ_NB4",
+                                       "GQ_GEMM_NB", "GQ_GEMM_RG", "GQ_GEMM_LOADERS", "GQ_GEMM_SPLITS",
+                                       "GQ_GEMM_PARTIAL", "GQ_GEMM_FUSED_REDUCE", "GQ_GEMV_CAP", "GQ_GEMV_R",
+                                       "GQ_WGEMM", "GQ_WGEMM_RG", "GQ_WGEMM_NB", "GQ_WGEMM_SPLITS", "GQ_ABLATE"};
+    for (const char *k : keys) {
+        const char *e = getenv(k); // the only getenv of the library: once per process
+        if (!e || !*e) continue;
+        long long v;
+        if (std::string(k) == "GQ_GEMM_PARTIAL") v = std::string(e) == "f32";
+        else v = atoll(e);
+        if (!parse_key(t, k, v)) fprintf(stderr, "gguf_mmq: ignoring %s=%s (out of range)\n", k, e);
+    }
+}
+
+} // namespace
+
+const Tuning &tuning()
+{
+    std::call_once(g_tuning_once, [] { tuning_from_env(g_tuning); });
+    return g_tuning;
+}
+
+int set_tuning(const char *key, long long value)
+{
+    tuning();
+    Tuning t = g_tuning;
+    if (!key || !parse_key(t, key, value)) return -1;
+    g_tuning = t;
+    return 0;
+}
+
+void reset_tuning()
+{
+    tuning();
+    tuning_from_env(g_tuning);
+}
+
+} // namespace gq
+
 namespace {
 
 thread_local std::string g_err;
@@ -45,12 +151,9 @@ bool use_gemv(int64_t N, int64_t K) { return N <= kGemvMaxTokens || !gq::gemm_su
 // override GQ_BLAS_MIN_TOKENS (0 = never) is for tuning and tests.
 int64_t blas_min_tokens()
 {
-    const char *e = getenv("GQ_BLAS_MIN_TOKENS");
-    if (e) {
-        const long long v = atoll(e);
-        return v <= 0 ? INT64_MAX : (int64_t)v;
-    }
-    return 768; // measured crossover: 11008x4096 Q4_K 512 tokens 90 vs 121 us, 4096^2 1024 tokens
+    // default 768: measured crossover (11008x4096 Q4_K 512 tokens 90 vs 121 us, 4096^2 1024 tokens)
+    const long long v = gq::tuning().blas_min_tokens;
+    return v <= 0 ? INT64_MAX : (int64_t)v;
 }
 bool use_blas(int64_t N, int64_t K) { return !use_gemv(N, K) && N >= blas_min_tokens(); }
 
@@ -62,9 +165,8 @@ bool use_blas(int64_t N, int64_t K) { return !use_gemv(N, K) && N >= blas_min_to
 // (GQ_GEMM_MAX_BYTES lowers the limit: tests cut small calls into many chunks.)
 int64_t gemm_max_bytes()
 {
-    const char *e = getenv("GQ_GEMM_MAX_BYTES");
     const int64_t lim = (int64_t)1 << 31;
-    const int64_t v = e ? atoll(e) : lim;
+    const int64_t v = gq::tuning().gemm_max_bytes;
     return v > 0 && v < lim ? v : lim;
 }
 int64_t row_bytes_of(int t, int64_t K) { return (K / block_elems(t)) * block_bytes(t); }
@@ -79,11 +181,26 @@ int64_t gemm_toks_per_launch(int64_t N, int64_t K)
     return n < 16 ? 16 : (n < N ? n : N);
 }
 
+// Weight-register GEMM (mmq_wgemm.hip) for the fp16 form from this many tokens on (GQ_WGEMM
+// forces it on / off).
+constexpr int64_t kWgemmMinTokens = 33;
+bool use_wgemm(int form, int64_t N)
+{
+    const int w = gq::tuning().wgemm;
+    return form == gq::AF_F16 && (w == 1 || (w < 0 && N >= kWgemmMinTokens));
+}
+gq::WGemmPlan wgemm_plan(int t, int64_t M, int64_t N, int64_t K)
+{
+    const gq::Tuning &tu = gq::tuning();
+    const int nb = tu.wgemm_nb ? tu.wgemm_nb : (N > 64 ? 8 : (N > 32 ? 4 : 2));
+    const int rg = tu.wgemm_rg ? tu.wgemm_rg : 2;
+    return gq::plan_wgemm(t, M, N, K, rg, nb, tu.wgemm_splits);
+}
+
 bool use_i8(int t, int64_t N, int64_t K)
 {
     if (t != GQ_Q8_0 || use_gemv(N, K) || use_blas(N, K)) return false;
-    const char *e = getenv("GQ_GEMM_I8");
-    return e ? atoi(e) != 0 : false;
+    return gq::tuning().gemm_i8 != 0;
 }
 
 // Which kernels a call runs.  The q8_1 activations (the reference's semantics) go to the fused
@@ -137,7 +254,8 @@ size_t ws_bytes(int t, int act, int64_t M, int64_t N, int64_t K)
         for (int64_t mc : {mr, M % mr})
             for (int64_t nc : {nt, N % nt})
                 if (mc > 0 && nc > 0) {
-                    const size_t q = gq::plan_gemm(t, mc, nc, K, r.form).partial_bytes;
+                    const size_t q = use_wgemm(r.form, nc) ? wgemm_plan(t, mc, nc, K).partial_bytes
+                                                            : gq::plan_gemm(t, mc, nc, K, r.form).partial_bytes;
                     p = q > p ? q : p;
                 }
         b += align_up(p);
@@ -216,6 +334,15 @@ size_t sharded_ws(int t, int64_t M, int64_t N, int64_t K, int world)
 } // namespace
 
 extern "C" {
+
+int gq_debug_set_tuning(const char *key, long long value)
+{
+    g_err.clear();
+    if (gq::set_tuning(key, value) != 0)
+        return fail(GQ_EINVAL, "unknown tuning key or value out of range: %s=%lld", key ? key : "(null)", value);
+    return GQ_OK;
+}
+void gq_debug_reset_tuning(void) { gq::reset_tuning(); }
 
 int gq_block_elems(gq_type t) { return block_elems(t); }
 int gq_block_bytes(gq_type t) { return block_bytes(t); }
@@ -330,6 +457,12 @@ static int compute(gq_type t, int act, const void *A, void *workspace, size_t wo
         for (int64_t n0 = 0; n0 < N && e == hipSuccess; n0 += nt)
             for (int64_t m0 = 0; m0 < M && e == hipSuccess; m0 += mr) {
                 const int64_t mc = M - m0 < mr ? M - m0 : mr, nc = N - n0 < nt ? N - n0 : nt;
+                if (use_wgemm(r.form, nc)) {
+                    e = gq::launch_wgemm(t, (const uint8_t *)A + m0 * row_bytes_of(t, K), c.xdeq + n0 * K,
+                                         (uint16_t *)C + n0 * ldc + m0, c.partials, wgemm_plan(t, mc, nc, K), mc, nc,
+                                         K, ldc, s);
+                    continue;
+                }
                 gq::GemmAct x;
                 x.xdeq = c.xdeq ? c.xdeq + n0 * K : nullptr;
                 x.xq = c.xq + n0 * K;
@@ -359,14 +492,15 @@ int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int6
         return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace ? workspace_bytes : (size_t)0, need);
     if (ldb < K) return fail(GQ_EINVAL, "ldb=%lld < K=%lld", (long long)ldb, (long long)K);
     const Route r = route(t, act, N, K);
-    if (r.gemv && gq::decode_fused_ok(t, N, K) && !getenv("GQ_NO_FUSED_DECODE")) {
+    if (r.gemv && gq::decode_fused_ok(t, N, K) && gq::tuning().fused_decode) {
         // one launch: activation quantization in LDS + decode GEMV
         hipError_t e = gq::launch_decode_fused(t, (const uint8_t *)A, (const uint16_t *)B, ldb, (uint16_t *)C, M, N,
                                                K, ldc, (hipStream_t)stream);
         if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (decode): %s", hipGetErrorString(e));
         return GQ_OK;
     }
-    if (!r.gemv && !r.blas && act == GQ_ACT_Q8_1 && r.form == gq::AF_F16 && gemm_rows_per_launch(t, M, K) >= M &&
+    if (!r.gemv && !r.blas && act == GQ_ACT_Q8_1 && r.form == gq::AF_F16 && !use_wgemm(r.form, N) &&
+        gemm_rows_per_launch(t, M, K) >= M &&
         gemm_toks_per_launch(N, K) >= N) {
         // 16/32-token tiles whose split fits LDS: the GEMM quantizes the activations itself (no
         // act_quant launch; bit-identical to the DEQ form it would read)

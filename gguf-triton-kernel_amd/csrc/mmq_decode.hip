@@ -542,7 +542,7 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p)
     // group wins (4096^2 11.1 vs 14.3, 14336x4096 27.4 vs 29.7) -- profiles/r02/decode_maxnt_ab.txt.
     // By K, not by size: row shards of one matrix take the same path (bit-identical results).
     int nt_cap = fmt == Q6_K && K >= 8192 ? 2 : 4;
-    if (const char *env = getenv("GQ_DECODE_MAXNT")) nt_cap = atoi(env); // tuning override
+    if (tuning().decode_maxnt > 0) nt_cap = tuning().decode_maxnt; // tuning override
     while (p.nt > 1 && p.nt > nt_cap) p.nt >>= 1;
     while ((size_t)RING + act_lds(fmt, p.nt, K) > (size_t)LDS_CAP) {
         if (p.nt == 1) return false;
@@ -586,7 +586,7 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p)
     p.itc = ((p.nt <= 2 && units <= (fmt == Q6_K ? 2 : 4)) || (p.nt == 1 && units <= 8)) ? (int)itc : 0;
     // four tokens, one unit per lane (K <= 4096): cached too (Q6_K 14336x4096 x4 27.7 -> 20.7 us,
     // profiles/r02/decode_nt4_cache_ab.txt; GQ_DECODE_NT4_CACHE=0: off)
-    if (p.nt == 4 && units == 1 && !(getenv("GQ_DECODE_NT4_CACHE") && getenv("GQ_DECODE_NT4_CACHE")[0] == '0'))
+    if (p.nt == 4 && units == 1 && tuning().decode_nt4_cache)
         p.itc = 1;
     const int64_t waves = g.ngroups < W ? g.ngroups : W;
     p.grid = (int)((waves + DW - 1) / DW);

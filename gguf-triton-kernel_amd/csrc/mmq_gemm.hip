@@ -1074,7 +1074,7 @@ hipError_t launch_cfg(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P,
     const bool fused = pl.splits > 1 && pl.pf16 && pl.fused_reduce;
     const int cb = fused ? split_counters((int)(grid.x * grid.y) * NWAVE) : -1;
 #ifdef GQ_ABLATION
-    const int abl = getenv("GQ_ABLATE") ? atoi(getenv("GQ_ABLATE")) : 0;
+    const int abl = tuning().ablate;
 #define GQ_ABL_CASE(v) \
     case v: gemm_kernel<F, NB, RG, v, AM, NL, AQ><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, ldd, cps, pl.pf16, cb); break;
     switch (abl) {
@@ -1150,14 +1150,13 @@ bool gemm_supported(int /*fmt*/, int64_t K) { return K > 0 && K % 256 == 0; }
 bool gemm_aq_ok(const GemmPlan &p)
 {
     if (GQ_GEMM_Q8_FINE) return false; // the in-kernel quantizer's loader schedule assumes super-block weight stages
-    if (const char *env = getenv("GQ_GEMM_AQ"))
-        if (env[0] == '0') return false;
+    if (!tuning().gemm_aq) return false;
     // splits of at most two super-blocks: the quantization (a few passes of the loader waves)
     // then hides under the first weight stage; longer splits measured neutral to 2% slower
     // (Q4_K 4096x11008 x16), shorter ones 4-9% faster (profiles/r02/gemm_aq_ab.txt)
     // 64-token tiles (GQ_GEMM_AQ_NB4=1) measured 11-14% slower: the loader waves' quantization
     // (32 blocks per lane) no longer hides under the first weight stage
-    const int max_nb = getenv("GQ_GEMM_AQ_NB4") && getenv("GQ_GEMM_AQ_NB4")[0] == '1' ? 4 : 2;
+    const int max_nb = tuning().gemm_aq_nb4 ? 4 : 2;
     return p.act == AF_F16 && p.loaders == 4 && p.rg == R1 && p.nb <= max_nb && p.chunks_per_split <= 2 &&
            4 * p.chunks_per_split <= aq_sub_of(p.nb);
 }
@@ -1167,18 +1166,18 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, int act)
     GemmPlan p;
     p.act = act == AF_I8 && fmt != Q8_0 ? AF_F16 : act;
     p.nb = pick_nb(N);
-    if (const char *env = getenv("GQ_GEMM_NB")) p.nb = atoi(env);
+    if (tuning().gemm_nb) p.nb = tuning().gemm_nb; // (validated: 1, 2, 4 or 8)
     // two 16-row groups per wave (256-row tiles: half the activation traffic per weight) for
     // tall matrices at full token tiles
     // (Q4_K only: Q6_K's padded 240-B rows and Q8_0's 272-B rows do not fit 256 rows twice)
     p.rg = (fmt == Q4_K && p.nb == 8 && M >= 8192) ? 2 * R1 : R1; // measured: 11008 rows 5% faster
-    if (const char *env = getenv("GQ_GEMM_RG")) p.rg = (fmt == Q4_K && p.nb == 8 && atoi(env) == 2) ? 2 * R1 : R1;
+    if (tuning().gemm_rg) p.rg = (fmt == Q4_K && p.nb == 8 && tuning().gemm_rg == 2) ? 2 * R1 : R1;
     if (p.act != AF_F16) p.rg = 1; // the code forms run 128-row tiles
     // four loader waves (DMA issue off the multiplying waves' path) for the 128-row fp16 form:
     // Q6_K 28672x8192x128 116.5 -> 103.7 us, Q4_K 4096^2x128 17.4 -> 16.7, Q8_0 4096^2x128
     // 20.6 -> 20.1 (profiles/r02/loader_tune.txt); GQ_GEMM_LOADERS=0 restores all-wave issue
     p.loaders = p.act == AF_F16 && p.rg == R1 ? 4 : 0;
-    if (const char *env = getenv("GQ_GEMM_LOADERS")) p.loaders = p.act == AF_F16 && atoi(env) == 4 ? 4 : 0;
+    if (tuning().gemm_loaders >= 0) p.loaders = p.act == AF_F16 && tuning().gemm_loaders == 4 ? 4 : 0;
     const int64_t nws = K / 256; // weight stages (super-blocks)
     if (nws == 0) return p;      // not a GEMM shape (gemm_supported() is false): nothing to plan
     const int64_t bm = 16 * NWAVE * p.rg;
@@ -1187,7 +1186,7 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, int act)
     // second wave of workgroups (258 workgroups ran 25% slower than 172 at 11008 x 4096 x 128)
     const int64_t cus = 256;
     int64_t S = tiles >= cus ? 1 : cus / tiles;
-    if (const char *env = getenv("GQ_GEMM_SPLITS")) S = atoll(env); // tuning / test override
+    if (tuning().gemm_splits > 0) S = tuning().gemm_splits; // tuning / test override
     const int64_t max_split = nws / 2 > 0 ? nws / 2 : 1;            // >= 2 super-blocks per split
     if (S > max_split) S = max_split;
     if (S < 1) S = 1;
@@ -1199,7 +1198,7 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, int act)
     // partial values rounded to fp16 after a power-of-two scale that keeps them below 2^15
     // (Q8_0 4096^2 x128 step 23.2 -> 22.1 us; profiles/r02/pf16_step.txt)
     p.pf16 = 1;
-    if (const char *env = getenv("GQ_GEMM_PARTIAL")) p.pf16 = env[0] == 'f' && env[1] == '1';
+    if (tuning().gemm_partial_f32) p.pf16 = 0;
     // GQ_GEMM_FUSED_REDUCE=1: fp16 partials summed inside the GEMM by the last wave to arrive
     // at each (tile, wave) row group, no reduce launch.  Bit-identical, but slower on every
     // shape measured (Q8_0 4096^2 x128 20.5 -> 24.9 us, Q4_K 11008x4096 x128 37.3 -> 41.6;
@@ -1207,7 +1206,7 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, int act)
     // agent-scope stores and loads (cache-wide write-back/invalidate fences instead: 3x slower),
     // where the separate launch finds the partials in its XCD's L2.  Off by default.
     p.fused_reduce = 0;
-    if (const char *env = getenv("GQ_GEMM_FUSED_REDUCE")) p.fused_reduce = p.pf16 && env[0] == '1';
+    p.fused_reduce = p.pf16 && tuning().gemm_fused_reduce;
     // blocked partials: S x (tiles) x 128 rows x 16*nb tokens (padded tiles)
     p.partial_bytes = S > 1 ? (size_t)S * tiles * bm * 16 * p.nb * (p.pf16 ? 2 : sizeof(float)) : 0;
     if (S > 1 && p.pf16) p.partial_bytes += (size_t)S * tiles * NWAVE * sizeof(int); // the per-wave e's

@@ -74,7 +74,7 @@ hipError_t launch_one(const uint8_t *A, const int8_t *xq, const float *xd, const
 {
     const int64_t groups = (M + 4 * R - 1) / (4 * R);
     int64_t cap = 2048;
-    if (const char *env = getenv("GQ_GEMV_CAP")) cap = atoll(env); // tuning
+    if (tuning().gemv_cap > 0) cap = tuning().gemv_cap; // tuning
     dim3 grid((unsigned)(groups < cap ? groups : cap), (unsigned)((N + NT - 1) / NT)), block(256);
     gemv_kernel<F, NT, R><<<grid, block, 0, s>>>(A, xq, xd, xs, C, M, N, K, ldc);
     return hipGetLastError();
@@ -88,7 +88,7 @@ hipError_t launch_fmt(const uint8_t *A, const int8_t *xq, const float *xd, const
     // (Q4_K 4096x28672 x2 30.3 -> 23.9 us, Q6_K 8192x28672 x2 64.9 -> 58.3); 3-4 tokens 2,
     // Q6_K 4 (x4 81.7 -> 72.9); GQ_GEMV_R overrides
     int r = N <= 2 ? (F == Q8_0 ? 4 : 2) : (F == Q6_K ? 4 : 2);
-    if (const char *env = getenv("GQ_GEMV_R")) r = atoi(env);
+    if (tuning().gemv_r) r = tuning().gemv_r; // (validated: 1, 2 or 4)
     if (N == 1) return r == 8 ? launch_one<F, 1, 8>(A, xq, xd, xs, C, M, N, K, ldc, s)
                               : r == 2 ? launch_one<F, 1, 2>(A, xq, xd, xs, C, M, N, K, ldc, s)
                                        : launch_one<F, 1, 4>(A, xq, xd, xs, C, M, N, K, ldc, s);

@@ -45,6 +45,8 @@ SIGNATURES = {
     "gq_mmq_sharded": ([_I, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _I, _P, _P, _SZ, _P], _I),
     "gq_last_error": ([], ctypes.c_char_p),
     "gq_version": ([], _I),
+    "gq_debug_set_tuning": ([ctypes.c_char_p, ctypes.c_longlong], _I),
+    "gq_debug_reset_tuning": ([], None),
 }
 
 _lib = None
@@ -65,6 +67,33 @@ def lib():
             fn.restype = restype
         _lib = handle
     return _lib
+
+
+def set_tuning(key: str, value: int):
+    """Override one GQ_* tuning default by name for later calls (gq_debug_set_tuning; the
+    library reads the environment once, so setting os.environ later has no effect)."""
+    _check(lib().gq_debug_set_tuning(key.encode(), int(value)))
+
+
+def reset_tuning():
+    """Back to the tuning values the environment gave at first use."""
+    lib().gq_debug_reset_tuning()
+
+
+class tuning:
+    """Context manager: `with tuning(GQ_GEMM_SPLITS=8, GQ_WGEMM=0): ...` (values reset on exit)."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            set_tuning(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        reset_tuning()
+        return False
 
 
 def _check(status: int):

@@ -151,6 +151,16 @@ const char *gq_last_error(void);
 /* Library ABI version (major * 100 + minor). */
 int gq_version(void);
 
+/*
+ * Debug / tuning only (no counterpart in the reference; not for production callers).  The
+ * library reads its GQ_* tuning variables from the environment ONCE, at first use; this entry
+ * overrides one of them by name (e.g. "GQ_GEMM_SPLITS", "GQ_WGEMM_NB") for later calls in the
+ * process.  Values no kernel is instantiated for are rejected (GQ_EINVAL).  Not thread-safe
+ * against calls running concurrently on other threads.  reset: back to the environment's values.
+ */
+int gq_debug_set_tuning(const char *key, long long value);
+void gq_debug_reset_tuning(void);
+
 #ifdef __cplusplus
 }
 #endif

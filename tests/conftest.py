@@ -32,3 +32,18 @@ def golden():
         return cases
 
     return {fmt: load(fmt) for fmt in ("q8_0", "q4_k", "q6_k")}
+
+
+@pytest.fixture
+def tune():
+    """tune(GQ_GEMM_SPLITS=8, GQ_WGEMM=0, ...): override the library's tuning defaults for this
+    test (gq_debug_set_tuning; the library reads GQ_* from the environment once, so setting
+    os.environ in a test has no effect); everything is reset after the test."""
+    import kernels._lib as kl
+
+    def set_(**kw):
+        for k, v in kw.items():
+            kl.set_tuning(k, int(v))
+
+    yield set_
+    kl.reset_tuning()

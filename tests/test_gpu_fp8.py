@@ -64,7 +64,7 @@ def test_fp8_mmq(fmt, M, N, K):
     assert O.max_rel_err(got, ref) <= FP8_BOUND, O.max_rel_err(got, ref)
 
 
-def test_fp8_prepared_and_splits(monkeypatch):
+def test_fp8_prepared_and_splits(tune):
     import kernels._lib as kl
     dev = _dev()
     M, N, K = 384, 96, 2048
@@ -77,7 +77,7 @@ def test_fp8_prepared_and_splits(monkeypatch):
         kl.act_prepare(B_t, N, K, ws, act="fp8")
         outs = []
         for splits in ("1", "4"):
-            monkeypatch.setenv("GQ_GEMM_SPLITS", splits)
+            tune(GQ_GEMM_SPLITS=splits)
             outs.append(kl.mmq_prepared(g, A_t, ws, M, N, K, act="fp8").cpu().numpy())
         ideal = O.mmq_fp8_ideal(fmt, qA, B, M, N, K)
         for o in outs:

@@ -219,15 +219,12 @@ def test_baseline_configs_full_size(fmt, M, K, Ns):
         # (3) row independence: the same rows computed as a separate matrix give identical bits
         #     (split-K off for both: the split factor is chosen per shape and changes the fp32
         #     summation order of the MFMA path)
-        import os
-        os.environ["GQ_GEMM_SPLITS"] = "1"
-        try:
+        import kernels._lib as kl
+        with kl.tuning(GQ_GEMM_SPLITS=1, GQ_WGEMM_SPLITS=1):
             Cf = _fn(fmt)(A_t, B_t, M, N, K)
             sub_t = torch.from_numpy(sub.view(np.int8)).to(dev)
             Cs = _fn(fmt)(sub_t, B_t, len(rows), N, K)
             torch.cuda.synchronize()
-        finally:
-            os.environ.pop("GQ_GEMM_SPLITS")
         assert np.array_equal(Cs.cpu().numpy().view(np.uint16), Cf.cpu().numpy()[:, rows].view(np.uint16))
 
 
@@ -248,11 +245,11 @@ def test_device_dequantize_matches_oracle(fmt):
 
 @pytest.mark.parametrize("fmt", FMTS)
 @pytest.mark.parametrize("M,N,K,force", [(300, 800, 512, False), (65, 24, 1024, True), (130, 33, 256, True)])
-def test_blas_path(fmt, M, N, K, force, monkeypatch):
+def test_blas_path(fmt, M, N, K, force, tune):
     """N_tok >= 768 (or any N with GQ_BLAS_MIN_TOKENS forced): dequantized fp16 W (same
     k-permutation as x~) on hipBLASLt; same tolerance as the MFMA path."""
     if force:
-        monkeypatch.setenv("GQ_BLAS_MIN_TOKENS", "9")
+        tune(GQ_BLAS_MIN_TOKENS=9)
     qA = random_blocks(fmt, M, K, seed=M + N)
     B = random_activations(N, K, seed=K)
     got = run(fmt, qA, B, M, N, K)
@@ -290,12 +287,13 @@ def test_layer_mix_from_gguf(tmp_path, fuse):
 
 
 @pytest.mark.parametrize("fmt", ("q4_k",))
-def test_gemm_256_row_tiles(fmt, monkeypatch):
-    """Two 16-row groups per wave (256-row tiles), with and without split-K, ragged edges."""
-    monkeypatch.setenv("GQ_GEMM_RG", "2")
+def test_gemm_256_row_tiles(fmt, tune):
+    """Two 16-row groups per wave (256-row tiles) of the LDS-DMA GEMM, with and without split-K,
+    ragged edges."""
+    tune(GQ_GEMM_RG=2, GQ_WGEMM=0)
     for M, N, K, splits in ((600, 100, 1024, None), (300, 128, 2048, "4")):
         if splits:
-            monkeypatch.setenv("GQ_GEMM_SPLITS", splits)
+            tune(GQ_GEMM_SPLITS=splits)
         qA = random_blocks(fmt, M, K, seed=M)
         B = random_activations(N, K, seed=N)
         got = run(fmt, qA, B, M, N, K)

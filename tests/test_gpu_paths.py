@@ -43,10 +43,10 @@ def _run(fmt, qA, B, M, N, K):
 @pytest.mark.parametrize("M,N,K,splits", [(128, 5, 256, None), (200, 16, 512, None), (130, 33, 768, "1"),
                                           (64, 64, 1024, None), (300, 100, 2048, "3"), (256, 128, 4096, None),
                                           (96, 128, 4096, "8"), (1000, 77, 1280, None)])
-def test_q8_0_int8_mfma_gemm(M, N, K, splits, monkeypatch):
-    monkeypatch.setenv("GQ_GEMM_I8", "1")
+def test_q8_0_int8_mfma_gemm(M, N, K, splits, tune):
+    tune(GQ_GEMM_I8=1, GQ_WGEMM=0)  # (the int8 form lives in the LDS-DMA GEMM)
     if splits:
-        monkeypatch.setenv("GQ_GEMM_SPLITS", splits)
+        tune(GQ_GEMM_SPLITS=splits)
     qA = random_blocks("q8_0", M, K, seed=M + 3 * N)
     B = random_activations(N, K, seed=K + N)
     got = _run("q8_0", qA, B, M, N, K)
@@ -57,9 +57,9 @@ def test_q8_0_int8_mfma_gemm(M, N, K, splits, monkeypatch):
     assert O.allclose(exact, got, 0.01)
 
 
-def test_q8_0_int8_mfma_golden(golden, monkeypatch):
+def test_q8_0_int8_mfma_golden(golden, tune):
     """Every golden case of the reference through the int8 form (cases with N >= 5 run it)."""
-    monkeypatch.setenv("GQ_GEMM_I8", "1")
+    tune(GQ_GEMM_I8=1, GQ_WGEMM=0)
     for c in golden["q8_0"]:
         got = _run("q8_0", c["qA"], c["B"], c["M"], c["N"], c["K"])
         if c["kind"] != "tiny":
@@ -92,14 +92,14 @@ def test_prepared_matches_oracle(fmt, N):
 @pytest.mark.parametrize("M,K", [(28672, 8192), (8192, 28672)])
 @pytest.mark.parametrize("G", (2, 4, 8))
 @pytest.mark.parametrize("N", (1, 128))
-def test_row_sharded_q6_k_70b(M, K, G, N, monkeypatch):
+def test_row_sharded_q6_k_70b(M, K, G, N, tune):
     """Config 4: Q6_K Llama-70B ffn_gate/up (28672x8192) and ffn_down (8192x28672) split into G
     row shards (zero-copy byte ranges), each run through RowShardedMMQ.local, assembled as the
     all-gather would; vs the unsharded call (bit for bit, split-K off on both) and the oracle
     on sampled rows."""
     from dist.row_shard import RowShardedMMQ, shard_bytes
     from kernels._lib import TYPES, mmq
-    monkeypatch.setenv("GQ_GEMM_SPLITS", "1")
+    tune(GQ_GEMM_SPLITS=1, GQ_WGEMM_SPLITS=1)
     dev = _dev()
     qA = random_blocks("q6_k", M, K, seed=M + G)
     B = random_activations(N, K, seed=N + K)
@@ -126,7 +126,7 @@ def test_row_sharded_q6_k_70b(M, K, G, N, monkeypatch):
 
 
 @pytest.mark.parametrize("fmt", ("q8_0", "q4_k", "q6_k"))
-def test_gemm_chunked_launches_bit_exact(fmt, monkeypatch):
+def test_gemm_chunked_launches_bit_exact(fmt, tune):
     """The GEMM path's 32-bit offset guard: calls over GQ_GEMM_MAX_BYTES of weights or of fp16
     activations run as row x token chunks; with a small limit (many chunks in both dims) the
     result equals the one-launch result bit for bit (split-K off on both)."""
@@ -137,10 +137,9 @@ def test_gemm_chunked_launches_bit_exact(fmt, monkeypatch):
     B = random_activations(N, K, seed=10)
     A_t = torch.from_numpy(qA.view(np.int8)).to(dev)
     B_t = torch.from_numpy(B).to(dev)
-    monkeypatch.setenv("GQ_GEMM_SPLITS", "1")
-    monkeypatch.setenv("GQ_BLAS_MIN_TOKENS", "0")
+    tune(GQ_GEMM_SPLITS=1, GQ_WGEMM_SPLITS=1, GQ_BLAS_MIN_TOKENS=0)
     one = mmq(TYPES[fmt], A_t, B_t, M, N, K)
-    monkeypatch.setenv("GQ_GEMM_MAX_BYTES", str(256 * 1024))  # 256 rows / 128 tokens per launch
+    tune(GQ_GEMM_MAX_BYTES=256 * 1024)  # 256 rows / 128 tokens per launch
     many = mmq(TYPES[fmt], A_t, B_t, M, N, K)
     torch.cuda.synchronize()
     assert torch.equal(one.view(torch.int16), many.view(torch.int16))
@@ -174,13 +173,12 @@ def test_gemm_weights_over_4gib():
 
 
 @pytest.mark.parametrize("partial", ("f16", "f32"))
-def test_split_k_partials_huge_cancelling_sums(partial, monkeypatch):
+def test_split_k_partials_huge_cancelling_sums(partial, tune):
     """Split-K partial sums far outside fp16's range whose total cancels to ~0: the second half
     of K repeats the first half's weights against negated activations.  fp16 partials carry a
     per-wave power-of-two scale, so neither form overflows (no inf/NaN) and both cancel."""
     from kernels._lib import TYPES, mmq
-    monkeypatch.setenv("GQ_GEMM_PARTIAL", partial)
-    monkeypatch.setenv("GQ_GEMM_SPLITS", "8")
+    tune(GQ_GEMM_PARTIAL=int(partial == "f32"), GQ_GEMM_SPLITS=8, GQ_WGEMM=0)
     dev = _dev()
     M, N, K = 256, 128, 4096
     half = random_blocks("q8_0", M, K // 2, seed=31).reshape(M, -1)
@@ -236,7 +234,7 @@ def test_long_k_small_n_routes(fmt, K, N):
 
 @pytest.mark.parametrize("fmt", ("q8_0", "q4_k", "q6_k"))
 @pytest.mark.parametrize("M,N,K", [(512, 5, 1024), (300, 16, 2048), (1024, 17, 4096), (640, 32, 1536), (128, 9, 512), (384, 64, 1024), (256, 40, 2048)])
-def test_gemm_in_kernel_quantization_bit_identical(fmt, M, N, K, monkeypatch):
+def test_gemm_in_kernel_quantization_bit_identical(fmt, M, N, K, tune):
     """16/32-token tiles quantize their activations inside the GEMM (no act_quant launch): the
     result is the same bits as the act_quant (DEQ) + GEMM path, and matches the oracle."""
     from kernels._lib import TYPES, mmq
@@ -249,7 +247,7 @@ def test_gemm_in_kernel_quantization_bit_identical(fmt, M, N, K, monkeypatch):
     Bw[:, :K] = torch.from_numpy(B).to(dev)
     B_t = Bw[:, :K]
     fused = mmq(TYPES[fmt], A_t, B_t, M, N, K)
-    monkeypatch.setenv("GQ_GEMM_AQ", "0")
+    tune(GQ_GEMM_AQ=0)
     staged = mmq(TYPES[fmt], A_t, B_t, M, N, K)
     torch.cuda.synchronize()
     assert torch.equal(fused.view(torch.int16), staged.view(torch.int16))
@@ -261,7 +259,7 @@ def test_gemm_in_kernel_quantization_bit_identical(fmt, M, N, K, monkeypatch):
 @pytest.mark.parametrize("M,N,K,splits", [(4096, 128, 4096, None), (300, 100, 2048, "3"), (1000, 77, 1280, "5"),
                                           (8192, 128, 2048, "2"), (520, 17, 4096, "11"), (256, 5, 4096, "16"),
                                           (384, 40, 3072, "12")])
-def test_fused_split_k_reduce_bit_identical(fmt, M, N, K, splits, monkeypatch):
+def test_fused_split_k_reduce_bit_identical(fmt, M, N, K, splits, tune):
     """Split-K partials summed inside the GEMM by each row group's last-arriving wave
     (GQ_GEMM_FUSED_REDUCE=1, mmq_gemm.hip GemmPlan::fused_reduce; measured slower, so opt-in)
     give the same bits as the separate
@@ -270,15 +268,16 @@ def test_fused_split_k_reduce_bit_identical(fmt, M, N, K, splits, monkeypatch):
     split counts that are not multiples of 8, ragged M/N."""
     from kernels._lib import TYPES, mmq
     dev = _dev()
+    tune(GQ_WGEMM=0)  # (the fused reduce belongs to the LDS-DMA GEMM)
     if splits:
-        monkeypatch.setenv("GQ_GEMM_SPLITS", splits)
+        tune(GQ_GEMM_SPLITS=splits)
     qA = random_blocks(fmt, M, K, seed=M + 7 * N)
     B = random_activations(N, K, seed=K + 5 * N)
     A_t = torch.from_numpy(qA.view(np.int8)).to(dev)
     B_t = torch.from_numpy(B).to(dev)
-    monkeypatch.setenv("GQ_GEMM_FUSED_REDUCE", "1")
+    tune(GQ_GEMM_FUSED_REDUCE=1)
     fused = [mmq(TYPES[fmt], A_t, B_t, M, N, K) for _ in range(3)]
-    monkeypatch.setenv("GQ_GEMM_FUSED_REDUCE", "0")
+    tune(GQ_GEMM_FUSED_REDUCE=0)
     staged = mmq(TYPES[fmt], A_t, B_t, M, N, K)
     torch.cuda.synchronize()
     for f in fused:
