@@ -30,6 +30,7 @@ struct Tuning {
     int wgemm_rg = 0;                         // GQ_WGEMM_RG: 1 or 2 (0: auto)
     int wgemm_nb = 0;                         // GQ_WGEMM_NB: 2/4/8 (0: auto)
     int wgemm_splits = 0;                     // GQ_WGEMM_SPLITS (0: auto)
+    int wgemm_wd = 0;                         // GQ_WGEMM_WD: weight super-blocks in registers, 2/3/4 (0: auto)
     int ablate = 0;                           // GQ_ABLATE (GQ_ABLATION diagnostic builds only)
 };
 const Tuning &tuning();
@@ -102,6 +103,7 @@ hipError_t launch_gemm(int fmt, const uint8_t *A, const GemmAct &x, uint16_t *C,
 // rows x 16*nb tokens per workgroup, split-K `splits` ways (fp16 partials + wreduce_kernel).
 struct WGemmPlan {
     int rg = 2, nb = 8;
+    int wd = 2; // super-blocks of weights held in registers (wd - 1 in flight): 2, 3, 4 (4: rg 1 only)
     int tiles_m = 0, tiles_n = 0;
     int splits = 1, sb_per_split = 1;
     size_t partial_bytes = 0;

@@ -1,33 +1,28 @@
-// mmq_wgemm.hip -- batched MMQ (many tokens) with the weights streamed straight into registers.
+// mmq_wgemm.hip -- batched MMQ (33+ tokens): weights streamed into registers, activations by
+// LDS-DMA, on v_mfma_f32_16x16x32_f16.
 //
-// C[t][m] = sum_k W[m][k] * x~[t][k] on v_mfma_f32_16x16x32_f16 (fp32 accumulate), x~ = fp16(d*q)
-// the q8_1-quantized activation (act_quant.hip DEQ form: the integers kernels/cpu_impls
-// multiplies, mmq_*_q8_1_cpu.py), W dequantized to fp16 in registers from the packed GGUF bytes.
-// Replaces the reference's Triton GEMM loops (kernels/mmq_q8_0.py:59-93, mmq_q4_k.py:167-229,
-// mmq_q6_k.py:122-186) for 64+ tokens.
+// C[t][m] = sum_k W[m][k] * x~[t][k] (fp32 accumulate), x~ = fp16(d*q) the q8_1-quantized
+// activation (act_quant.hip DEQ form: the integers kernels/cpu_impls multiplies,
+// mmq_*_q8_1_cpu.py), W dequantized to fp16 in registers from the packed GGUF bytes.  Replaces
+// the reference's Triton GEMM loops (kernels/mmq_q8_0.py:59-93, mmq_q4_k.py:167-229,
+// mmq_q6_k.py:122-186).
 //
-// Why this shape.  In mmq_gemm.hip both operands went HBM/L2 -> LDS by LDS-DMA and
-// the per-CU DMA ingest (~25 GB/s per CU), not the MFMA or HBM, bounded the kernel.  Here a
-// wave's A operand -- 16*RG weight rows private to it -- never touches LDS: each lane loads the
-// bytes of its own fragment slots with buffer loads one super-block ahead (VGPR double buffer),
-// dequantizes in registers and feeds the MFMA.  Only the activations, which all 8 waves share,
-// go through LDS: register-staged (a buffer load one sub-stage ahead, ds_write_b128 the next
-// sub-stage behind), a two-slot ring, one barrier per 64-element sub-stage.  Every VMEM op is
-// an ordinary load the compiler counts (no LDS-DMA, so no vmcnt(0) drains).
+// Why this shape.  A wave's vector-memory returns are in issue order: a wave that
+// streams both the weights (HBM) and the activations (L2, re-read by every row tile) waits for
+// the slow stream whenever it needs the fast one.  So the two streams live in different waves:
+//   loader waves (NL = 4): the tile's activations, HBM/L2 -> LDS by LDS-DMA (1 KiB per
+//     instruction), a ring of R sub-stages (64 K elements each) with L = R - 2 in flight;
+//     nothing else in their queues;
+//   compute waves (NWC): each owns 16*RG weight rows; its lanes load their own fragment bytes of
+//     a super-block (256 K elements) into registers one super-block ahead (double buffer),
+//     dequantize in registers, read the activation fragments from the ring, multiply.
+// One s_barrier per sub-stage (loaders: before it, wait for sub-stage a to land; after it, issue
+// sub-stage a + L into the slot read two sub-stages ago).
 //
-// Workgroup = 8 waves (two per SIMD, <= 256 VGPRs) = BM = 128*RG weight rows x BN = 16*NB tokens
-// x one K split.  Wave w owns rows 16*(RG*w + rf) + [0,16) and every token of the tile, so each
-// weight is dequantized once per workgroup and each activation fragment read from LDS feeds RG
-// MFMAs.
-//
-// K order.  An MFMA k-step is one natural 32-element run of K (a Q8_0 block, a Q4_K sub-block,
-// two Q6_K scale groups) and lane group g = lane>>4 takes its 8-element piece g, as fp16 pairs in
-// the order (0,2,1,3,4,6,5,7) that packed dequantization produces -- exactly act_quant's DEQ
-// layout, so a B fragment is one 16-byte LDS read.  Per super-block (256 elements) lane (row r,
-// g) therefore needs: Q4_K qs bytes 32j+8g..+8 (j = 0..3, both nibbles) + the 16-byte header;
-// Q6_K ql bytes 64h+32v+8g..+8, qh bytes 128+32h+8g..+8, the 16 scale bytes and d; Q8_0 qs bytes
-// 34i+2+8g..+8 and d of each of the 8 blocks.  Those are loaded as they lie (gfx950 runs with
-// unaligned buffer access: Q6_K/Q8_0 fields are 2-byte aligned).
+// K order.  The k-step -> element map follows what a lane loaded (WB<F>::e below): lane group
+// g = lane>>4 supplies 8 consecutive elements in the order (0,2,1,3,4,6,5,7) that packed
+// dequantization produces -- act_quant's DEQ layout, so a B fragment is one 16-byte LDS read of
+// the same 8 activations.
 //
 // MFMA 16x16x32 f16 (gfx950): lane l holds A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15];
 // D[row 4(l>>4)+i][col l&15] in acc element i.  Weight rows are A rows, tokens B columns.
@@ -42,9 +37,9 @@ namespace {
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
 
-constexpr int NWAVE = 8;
-constexpr int THREADS = 64 * NWAVE;
+constexpr int NL = 4; // loader waves
 
 __device__ __forceinline__ h2 as_h2(uint32_t v) { return __builtin_bit_cast(h2, v); }
 __device__ __forceinline__ uint32_t as_u32(h2 v) { return __builtin_bit_cast(uint32_t, v); }
@@ -60,10 +55,6 @@ __device__ __forceinline__ h2 magic(uint32_t v, uint32_t mask) { return as_h2((v
 __device__ __forceinline__ h2 pair02(uint32_t c) { return as_h2(__builtin_amdgcn_perm(0x64646464u, c, 0x04020400u)); }
 __device__ __forceinline__ h2 pair13(uint32_t c) { return as_h2(__builtin_amdgcn_perm(0x64646464u, c, 0x04030401u)); }
 
-__device__ __forceinline__ u32x2 bl8(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s)
-{
-    return __builtin_amdgcn_raw_buffer_load_b64(r, v, s, 0);
-}
 __device__ __forceinline__ u32x4 bl16(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s)
 {
     return __builtin_amdgcn_raw_buffer_load_b128(r, v, s, 0);
@@ -72,18 +63,23 @@ __device__ __forceinline__ uint32_t bl4(__amdgpu_buffer_rsrc_t r, uint32_t v, ui
 {
     return __builtin_amdgcn_raw_buffer_load_b32(r, v, s, 0);
 }
+// one LDS-DMA instruction: 16 bytes per lane from (voff + soff) to lds_dst + 16 * lane
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_dst, uint32_t voff, uint32_t soff)
+{
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void *)lds_dst, 16, voff, soff, 0, 0);
+}
 
 // Diagnostic ablations (GQ_WGEMM_ABL, a -D of a separate build; 0 in the product): 1 = no
-// weight loads after the prologue, 2 = no activation staging after the prologue, 4 = no MFMA,
-// 8 = no dequantization (raw bits as fp16), 16 = weight loads at 8-byte aligned addresses (wrong
-// values: an access-pattern probe).
+// weight loads after the prologue, 2 = no activation DMA after the prologue, 4 = no MFMA,
+// 8 = no dequantization (raw bits as fp16), 16 / 32 = weight loads at 4- / 16-byte aligned
+// addresses (wrong values: access-pattern probes).
 #ifndef GQ_WGEMM_ABL
 #define GQ_WGEMM_ABL 0
 #endif
 constexpr int ABL = GQ_WGEMM_ABL;
 // weight byte offset as loaded (the alignment probe rounds it down)
-__device__ __forceinline__ uint32_t wo(uint32_t v) { return ABL & 16 ? v & ~7u : v; }
-
+constexpr uint32_t WMASK = ABL & 32 ? ~15u : (ABL & 16 ? ~3u : ~0u);
+__device__ __forceinline__ uint32_t wo(uint32_t v) { return v & WMASK; }
 
 // ---------------------------------------------------------------------------------------
 // One super-block of one 16-row fragment: this lane's bytes (WB<F>::load: back-to-back 16-byte
@@ -111,6 +107,9 @@ template <> struct WB<Q4_K> {
     {
         return 64 * (2 * (s >> 2) + (g >> 1)) + 32 * ((s >> 1) & 1) + 16 * (g & 1) + 8 * (s & 1);
     }
+    // e(2j + kk, g) = base(j) + off(kk, g)
+    static __device__ __forceinline__ int base(int j) { return 128 * (j >> 1) + 32 * (j & 1); }
+    static __device__ __forceinline__ int off(int kk, int g) { return 64 * (g >> 1) + 16 * (g & 1) + 8 * kk; }
     __device__ __forceinline__ f16x8 frag(int s, int g) const
     {
         const int i = s >> 2, nib = (s >> 1) & 1, half = s & 1;
@@ -140,32 +139,55 @@ template <> struct WB<Q4_K> {
 // scales and d.  ql byte 64h + 16g + t (t < 16) holds elements 128h + 32(g>>1) + 16(g&1) + t (low
 // nibble) and +64 (high); its qh bits sit in qh byte 32h + 16(g&1) + t at 2(g>>1) + 4nib.
 // k-step s = 4h + 2nib + half; scale index 8h + 4nib + 2(g>>1) + (g&1) = byte g of word 2h + nib.
+// A 210-byte super-block starts only 2-byte aligned, and 16-byte loads at addresses = 2 mod 4 run
+// at ~3/4 of the aligned rate (measured: profiles/r03/wgemm_align_probe.log): every chunk is
+// loaded from 4-byte aligned `addr - sh` (sh = addr & 2) with one trailing dword, and realigned
+// by v_alignbyte where a word is used; the scales' trailing dword is the one holding d.
 template <> struct WB<Q6_K> {
     static constexpr int SB = 210;
     u32x4 ql[2], qh[2];
-    u32x4 sc;   // the 16 int8 scales
-    uint32_t d; // bytes 206..209: d in the high half
+    uint32_t qle[2], qhe[2]; // the dword after each chunk
+    u32x4 sc;                // the 16 int8 scales
+    uint32_t d;              // bytes 206..209: d in the high half
+    uint32_t sh;             // 0 or 2: the chunks' byte shift
     __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, uint32_t v, int g, uint32_t s0)
     {
-        ql[0] = bl16(r, wo(v + 16 * g), s0);
-        ql[1] = bl16(r, wo(v + 64 + 16 * g), s0);
-        qh[0] = bl16(r, wo(v + 128 + 16 * (g & 1)), s0);
-        qh[1] = bl16(r, wo(v + 160 + 16 * (g & 1)), s0);
-        sc = bl16(r, wo(v + 192), s0);
-        d = bl4(r, wo(v + 206), s0);
+        // (the shift is folded into the per-lane offset: the buffer's range check applies to the
+        // VGPR offset alone, so v - sh must not wrap below 0 at row 0)
+        const uint32_t a = v + s0;
+        sh = a & 2u;
+        const uint32_t vb = a - sh;
+        ql[0] = bl16(r, wo(vb + 16 * g), 0);
+        qle[0] = bl4(r, wo(vb + 16 * g + 16), 0);
+        ql[1] = bl16(r, wo(vb + 64 + 16 * g), 0);
+        qle[1] = bl4(r, wo(vb + 80 + 16 * g), 0);
+        qh[0] = bl16(r, wo(vb + 128 + 16 * (g & 1)), 0);
+        qhe[0] = bl4(r, wo(vb + 144 + 16 * (g & 1)), 0);
+        qh[1] = bl16(r, wo(vb + 160 + 16 * (g & 1)), 0);
+        qhe[1] = bl4(r, wo(vb + 176 + 16 * (g & 1)), 0);
+        sc = bl16(r, wo(vb + 192), 0);
+        d = bl4(r, wo(a + 206), 0);
+    }
+    // word i (0..3) of a chunk loaded sh bytes early, e = the dword after it
+    __device__ __forceinline__ uint32_t word(const u32x4 &q, uint32_t e, int i) const
+    {
+        const uint32_t lo = i == 0 ? q.x : (i == 1 ? q.y : (i == 2 ? q.z : q.w));
+        const uint32_t hi = i == 0 ? q.y : (i == 1 ? q.z : (i == 2 ? q.w : e));
+        return __builtin_amdgcn_alignbyte(hi, lo, sh);
     }
     static __device__ __forceinline__ int e(int s, int g)
     {
         return 128 * (s >> 2) + 64 * ((s >> 1) & 1) + 32 * (g >> 1) + 16 * (g & 1) + 8 * (s & 1);
     }
+    static __device__ __forceinline__ int base(int j) { return 128 * (j >> 1) + 64 * (j & 1); }
+    static __device__ __forceinline__ int off(int kk, int g) { return 32 * (g >> 1) + 16 * (g & 1) + 8 * kk; }
     __device__ __forceinline__ f16x8 frag(int s, int g) const
     {
         const int h = s >> 2, nib = (s >> 1) & 1, half = s & 1;
-        const u32x4 q4 = ql[h], h4 = qh[h];
-        const uint32_t qx = half ? q4.z : q4.x, qy = half ? q4.w : q4.y;
-        const uint32_t hx = half ? h4.z : h4.x, hy = half ? h4.w : h4.y;
+        const uint32_t qx = word(ql[h], qle[h], 2 * half), qy = word(ql[h], qle[h], 2 * half + 1);
+        const uint32_t hx = word(qh[h], qhe[h], 2 * half), hy = word(qh[h], qhe[h], 2 * half + 1);
         const int sq = 2 * (g >> 1) + 4 * nib;
-        const uint32_t sw = (2 * h + nib) == 0 ? sc.x : ((2 * h + nib) == 1 ? sc.y : ((2 * h + nib) == 2 ? sc.z : sc.w));
+        const uint32_t sw = word(sc, d, 2 * h + nib);
         const float scv = (float)(int8_t)((sw >> (8 * g)) & 0xffu);
         const h2 dsc = splat(h2f(d >> 16) * scv);
         const h2 bias = splat(-1056.f); // 1024 + 32
@@ -196,6 +218,8 @@ template <> struct WB<Q8_0> {
         return (k & 3) == 0 ? q.x : ((k & 3) == 1 ? q.y : ((k & 3) == 2 ? q.z : q.w));
     }
     static __device__ __forceinline__ int e(int s, int g) { return 64 * g + 32 * (s >> 2) + 8 * (s & 3); }
+    static __device__ __forceinline__ int base(int j) { return 32 * (j >> 1) + 16 * (j & 1); }
+    static __device__ __forceinline__ int off(int kk, int g) { return 64 * g + 8 * kk; }
     __device__ __forceinline__ f16x8 frag(int s, int) const
     {
         const int blk = s >> 2, p = s & 3;
@@ -218,26 +242,26 @@ template <> struct WB<Q8_0> {
 };
 
 // ---------------------------------------------------------------------------------------
-// LDS: two activation slots of one super-block, [k-step s][token n][4 lane groups x 16 bytes]
-// (64 bytes per token and k-step); lane group g's piece stored at g ^ kF[(n >> 2) & 3]: the
-// 16-lane groups of a ds_read_b128 then hit 16 distinct 16-byte bank slots.
-__device__ __forceinline__ int swz(int g, int n)
-{
-    constexpr uint32_t kF = 0x1320u; // F = {0, 2, 3, 1}
-    return g ^ (int)((kF >> (4 * ((n >> 2) & 3))) & 3u);
-}
+// Activation ring: R slots of one sub-stage (64 K elements = k-steps 2j, 2j+1 of super-block
+// sb): per token 128 bytes = 8 pieces, piece kk*4 + g (the 8 activations lane group g reads at
+// k-step 2j + kk) stored at position piece ^ swz8(token): a ds_read_b128's 16-lane groups then
+// hit 16 distinct 16-byte bank slots.  A DMA instruction fills 1 KiB = 8 tokens' rows (lane l:
+// token l>>3, position l&7), its per-lane source address picking the piece.
+__device__ __forceinline__ int swz8(int n) { return (n >> 1) & 7; }
 
-template <int F, int RG, int NB>
+template <int NWC, int NB>
 struct WCfg {
-    static constexpr int BM = 16 * NWAVE * RG, BN = 16 * NB;
-    static constexpr int SLOT = BN * 512; // one super-block of BN tokens
-    static constexpr int LDS_BYTES = 2 * SLOT;
-    // activation staging: BN * 32 pieces of 16 bytes per super-block, NQ per thread (each thread
-    // an equal share: a conditional store would let the compiler sink its loads); BN = 16: 8-byte
-    // halves of pieces
-    static constexpr int U = BN >= 32 ? 16 : 8;
-    static constexpr int NQ = BN * 512 / THREADS / U;
-    static_assert(NQ >= 1 && NQ * U * THREADS == BN * 512, "whole staging passes");
+    static constexpr int BN = 16 * NB;
+    static constexpr int SLOT = BN * 128;
+    static constexpr int DMA_SUB = SLOT / 1024;                                    // DMA instructions per sub-stage
+    static constexpr int DPL = DMA_SUB >= NL ? DMA_SUB / NL : 1;                   // per loader wave
+    static constexpr int L = NB >= 8 ? 6 : 8;                                      // sub-stages in flight
+    static constexpr int R = L + 2;                                                // ring slots
+    static constexpr int LDS_BYTES = R * SLOT;
+    static constexpr int THREADS = 64 * (NWC + NL);
+    static_assert(DMA_SUB % NL == 0 || DMA_SUB < NL, "loader share");
+    static_assert((L - 1) * DPL <= 63, "vmcnt range");
+    static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 };
 
 // Block -> (tile, split): the S splits of tile t run on XCD t % 8 when the tile count is a
@@ -255,34 +279,75 @@ __device__ __forceinline__ void block_map(int b, int ntiles, int S, int &tile, i
     }
 }
 
+// s_waitcnt vmcnt(n) for a compile-time n
+template <int n> __device__ __forceinline__ void vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n) : "memory"); }
+
 // P (S > 1): fp16 partials per (tile, split) block in accumulator order -- unit
-// q = ((wr*(NB/2) + u)*64 + lane) (wr = RG*wave + rf) holds token tiles 2u, 2u+1 of the lane's 4
-// rows, scaled by 2^-e (e per (block, wave), ints after all the blocks); NB = 1: 8-byte units of
-// one token tile.  wreduce_kernel sums them.
-template <int F, int RG, int NB>
-__global__ __launch_bounds__(THREADS) void wgemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
-                                                       uint16_t *__restrict__ C, uint16_t *__restrict__ P, int M, int N,
-                                                       int K, int ldc, int tiles_m, int S, int sb_per_split)
+// q = ((wr*(NB/2) + u)*64 + lane) (wr = RG*wave + rf, wave < NWC) holds token tiles 2u, 2u+1 of
+// the lane's 4 rows, scaled by 2^-e (e per (block, compute wave), ints after all the blocks).
+// wreduce_kernel sums them.
+template <int F, int NWC, int RG, int NB, int WD>
+__global__ __launch_bounds__(64 * (NWC + NL)) void wgemm_kernel(
+    const uint8_t *__restrict__ A, const uint16_t *__restrict__ X, uint16_t *__restrict__ C, uint16_t *__restrict__ P,
+    int M, int N, int K, int ldc, int tiles_m, int S, int sb_per_split)
 {
-    using G = WCfg<F, RG, NB>;
+    using G = WCfg<NWC, NB>;
     using W = WB<F>;
+    constexpr int BM = 16 * NWC * RG, BN = G::BN;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[G::LDS_BYTES];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int g = lane >> 4, c = lane & 15;
     int tile, sp;
     block_map(blockIdx.x, (int)gridDim.x / S, S, tile, sp);
     const int tm = tile % tiles_m, tn = tile / tiles_m;
-    const int m0 = tm * G::BM, n0 = tn * G::BN;
+    const int m0 = tm * BM, n0 = tn * BN;
     const int nsb = K / 256;
     const int sb0 = sp * sb_per_split;
     const int sb1 = sb0 + sb_per_split < nsb ? sb0 + sb_per_split : nsb;
+    const int nsub = 4 * (sb1 - sb0);
+
+    if (wave >= NWC) {
+        // ---- loader wave: the ring of activation sub-stages, DMA only ----
+        if (nsub <= 0) return;
+        const int lw = wave - NWC;
+        const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, N * K * 2, 0x00020000);
+        // instruction i of this wave: DMA k = lw + NL*i (BN = 16: waves 2, 3 repeat 0, 1's -- same
+        // bytes to the same place); lane: token 8k + (lane>>3), position lane&7
+        uint32_t xv[G::DPL];
+        int kd[G::DPL];
+#pragma unroll
+        for (int i = 0; i < G::DPL; ++i) {
+            const int k = G::DMA_SUB >= NL ? lw + NL * i : lw % G::DMA_SUB;
+            const int n = 8 * k + (lane >> 3), pc = (lane & 7) ^ swz8(n);
+            const int tok = n0 + n < N ? n0 + n : N - 1;
+            xv[i] = (uint32_t)tok * (uint32_t)K * 2u + 2u * (uint32_t)W::off(pc >> 2, pc & 3);
+            kd[i] = 1024 * k;
+        }
+        auto issue = [&](int a) { // sub-stage a (clamped source) into slot a % R
+            const int ac = a < nsub ? a : nsub - 1;
+            const uint32_t so = 2u * (uint32_t)(256 * (sb0 + (ac >> 2)) + W::base(ac & 3));
+            uint8_t *dst = lds + (a % G::R) * G::SLOT;
+#pragma unroll
+            for (int i = 0; i < G::DPL; ++i) {
+                if constexpr (!(ABL & 2)) dma16(xrs, dst + kd[i], xv[i], so);
+            }
+        };
+#pragma unroll
+        for (int a = 0; a < G::L; ++a) issue(a);
+        for (int a = 0; a < nsub; ++a) {
+            if constexpr (ABL & 2) asm volatile("s_barrier" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((G::L - 1) * G::DPL) : "memory"); // sub-stage a landed
+            issue(a + G::L); // into the slot of sub-stage a + L - R = a - 2: read before the last barrier
+        }
+        vmcnt<0>(); // no DMA may land after the workgroup exits
+        return;
+    }
+
+    // ---- compute wave ----
+    const int g = lane >> 4, c = lane & 15;
     const int row_bytes = (K / Layout<F>::QK) * Layout<F>::BYTES;
-
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, M * row_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, N * K * 2, 0x00020000);
-
     // this lane's weight rows (clamped: rows past M compute garbage that is never stored)
     uint32_t wv[RG];
 #pragma unroll
@@ -290,72 +355,35 @@ __global__ __launch_bounds__(THREADS) void wgemm_kernel(const uint8_t *__restric
         const int row = m0 + 16 * (RG * wave + rf) + c;
         wv[rf] = (uint32_t)((row < M ? row : M - 1) * row_bytes);
     }
-    // activation staging: pass q moves piece (half) i = q*THREADS + tid: token i / 32, natural
-    // piece P = i % 32 of the super-block (U = 8: i / 64, piece (i % 64) / 2, half i % 2), to the
-    // LDS position of the (k-step, lane group) that multiplies it
-    uint32_t xv[G::NQ];
-    int xd[G::NQ];
-#pragma unroll
-    for (int q = 0; q < G::NQ; ++q) {
-        const int i = q * THREADS + tid;
-        const int per = 32 * 16 / G::U; // units per token
-        const int n = i / per, u = i % per, Pc = u * G::U / 16, b = u * G::U % 16;
-        const int tok = n0 + n < N ? n0 + n : N - 1;
-        xv[q] = (uint32_t)tok * (uint32_t)K * 2u + 16u * (uint32_t)Pc + (uint32_t)b;
-        int ks = 0, kg = 0; // the (k-step, lane group) whose e(s, g) is piece Pc
-#pragma unroll
-        for (int s = 0; s < 8; ++s)
-#pragma unroll
-            for (int gg = 0; gg < 4; ++gg)
-                if (W::e(s, gg) == 8 * Pc) ks = s, kg = gg;
-        xd[q] = ks * (G::BN * 64) + n * 64 + 16 * swz(kg, n) + b;
-    }
-
     f32x4 acc[RG][NB];
 #pragma unroll
     for (int rf = 0; rf < RG; ++rf)
 #pragma unroll
         for (int t = 0; t < NB; ++t) acc[rf][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-    if (sb1 > sb0) {
-        using XU = typename std::conditional<G::U == 16, u32x4, u32x2>::type;
-        W wb[2][RG]; // super-block double buffer
-        XU xs[G::NQ];
-        auto load_w = [&](int b, int sb) { // super-block sb (clamped) into buffer b
-            const uint32_t s0 = (uint32_t)((sb < sb1 ? sb : sb1 - 1) * W::SB) & (ABL & 16 ? ~7u : ~0u);
+    if (nsub > 0) {
+        W wb[WD][RG]; // super-block ring: WD - 1 super-blocks of weights in flight
+        auto load_w = [&](int b, int sb) { // super-block sb (clamped: surplus re-reads hit the cache)
+            const uint32_t s0 = (uint32_t)((sb < sb1 ? sb : sb1 - 1) * W::SB) & WMASK;
 #pragma unroll
             for (int rf = 0; rf < RG; ++rf) wb[b][rf].load(wrs, wv[rf], g, s0);
         };
-        auto load_x = [&](int sb) { // super-block sb (clamped) of the tile's tokens
-            const uint32_t so = 512u * (uint32_t)(sb < sb1 ? sb : sb1 - 1);
-#pragma unroll
-            for (int q = 0; q < G::NQ; ++q) {
-                if constexpr (G::U == 16) xs[q] = bl16(xrs, xv[q], so);
-                else xs[q] = bl8(xrs, xv[q], so);
-            }
-        };
-        auto store_x = [&](int slot) {
-#pragma unroll
-            for (int q = 0; q < G::NQ; ++q) *(XU *)(lds + slot * G::SLOT + xd[q]) = xs[q];
-        };
-        auto barrier = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-        auto pin = [] { __builtin_amdgcn_sched_barrier(0); };
-        // multiply one super-block: weights from buffer b, activations from LDS slot `slot`
-        auto compute = [&](int b, int slot) {
+        // multiply sub-stage j (k-steps 2j, 2j+1) of the super-block in buffer b from ring slot `slot`
+        auto compute = [&](int b, int j, int slot) {
             const uint8_t *xsl = lds + slot * G::SLOT;
 #pragma unroll
-            for (int s = 0; s < 8; ++s) {
+            for (int kk = 0; kk < 2; ++kk) {
                 f16x8 bf[NB];
 #pragma unroll
                 for (int t = 0; t < NB; ++t) {
                     const int n = 16 * t + c;
-                    bf[t] = *(const f16x8 *)(xsl + s * (G::BN * 64) + n * 64 + 16 * swz(g, n));
+                    bf[t] = *(const f16x8 *)(xsl + n * 128 + 16 * ((4 * kk + g) ^ swz8(n)));
                 }
                 f16x8 af[RG];
 #pragma unroll
                 for (int rf = 0; rf < RG; ++rf) {
-                    if constexpr (ABL & 8) af[rf] = __builtin_bit_cast(f16x8, (u32x4){wv[rf], wv[rf] + 1u, (uint32_t)s, 5u});
-                    else af[rf] = wb[b][rf].frag(s, g);
+                    if constexpr (ABL & 8) af[rf] = __builtin_bit_cast(f16x8, (u32x4){wv[rf], wv[rf] + 1u, (uint32_t)j, 5u});
+                    else af[rf] = wb[b][rf].frag(2 * j + kk, g);
                 }
 #pragma unroll
                 for (int rf = 0; rf < RG; ++rf)
@@ -366,48 +394,45 @@ __global__ __launch_bounds__(THREADS) void wgemm_kernel(const uint8_t *__restric
                     }
             }
         };
-
-        // Super-block i (buffer i & 1, LDS slot i & 1): multiply; ds_write the activations of
-        // i + 1 (loaded one super-block ago); load the activations of i + 2, then the weights of
-        // i + 2 into buffer i & 1; barrier.  Issue order is what matters to the in-order vmcnt
-        // queue: each activation load is issued BEFORE the weight burst of its super-block, so
-        // waiting for it never waits for HBM weight bytes younger than one super-block, and every
-        // stream has a full super-block of lead.  The prologue issues the same sequence (X, W, X,
-        // W), so the compiler's counts at the loop head agree on both paths.  Every load is
-        // unconditional (indices clamped: surplus re-reads hit the cache) -- a load under a
-        // condition makes the count at the merge the smaller one, i.e. a drain.
-        load_x(sb0);
-        pin();
-        load_w(0, sb0);
-        pin();
-        store_x(0);
-        load_x(sb0 + 1);
-        pin();
-        load_w(1, sb0 + 1);
-        barrier();
-        auto body = [&](int sb, int b) {
-            compute(b, b);
-            pin();
-            if constexpr (!(ABL & 2)) store_x(b ^ 1); // (past the end: a slot nobody reads)
-            if constexpr (!(ABL & 2)) load_x(sb + 2);
-            pin();
-            if constexpr (!(ABL & 1)) load_w(b, sb + 2);
-            barrier();
+        // (sched_barrier on both sides: register-only work -- the dequantization -- would otherwise
+        // be hoisted across the asm barrier to the loop head, where it waits for the weight loads
+        // just issued)
+        auto barrier = [] {
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
         };
-        // pairs in the loop (static buffer parity), an odd last super-block after it: the loop's
-        // back edge always follows the same two bodies
+        // Super-block i (buffer i % WD): 4 sub-stages (barrier: the loaders' sub-stage landed; then
+        // multiply), then its buffer is refilled with super-block i + WD -- the weights have WD - 1
+        // super-blocks of lead and are the only loads in this wave's queue.  WD bodies per loop
+        // iteration (static buffer indices), the last < WD super-blocks after it, so the loop's back
+        // edge always follows the same code.
+        auto body = [&](int sb, int b) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int a = 4 * (sb - sb0) + j;
+                barrier();
+                compute(b, j, a % G::R);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (!(ABL & 1)) load_w(b, sb + WD);
+        };
+#pragma unroll
+        for (int b = 0; b < WD; ++b) load_w(b, sb0 + b);
         int sb = sb0;
-        for (; sb + 1 < sb1; sb += 2) {
-            body(sb, 0);
-            body(sb + 1, 1);
+        for (; sb + WD - 1 < sb1; sb += WD) {
+#pragma unroll
+            for (int b = 0; b < WD; ++b) body(sb + b, b);
         }
-        if (sb < sb1) body(sb, 0);
+#pragma unroll
+        for (int b = 0; b < WD - 1; ++b)
+            if (sb + b < sb1) body(sb + b, b);
     }
 
     // epilogue: acc[rf][t][i] = D[row 16*(RG*wave + rf) + 4g + i][token 16t + c]
     if (S > 1) {
         const int bidx = tile * S + sp;
-        uint16_t *hb = P + (size_t)bidx * (G::BM * G::BN);
+        uint16_t *hb = P + (size_t)bidx * (BM * BN);
         float mx = 0.f;
 #pragma unroll
         for (int rf = 0; rf < RG; ++rf)
@@ -428,21 +453,17 @@ __global__ __launch_bounds__(THREADS) void wgemm_kernel(const uint8_t *__restric
         const int e = E - 14 > 0 ? (E - 14 < 127 ? E - 14 : 126) : 0;
         const float down = __builtin_bit_cast(float, (uint32_t)(127 - e) << 23);
         const int nblk = (int)gridDim.x;
-        if (lane == 0) ((int *)(P + (size_t)nblk * (G::BM * G::BN)))[bidx * NWAVE + wave] = e;
+        if (lane == 0) ((int *)(P + (size_t)nblk * (BM * BN)))[bidx * NWC + wave] = e;
         auto pk = [down](const f32x4 &v) {
             return (u32x2){(uint32_t)f2h_bits(v[0] * down) | ((uint32_t)f2h_bits(v[1] * down) << 16),
                            (uint32_t)f2h_bits(v[2] * down) | ((uint32_t)f2h_bits(v[3] * down) << 16)};
         };
 #pragma unroll
         for (int rf = 0; rf < RG; ++rf) {
-            if constexpr (NB == 1) {
-                ((u32x2 *)hb)[(RG * wave + rf) * 64 + lane] = pk(acc[rf][0]);
-            } else {
 #pragma unroll
-                for (int u = 0; u < NB / 2; ++u) {
-                    const u32x2 lo = pk(acc[rf][2 * u]), hi = pk(acc[rf][2 * u + 1]);
-                    ((u32x4 *)hb)[((RG * wave + rf) * (NB / 2) + u) * 64 + lane] = (u32x4){lo.x, lo.y, hi.x, hi.y};
-                }
+            for (int u = 0; u < NB / 2; ++u) {
+                const u32x2 lo = pk(acc[rf][2 * u]), hi = pk(acc[rf][2 * u + 1]);
+                ((u32x4 *)hb)[((RG * wave + rf) * (NB / 2) + u) * 64 + lane] = (u32x4){lo.x, lo.y, hi.x, hi.y};
             }
         }
         return;
@@ -467,17 +488,16 @@ __global__ __launch_bounds__(THREADS) void wgemm_kernel(const uint8_t *__restric
     }
 }
 
-// C = fp16(sum_s 2^e_s * partial_s) in split order (deterministic), one thread per 16-byte
-// unit (two token tiles of a lane's 4 rows; NB = 1: one 8-byte unit), every split's load issued
-// before the first add.  Reduce block b takes a tile of XCD b % 8 when the tile count allows it
-// (block_map's placement), so the partials are read from the L2 that holds them.
-template <int RG, int NB>
+// C = fp16(sum_s 2^e_s * partial_s) in split order (deterministic), one thread per 16-byte unit
+// (two token tiles of a lane's 4 rows), every split's load issued before the first add.  Reduce
+// block b takes a tile of XCD b % 8 when the tile count allows it (block_map's placement), so
+// the partials are read from the L2 that holds them.
+template <int NWC, int RG, int NB>
 __global__ __launch_bounds__(256) void wreduce_kernel(const uint16_t *__restrict__ P, uint16_t *__restrict__ C, int M,
                                                       int N, int ldc, int S, int tiles_m, int ntiles)
 {
-    constexpr int TPU = NB == 1 ? 1 : 2;
-    constexpr int UNITS = NWAVE * RG * (NB / TPU) * 64; // per tile block
-    constexpr int BPT = (UNITS + 255) / 256;            // reduce blocks per tile
+    constexpr int UNITS = NWC * RG * (NB / 2) * 64; // per tile block
+    constexpr int BPT = (UNITS + 255) / 256;        // reduce blocks per tile
     int tile, chunk;
     if (ntiles % 8 == 0) {
         const int i = blockIdx.x >> 3;
@@ -489,32 +509,27 @@ __global__ __launch_bounds__(256) void wreduce_kernel(const uint16_t *__restrict
     }
     const int q = chunk * 256 + threadIdx.x;
     if (tile >= ntiles || q >= UNITS) return;
-    const int lane = q & 63, u = (q >> 6) % (NB / TPU), wr = (q >> 6) / (NB / TPU);
+    const int lane = q & 63, u = (q >> 6) % (NB / 2), wr = (q >> 6) / (NB / 2);
     const int wv = wr / RG;
-    constexpr int BLK = NWAVE * RG * 16 * 16 * NB; // halves per block
+    constexpr int BLK = NWC * RG * 16 * 16 * NB; // halves per block
     const int *es = (const int *)(P + (size_t)ntiles * S * BLK);
-    f32x4 acc[TPU];
+    f32x4 acc[2];
 #pragma unroll
-    for (int j = 0; j < TPU; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 2; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     for (int s0 = 0; s0 < S; s0 += 8) {
         u32x4 v[8];
         float up[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int sp = tile * S + (s0 + i < S ? s0 + i : S - 1); // unconditional loads
-            if constexpr (TPU == 2) {
-                v[i] = ((const u32x4 *)(P + (size_t)sp * BLK))[q];
-            } else {
-                const u32x2 w = ((const u32x2 *)(P + (size_t)sp * BLK))[q];
-                v[i] = (u32x4){w.x, w.y, 0u, 0u};
-            }
-            up[i] = __builtin_bit_cast(float, (uint32_t)(127 + es[sp * NWAVE + wv]) << 23);
+            v[i] = ((const u32x4 *)(P + (size_t)sp * BLK))[q];
+            up[i] = __builtin_bit_cast(float, (uint32_t)(127 + es[sp * NWC + wv]) << 23);
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             if (s0 + i >= S) break;
 #pragma unroll
-            for (int j = 0; j < TPU; ++j) {
+            for (int j = 0; j < 2; ++j) {
                 const uint32_t lo = j ? v[i].z : v[i].x, hi = j ? v[i].w : v[i].y;
                 acc[j][0] += h2f(lo & 0xffffu) * up[i];
                 acc[j][1] += h2f(lo >> 16) * up[i];
@@ -524,11 +539,11 @@ __global__ __launch_bounds__(256) void wreduce_kernel(const uint16_t *__restrict
         }
     }
     const int tm = tile % tiles_m, tn = tile / tiles_m;
-    const int row = tm * (16 * NWAVE * RG) + 16 * wr + 4 * (lane >> 4);
+    const int row = tm * (16 * NWC * RG) + 16 * wr + 4 * (lane >> 4);
     if (row >= M) return;
 #pragma unroll
-    for (int j = 0; j < TPU; ++j) {
-        const int tok = tn * 16 * NB + 16 * (TPU * u + j) + (lane & 15);
+    for (int j = 0; j < 2; ++j) {
+        const int tok = tn * 16 * NB + 16 * (2 * u + j) + (lane & 15);
         if (tok >= N) continue;
         uint16_t *dst = C + (size_t)tok * ldc + row;
         if (row + 4 <= M) {
@@ -540,38 +555,62 @@ __global__ __launch_bounds__(256) void wreduce_kernel(const uint16_t *__restrict
     }
 }
 
-template <int F, int RG, int NB>
+template <int F, int NWC, int RG, int NB>
 hipError_t launch_cfg(const uint8_t *A, const uint16_t *X, uint16_t *C, uint16_t *P, const WGemmPlan &pl, int64_t M,
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
+    using G = WCfg<NWC, NB>;
     const int ntiles = pl.tiles_m * pl.tiles_n;
-    wgemm_kernel<F, RG, NB><<<dim3((unsigned)(ntiles * pl.splits)), dim3(THREADS), 0, s>>>(
-        A, X, C, P, (int)M, (int)N, (int)K, (int)ldc, pl.tiles_m, pl.splits, pl.sb_per_split);
+    const dim3 grid((unsigned)(ntiles * pl.splits)), block(G::THREADS);
+    // weight super-blocks in registers: 4 only for the one-fragment waves, 3 except where it
+    // would spill (Q6_K, two fragments x 8 column blocks)
+    constexpr bool wd4 = NWC == 8, wd3 = !(F == Q6_K && RG == 2 && NB == 8);
+    const int wd = pl.wd == 4 && !wd4 ? 3 : pl.wd;
+    bool done = false;
+    if constexpr (wd4) {
+        if (wd == 4) {
+            wgemm_kernel<F, NWC, RG, NB, 4><<<grid, block, 0, s>>>(A, X, C, P, (int)M, (int)N, (int)K, (int)ldc,
+                                                                  pl.tiles_m, pl.splits, pl.sb_per_split);
+            done = true;
+        }
+    }
+    if constexpr (wd3) {
+        if (!done && wd == 3) {
+            wgemm_kernel<F, NWC, RG, NB, 3><<<grid, block, 0, s>>>(A, X, C, P, (int)M, (int)N, (int)K, (int)ldc,
+                                                                  pl.tiles_m, pl.splits, pl.sb_per_split);
+            done = true;
+        }
+    }
+    if (!done)
+        wgemm_kernel<F, NWC, RG, NB, 2><<<grid, block, 0, s>>>(A, X, C, P, (int)M, (int)N, (int)K, (int)ldc, pl.tiles_m,
+                                                              pl.splits, pl.sb_per_split);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || pl.splits == 1) return e;
-    constexpr int TPU = NB == 1 ? 1 : 2;
-    constexpr int UNITS = NWAVE * RG * (NB / TPU) * 64, BPT = (UNITS + 255) / 256;
-    wreduce_kernel<RG, NB><<<dim3((unsigned)(ntiles * BPT)), dim3(256), 0, s>>>(P, C, (int)M, (int)N, (int)ldc,
-                                                                               pl.splits, pl.tiles_m, ntiles);
+    constexpr int UNITS = NWC * RG * (NB / 2) * 64, BPT = (UNITS + 255) / 256;
+    wreduce_kernel<NWC, RG, NB><<<dim3((unsigned)(ntiles * BPT)), dim3(256), 0, s>>>(P, C, (int)M, (int)N, (int)ldc,
+                                                                                    pl.splits, pl.tiles_m, ntiles);
     return hipGetLastError();
+}
+
+template <int F, int NWC, int RG>
+hipError_t launch_nb(const uint8_t *A, const uint16_t *X, uint16_t *C, uint16_t *P, const WGemmPlan &pl, int64_t M,
+                     int64_t N, int64_t K, int64_t ldc, hipStream_t s)
+{
+    switch (pl.nb) {
+    case 2: return launch_cfg<F, NWC, RG, 2>(A, X, C, P, pl, M, N, K, ldc, s);
+    case 4: return launch_cfg<F, NWC, RG, 4>(A, X, C, P, pl, M, N, K, ldc, s);
+    case 8: return launch_cfg<F, NWC, RG, 8>(A, X, C, P, pl, M, N, K, ldc, s);
+    default: return hipErrorInvalidValue;
+    }
 }
 
 template <int F>
 hipError_t launch_fmt(const uint8_t *A, const uint16_t *X, uint16_t *C, uint16_t *P, const WGemmPlan &pl, int64_t M,
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
-    if (pl.rg == 1) switch (pl.nb) {
-        case 2: return launch_cfg<F, 1, 2>(A, X, C, P, pl, M, N, K, ldc, s);
-        case 4: return launch_cfg<F, 1, 4>(A, X, C, P, pl, M, N, K, ldc, s);
-        case 8: return launch_cfg<F, 1, 8>(A, X, C, P, pl, M, N, K, ldc, s);
-        default: return hipErrorInvalidValue;
-        }
-    switch (pl.nb) {
-    case 2: return launch_cfg<F, 2, 2>(A, X, C, P, pl, M, N, K, ldc, s);
-    case 4: return launch_cfg<F, 2, 4>(A, X, C, P, pl, M, N, K, ldc, s);
-    case 8: return launch_cfg<F, 2, 8>(A, X, C, P, pl, M, N, K, ldc, s);
-    default: return hipErrorInvalidValue;
-    }
+    // (rg, compute waves): (2, 4) = 128 rows, one compute wave per SIMD; (1, 8) = 128 rows, two
+    if (pl.rg == 1) return launch_nb<F, 8, 1>(A, X, C, P, pl, M, N, K, ldc, s);
+    return launch_nb<F, 4, 2>(A, X, C, P, pl, M, N, K, ldc, s);
 }
 
 } // namespace
@@ -582,7 +621,7 @@ WGemmPlan plan_wgemm(int fmt, int64_t M, int64_t N, int64_t K, int rg, int nb, i
     (void)fmt;
     p.rg = rg == 1 ? 1 : 2;
     p.nb = nb == 2 || nb == 4 ? nb : 8;
-    const int64_t bm = 16 * NWAVE * p.rg, bn = 16 * p.nb;
+    const int64_t bm = 128, bn = 16 * p.nb; // both (rg, waves) shapes are 128 rows
     p.tiles_m = (int)((M + bm - 1) / bm);
     p.tiles_n = (int)((N + bn - 1) / bn);
     const int64_t nsb = K / 256, tiles = (int64_t)p.tiles_m * p.tiles_n;
@@ -593,7 +632,7 @@ WGemmPlan plan_wgemm(int fmt, int64_t M, int64_t N, int64_t K, int rg, int nb, i
     S = (nsb + sps - 1) / sps;
     p.splits = (int)S;
     p.sb_per_split = (int)sps;
-    p.partial_bytes = S > 1 ? (size_t)S * tiles * bm * bn * 2 + (size_t)S * tiles * NWAVE * sizeof(int) : 0;
+    p.partial_bytes = S > 1 ? (size_t)S * tiles * bm * bn * 2 + (size_t)S * tiles * 8 * sizeof(int) : 0;
     return p;
 }
 

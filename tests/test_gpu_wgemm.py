@@ -1,6 +1,6 @@
 """GPU parity of the weight-register GEMM (csrc/mmq_wgemm.hip, the 33+-token path) against the
-oracle, over its whole configuration space: tile shapes (RG 1/2 x NB 2/4/8), split-K factors, ragged rows/tokens, the split-K partial range, row
-independence.  Tolerance: TIGHT_GEMM (fp16 W x fp16 x~ on fp32 MFMA) vs oracle IDEAL, and the
+oracle, over its whole configuration space: tile shapes (RG 1/2 x NB 2/4/8), weight ring depths
+(WD 2/3/4), split-K factors, ragged rows/tokens, the split-K partial range, row independence.  Tolerance: TIGHT_GEMM (fp16 W x fp16 x~ on fp32 MFMA) vs oracle IDEAL, and the
 reference's own 1% gate vs oracle EXACT (kernels/cpu_impls arithmetic)."""
 import numpy as np
 import pytest
@@ -30,11 +30,12 @@ def _run(fmt, qA, B, M, N, K):
 
 
 @pytest.mark.parametrize("fmt", FMTS)
-@pytest.mark.parametrize("rg,nb", [(2, 8), (1, 8), (2, 4), (1, 4), (2, 2), (1, 2)])
+@pytest.mark.parametrize("rg,nb,wd", [(1, 8, 4), (1, 8, 3), (1, 8, 2), (1, 4, 4), (1, 2, 4), (2, 8, 2), (2, 8, 3),
+                                       (2, 4, 3), (2, 2, 2)])
 @pytest.mark.parametrize("M,N,K,splits", [(300, 128, 1024, 0), (257, 100, 768, 3), (64, 200, 512, 1),
                                           (1000, 48, 2048, 0), (130, 33, 256, 0), (520, 256, 1024, 2)])
-def test_wgemm_configs(fmt, rg, nb, M, N, K, splits, tune):
-    tune(GQ_WGEMM=1, GQ_WGEMM_RG=rg, GQ_WGEMM_NB=nb, GQ_WGEMM_SPLITS=splits)
+def test_wgemm_configs(fmt, rg, nb, wd, M, N, K, splits, tune):
+    tune(GQ_WGEMM=1, GQ_WGEMM_RG=rg, GQ_WGEMM_NB=nb, GQ_WGEMM_WD=wd, GQ_WGEMM_SPLITS=splits)
     qA = random_blocks(fmt, M, K, seed=M + N + K)
     B = random_activations(N, K, seed=K + 3 * N)
     got = _run(fmt, qA, B, M, N, K)
@@ -47,12 +48,13 @@ def test_wgemm_configs(fmt, rg, nb, M, N, K, splits, tune):
 
 @pytest.mark.parametrize("fmt", FMTS)
 def test_wgemm_golden(golden, fmt, tune):
-    """Every golden case of the reference with 33+ tokens and K % 256 == 0 through the kernel."""
+    """Every golden case of the reference with K % 256 == 0, its GEMM-routed ones (5+ tokens)
+    through the kernel (forced on: the fixtures hold at most 16 tokens)."""
     tune(GQ_WGEMM=1)
     n = 0
     for c in golden[fmt]:
         M, N, K = c["M"], c["N"], c["K"]
-        if N < 33 or K % 256:
+        if K % 256:
             continue
         got = _run(fmt, c["qA"], c["B"], M, N, K)
         ideal = O.mmq(fmt, c["qA"], c["qB"], M, N, K, O.IDEAL)

@@ -29,7 +29,7 @@ def parity(dev, quick):
     from utils.synth import random_activations, random_blocks
     shapes = [(130, 33, 256), (200, 64, 512), (257, 100, 768), (300, 128, 1024), (64, 200, 512), (1000, 48, 2048),
               (520, 256, 1024)]
-    cfgs = [dict(GQ_WGEMM=1)] + ([] if quick else [dict(GQ_WGEMM=1, GQ_WGEMM_RG=1), dict(GQ_WGEMM=1, GQ_WGEMM_NB=2),
+    cfgs = [dict(GQ_WGEMM=1), dict(GQ_WGEMM=1, GQ_WGEMM_RG=1)] + ([] if quick else [dict(GQ_WGEMM=1, GQ_WGEMM_NB=2),
                                                    dict(GQ_WGEMM=1, GQ_WGEMM_NB=4, GQ_WGEMM_SPLITS=3),
                                                    dict(GQ_WGEMM=1, GQ_WGEMM_SPLITS=1),
                                                    dict(GQ_WGEMM=1, GQ_WGEMM_RG=2, GQ_WGEMM_NB=8, GQ_WGEMM_SPLITS=2)])
@@ -132,6 +132,11 @@ CONFIGS = {
     "q6_k_8192x28672_m128": ("q6_k", 8192, 28672, 128),
     "q4_k_4096x4096_m64": ("q4_k", 4096, 4096, 64),
     "q4_k_4096x4096_m256": ("q4_k", 4096, 4096, 256),
+    "q4_k_4096x4096_m40": ("q4_k", 4096, 4096, 40),
+    "q8_0_4096x4096_m64": ("q8_0", 4096, 4096, 64),
+    "q8_0_4096x4096_m256": ("q8_0", 4096, 4096, 256),
+    "q8_0_4096x4096_m512": ("q8_0", 4096, 4096, 512),
+    "q4_k_11008x4096_m512": ("q4_k", 11008, 4096, 512),
 }
 
 
@@ -145,6 +150,12 @@ VARIANTS = {
     "w_rg2_nb4_s4": dict(GQ_WGEMM=1, GQ_WGEMM_RG=2, GQ_WGEMM_NB=4, GQ_WGEMM_SPLITS=4),
     "w_rg2_nb4_s8": dict(GQ_WGEMM=1, GQ_WGEMM_RG=2, GQ_WGEMM_NB=4, GQ_WGEMM_SPLITS=8),
     "w_rg1_nb8_s4": dict(GQ_WGEMM=1, GQ_WGEMM_RG=1, GQ_WGEMM_NB=8, GQ_WGEMM_SPLITS=4),
+    "w_rg1_nb8_wd3": dict(GQ_WGEMM=1, GQ_WGEMM_RG=1, GQ_WGEMM_NB=8, GQ_WGEMM_WD=3),
+    "w_rg1_nb8_wd4": dict(GQ_WGEMM=1, GQ_WGEMM_RG=1, GQ_WGEMM_NB=8, GQ_WGEMM_WD=4),
+    "w_rg2_nb8_wd3": dict(GQ_WGEMM=1, GQ_WGEMM_RG=2, GQ_WGEMM_NB=8, GQ_WGEMM_WD=3),
+    "w_rg1_nb4_wd4": dict(GQ_WGEMM=1, GQ_WGEMM_RG=1, GQ_WGEMM_NB=4, GQ_WGEMM_WD=4),
+    "w_rg1_nb2_wd4": dict(GQ_WGEMM=1, GQ_WGEMM_RG=1, GQ_WGEMM_NB=2, GQ_WGEMM_WD=4),
+    "w_rg1_wd4": dict(GQ_WGEMM=1, GQ_WGEMM_RG=1, GQ_WGEMM_WD=4),
 }
 
 
