@@ -185,18 +185,21 @@ int64_t gemm_toks_per_launch(int64_t N, int64_t K)
     return n < 16 ? 16 : (n < N ? n : N);
 }
 
-// Weight-register GEMM (mmq_wgemm.hip) for the fp16 form (GQ_WGEMM forces it on / off).  By
-// default only where it measured faster than the LDS-DMA GEMM (graph-timed, profiles/r03/
-// wgemm_ab_final.log): Q4_K with 8192+ rows (11008x4096: x128 30.6 vs 35.1 us, x512 86.2 vs
-// 93.9).  Elsewhere it is level or slower (4096^2 x128: Q8_0 20.8 vs 17.3, Q4_K 15.6 vs 15.4;
-// Q6_K 28672x8192 x128 115.6 vs 111.9), so those stay on the LDS-DMA GEMM.
-constexpr int64_t kWgemmMinTokens = 33, kWgemmMinRows = 8192;
-bool use_wgemm(int t, int form, int64_t M, int64_t N)
+// Weight-register GEMM (mmq_wgemm.hip) for the fp16 form (GQ_WGEMM forces it on / off).  The
+// choice depends on the type and the token count only -- never on the row count, so a row
+// subset (a shard) runs the same arithmetic as the whole matrix (bit-identical rows).  By
+// default Q4_K from 33 tokens on, where it measured level or faster than the LDS-DMA GEMM
+// (graph-timed, profiles/r03/wgemm_ab_final.log: 11008x4096 x128 30.6 vs 35.1 us, x512 86.2 vs
+// 93.9; 4096^2 x128 15.6 vs 15.4, x256 22.3 vs 22.5; 4096x11008 x128 28.8 vs 29.1).  Q8_0 and
+// Q6_K stay on the LDS-DMA GEMM (4096^2 x128 Q8_0 20.8 vs 17.3; Q6_K 28672x8192 x128 115.6 vs
+// 111.9).
+constexpr int64_t kWgemmMinTokens = 33;
+bool use_wgemm(int t, int form, int64_t N)
 {
     const int w = gq::tuning().wgemm;
     if (form != gq::AF_F16 || w == 0) return false;
     if (w == 1) return true;
-    return t == GQ_Q4_K && N >= kWgemmMinTokens && M >= kWgemmMinRows;
+    return t == GQ_Q4_K && N >= kWgemmMinTokens;
 }
 gq::WGemmPlan wgemm_plan(int t, int64_t M, int64_t N, int64_t K)
 {
@@ -206,7 +209,7 @@ gq::WGemmPlan wgemm_plan(int t, int64_t M, int64_t N, int64_t K)
     gq::WGemmPlan p = gq::plan_wgemm(t, M, N, K, rg, nb, tu.wgemm_splits);
     // weight super-blocks held in registers (wd - 1 in flight); launch_wgemm lowers 4 to 3 for
     // the two-fragment waves, 3 to 2 where it would spill
-    p.wd = tu.wgemm_wd ? tu.wgemm_wd : 3;
+    p.wd = tu.wgemm_wd ? tu.wgemm_wd : (nb <= 4 ? 4 : 3);
     return p;
 }
 
@@ -267,7 +270,7 @@ size_t ws_bytes(int t, int act, int64_t M, int64_t N, int64_t K)
         for (int64_t mc : {mr, M % mr})
             for (int64_t nc : {nt, N % nt})
                 if (mc > 0 && nc > 0) {
-                    const size_t q = use_wgemm(t, r.form, mc, nc) ? wgemm_plan(t, mc, nc, K).partial_bytes
+                    const size_t q = use_wgemm(t, r.form, nc) ? wgemm_plan(t, mc, nc, K).partial_bytes
                                                             : gq::plan_gemm(t, mc, nc, K, r.form).partial_bytes;
                     p = q > p ? q : p;
                 }
@@ -470,7 +473,7 @@ static int compute(gq_type t, int act, const void *A, void *workspace, size_t wo
         for (int64_t n0 = 0; n0 < N && e == hipSuccess; n0 += nt)
             for (int64_t m0 = 0; m0 < M && e == hipSuccess; m0 += mr) {
                 const int64_t mc = M - m0 < mr ? M - m0 : mr, nc = N - n0 < nt ? N - n0 : nt;
-                if (use_wgemm(t, r.form, mc, nc)) {
+                if (use_wgemm(t, r.form, nc)) {
                     e = gq::launch_wgemm(t, (const uint8_t *)A + m0 * row_bytes_of(t, K), c.xdeq + n0 * K,
                                          (uint16_t *)C + n0 * ldc + m0, c.partials, wgemm_plan(t, mc, nc, K), mc, nc,
                                          K, ldc, s);
@@ -512,7 +515,7 @@ int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int6
         if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (decode): %s", hipGetErrorString(e));
         return GQ_OK;
     }
-    if (!r.gemv && !r.blas && act == GQ_ACT_Q8_1 && r.form == gq::AF_F16 && !use_wgemm(t, r.form, M, N) &&
+    if (!r.gemv && !r.blas && act == GQ_ACT_Q8_1 && r.form == gq::AF_F16 && !use_wgemm(t, r.form, N) &&
         gemm_rows_per_launch(t, M, K) >= M &&
         gemm_toks_per_launch(N, K) >= N) {
         // 16/32-token tiles whose split fits LDS: the GEMM quantizes the activations itself (no
