@@ -291,166 +291,318 @@ def cpu_baseline(fmt, M, K, N, target_s=6.0):
     return main, [one, vec]
 
 
-class ShardedRunner:
-    """One rank's part of a row-sharded step: RowShardedMMQ over rotating copies of this rank's
-    packed rows (>= 1 GiB), the local MMQ through the C ABI into a padded slab (graph-capturable:
-    preallocated workspace, torch's current stream), then the RCCL all_gather + assemble."""
+# ---------------------------------------------------------------------------------------
+# N > 1: row-sharded strong scaling of BASELINE configs[3] (+ weak scaling as an extra field)
 
-    def __init__(self, fmt, M_global, K, N, dev, world, rank, seed=0):
-        import kernels._lib as kl
-        from dist.row_shard import RowShardedMMQ, shard_rows
-        self.L = kl.lib()
-        self.fmt, self.K, self.N, self.dev, self.world = fmt, K, N, dev, world
-        self.row0, self.rows, self.R = shard_rows(M_global, world, rank)
-        qk, nbytes = BLOCK[fmt]
-        wbytes = max(1, self.rows * (K // qk) * nbytes)
-        self.ncopies = max(2, math.ceil(ROTATE_BYTES / wbytes))
-        base = device_random_blocks(fmt, max(self.rows, 1), K, dev, seed + rank)[:self.rows * (K // qk) * nbytes]
-        self.ws_bytes = max(1, kl.workspace_size(GTYPE[fmt], max(self.rows, 1), N, K))
-        self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=dev)
-        self.parts = [RowShardedMMQ(fmt, base if c == 0 else base.clone(), M_global, K, align=64,
-                                    compute=self._compute, world=world, rank=rank) for c in range(self.ncopies)]
-        g = torch.Generator(device=dev).manual_seed(seed + 1)
-        self.B = torch.randn(N, K, device=dev, generator=g).to(torch.float16)
-        self.slab = [torch.zeros(N, self.R, dtype=torch.float16, device=dev) for _ in range(2)]
-        self.gathered = [torch.empty(world, N, self.R, dtype=torch.float16, device=dev) for _ in range(2)]
+# (fmt, N_out, K) of the strong-scaling matrix and its token counts; the CPU rehearsal
+# (BENCH_REHEARSAL=1: no GPU, gloo, the product's CPU MMQ) runs the same code on a small shape
+STRONG_SHAPE, STRONG_TOKENS = ("q6_k", 28672, 8192), (1, 128)
+WEAK_SHAPE = ("q8_0", 4096, 4096, 128)
+REHEARSAL_STRONG, REHEARSAL_TOKENS, REHEARSAL_WEAK = ("q6_k", 2048, 512), (1, 8), ("q8_0", 256, 512, 8)
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(argv, n: int) -> int:
+    """--gpus N > 1 outside torch.distributed: run the N ranks (one process per GPU) as a child
+    `python -m torch.distributed.run` and return its exit code.  Runs before any GPU call, and
+    the parent never replaces itself (no exec)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + list(argv)
+    return subprocess.run(cmd).returncode
+
+
+class ShardStep:
+    """One rank's part of a row-sharded MMQ step (dist/row_shard.py's partitioning): its R rows of
+    an M_global-row matrix, cut into C row chunks; per chunk the local MMQ into a contiguous (N, Rc)
+    slab, an all_gather of the chunk (RCCL over xGMI; gloo in the rehearsal) and its assembly into
+    the (N, world * R) output -- chunk c's exchange runs on a side stream under chunk c+1's compute
+    ("pipeline the all-gather in chunks").  On a GPU everything is captured into
+    HIP graphs (the C ABI on torch's streams); in the CPU rehearsal (cpu=True) the compute is the
+    product's CPU MMQ (libgguf_quant) and the timing eager."""
+
+    CHUNKS = (1, 2, 4)
+
+    def __init__(self, fmt, M_global, K, N, dev, world, rank, seed=0, cpu=False, A_shard=None, B=None):
+        """A_shard / B (tests): this rank's packed rows (dist.row_shard.shard_bytes, align 256) and
+        the fp16 activations, instead of random ones."""
+        from dist.row_shard import shard_rows
+        self.fmt, self.Mg, self.K, self.N, self.dev, self.world, self.cpu = fmt, M_global, K, N, dev, world, cpu
         self.gtype = GTYPE[fmt]
+        # R divisible into max(CHUNKS) chunks of whole 64-row tiles
+        self.row0, self.rows, self.R = shard_rows(M_global, world, rank, align=64 * max(self.CHUNKS))
+        qk, nbytes = BLOCK[fmt]
+        self.rb = (K // qk) * nbytes
+        nrows = max(self.rows, 1)
+        if cpu:
+            from utils.quantize.q8_1 import quantize_to_q8_1
+            from utils.synth import random_blocks
+            self.ncopies = 1
+            base = torch.from_numpy(random_blocks(fmt, nrows, K, seed=seed + rank).view(np.int8))
+            g = torch.Generator().manual_seed(seed + 1)
+            self.B = torch.randn(N, K, generator=g).to(torch.float16) if B is None else B
+            self.Bq = quantize_to_q8_1(self.B)
+        else:
+            import kernels._lib as kl
+            self.kl, self.L = kl, kl.lib()
+            self.ncopies = max(2, math.ceil(ROTATE_BYTES / max(1, self.rows * self.rb)))
+            base = device_random_blocks(fmt, nrows, K, dev, seed + rank)
+            g = torch.Generator(device=dev).manual_seed(seed + 1)
+            self.B = torch.randn(N, K, device=dev, generator=g).to(torch.float16) if B is None else B
+            self.ws_bytes = max(max(1, kl.workspace_size(self.gtype, self.R // C, N, K)) for C in self.CHUNKS)
+            self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=dev)
+        base = base[:self.rows * self.rb] if A_shard is None else A_shard
+        assert base.numel() == self.rows * self.rb, "A_shard is not this rank's row range"
+        self.weights = [base] + [base.clone() for _ in range(self.ncopies - 1)]
+        z = dict(dtype=torch.float16, device=dev)
+        # per chunk count, two buffer sets (steps alternate): slabs, gathered chunks, output
+        self.slab = {C: [[torch.zeros(N, self.R // C, **z) for _ in range(C)] for _ in range(2)] for C in self.CHUNKS}
+        self.gath = {C: [[torch.zeros(world, N, self.R // C, **z) for _ in range(C)] for _ in range(2)]
+                     for C in self.CHUNKS}
+        self.out = [torch.zeros(N, world * self.R, **z) for _ in range(2)]
 
-    def _compute(self, A_shard, B, rows, N, K, out):
-        rc = self.L.gq_mmq(self.gtype, A_shard.data_ptr(), B.data_ptr(), out.data_ptr(), rows, N, K, K,
-                           out.stride(0), self.ws.data_ptr(), self.ws_bytes,
-                           torch.cuda.current_stream(self.dev).cuda_stream)
+    # -- the pieces of a step -------------------------------------------------------------
+    def prepare(self):
+        """Quantize the activations once per step (GEMM shapes; N <= 4 fuses it per call)."""
+        if self.cpu or self.N <= 4:
+            return
+        rc = self.L.gq_act_prepare(self.B.data_ptr(), self.N, self.K, self.K, self.ws.data_ptr(), self.ws_bytes,
+                                   torch.cuda.current_stream(self.dev).cuda_stream)
         if rc:
             raise RuntimeError(self.L.gq_last_error().decode())
 
-    def local(self, i):
-        self.parts[i % self.ncopies].local(self.B, self.N, self.slab[i & 1])
+    def compute(self, i, C, c, j):
+        """Local MMQ of chunk c (of C) of step i's weight copy into slab set j."""
+        Rc = self.R // C
+        r0 = c * Rc
+        n = max(0, min(self.rows - r0, Rc))
+        if n == 0 or self.N == 0:
+            return
+        A = self.weights[i % self.ncopies]
+        out = self.slab[C][j][c]
+        if self.cpu:
+            from kernels.cpu_impls._cpu import cpu_mmq
+            out[:, :n] = cpu_mmq(self.gtype, A[r0 * self.rb:(r0 + n) * self.rb], self.Bq, n, self.N, self.K)
+            return
+        a_ptr = A.data_ptr() + r0 * self.rb
+        st = torch.cuda.current_stream(self.dev).cuda_stream
+        if self.N <= 4:
+            rc = self.L.gq_mmq(self.gtype, a_ptr, self.B.data_ptr(), out.data_ptr(), n, self.N, self.K, self.K, Rc,
+                               self.ws.data_ptr(), self.ws_bytes, st)
+        else:
+            rc = self.L.gq_mmq_prepared(self.gtype, a_ptr, self.ws.data_ptr(), self.ws_bytes, out.data_ptr(), n,
+                                        self.N, self.K, Rc, st)
+        if rc:
+            raise RuntimeError(self.L.gq_last_error().decode())
 
-    def capture(self, n, first=0):
-        g = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream(self.dev)
-        s.wait_stream(torch.cuda.current_stream(self.dev))
-        with torch.cuda.stream(s):
-            self.local(first)
-        torch.cuda.current_stream(self.dev).wait_stream(s)
-        torch.cuda.synchronize(self.dev)
-        with torch.cuda.graph(g):
-            for i in range(n):
-                self.local(first + i)
-        return g
+    def gather(self, C, c, j, async_op=False):
+        import torch.distributed as dist
+        g, sl = self.gath[C][j][c], self.slab[C][j][c]
+        return dist.all_gather_into_tensor(g.view(self.world * self.N, self.R // C), sl, async_op=async_op)
 
-    def capture_e2e(self, n):
-        """One graph of n whole steps: local MMQ on the compute stream; the all_gather (RCCL,
-        captured) and the assemble on a side stream, so step i's exchange overlaps step i+1's
-        compute; slab j is rewritten only after the exchange that read it (events)."""
-        part = self.parts[0]
-        side = torch.cuda.Stream(self.dev)
-        done = [torch.cuda.Event() for _ in range(2)]
-        out = [None, None]
+    def assemble(self, C, c, j):
+        """Gathered chunk c -> its column range of every rank's part of the output."""
+        Rc = self.R // C
+        self.out[j].view(self.N, self.world, self.R)[:, :, c * Rc:(c + 1) * Rc].copy_(
+            self.gath[C][j][c].permute(1, 0, 2))
 
-        def body(i):
-            if i >= 2:
-                torch.cuda.current_stream(self.dev).wait_event(done[i & 1])
-            self.local(i)
-            side.wait_stream(torch.cuda.current_stream(self.dev))
-            with torch.cuda.stream(side):
-                part.gather(self.slab[i & 1], self.gathered[i & 1])
-                out[i & 1] = part.assemble(self.gathered[i & 1])
-                done[i & 1].record(side)
+    def result(self, j=0):
+        return self.out[j][:, :self.Mg]
 
+    # -- GPU: three graphs ----------------------------------------------------------------
+    def _graph(self, body, n):
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(s):  # warm every op outside capture (RCCL communicator included)
-            for i in range(2):
-                body(i)
-            s.wait_stream(side)
+            body(0, True)
+            body(1, True)
         torch.cuda.current_stream(self.dev).wait_stream(s)
         torch.cuda.synchronize(self.dev)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread_local: the process group's watchdog thread polls its work events during capture
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             for i in range(n):
-                body(i)
-            torch.cuda.current_stream(self.dev).wait_stream(side)
+                body(i, False)
         return g
 
-    def end_to_end(self, steps):
-        """(seconds for `steps` whole steps -- local MMQ + all_gather + assemble -- max over
-        ranks, how it ran).  The steps are one captured graph (RCCL collectives captured);
-        for a backend that cannot be captured (gloo rehearsals), an eager loop: per step a one-step graph replay and an async
-        all_gather on RCCL's stream, one exchange in flight behind the next step's compute."""
-        import torch.distributed as dist
-        if dist.is_initialized() and dist.get_backend() == "nccl":  # RCCL collectives are capturable
-            g = self.capture_e2e(steps)
-            g.replay()
-            t = min(timed_replay(g, self.dev, True) for _ in range(3))
-            return t, "graph"
-        # (a failed capture leaves the stream poisoned, so no try: other backends run eagerly)
-        how = f"eager ({dist.get_backend() if dist.is_initialized() else 'no'} backend: not capturable)"
-        one = [self.capture(1, j) for j in range(2)]
-        part = self.parts[0]
+    def graph_compute(self, n):
+        def body(i, warm):
+            self.prepare()
+            self.compute(i, 1, 0, i & 1)
+        return self._graph(body, n)
 
-        def run(n):
+    def graph_overlap(self, n):
+        """Independent steps: step i's exchange (one all_gather) runs on a side stream under step
+        i+1's compute; slab set j is rewritten only after the exchange that read it."""
+        side = torch.cuda.Stream(self.dev)
+        done = [torch.cuda.Event() for _ in range(2)]
+
+        def body(i, warm):
+            j = i & 1
+            cur = torch.cuda.current_stream(self.dev)
+            if i >= 2 and not warm:  # (only events recorded inside this capture)
+                cur.wait_event(done[j])
+            self.prepare()
+            self.compute(i, 1, 0, j)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                self.gather(1, 0, j)
+                self.assemble(1, 0, j)
+                done[j].record(side)
+            if warm or i == n - 1:
+                cur.wait_stream(side)
+        return self._graph(body, n)
+
+    def graph_chain(self, n, C):
+        """Dependent steps: step i+1's matmul waits for step i's assembled output; inside a step
+        the C chunks pipeline compute against the exchange."""
+        side = torch.cuda.Stream(self.dev)
+        ev = [torch.cuda.Event() for _ in range(C)]
+
+        def body(i, warm):
+            cur = torch.cuda.current_stream(self.dev)
+            self.prepare()
+            for c in range(C):
+                self.compute(i, C, c, 0)
+                ev[c].record(cur)
+                side.wait_event(ev[c])
+                with torch.cuda.stream(side):
+                    self.gather(C, c, 0)
+                    self.assemble(C, c, 0)
+            cur.wait_stream(side)  # the next step starts from this step's output
+        return self._graph(body, n)
+
+    # -- CPU rehearsal: the same three, eager -------------------------------------------
+    def cpu_compute(self, n):
+        for i in range(n):
+            self.compute(i, 1, 0, i & 1)
+
+    def cpu_overlap(self, n):
+        pending = []
+        for i in range(n):
+            j = i & 1
+            self.compute(i, 1, 0, j)
+            pending.append((self.gather(1, 0, j, async_op=True), j))
+            if len(pending) > 1:
+                w, jj = pending.pop(0)
+                w.wait()
+                self.assemble(1, 0, jj)
+        for w, jj in pending:
+            w.wait()
+            self.assemble(1, 0, jj)
+
+    def cpu_chain(self, n, C):
+        for i in range(n):
             works = []
-            for i in range(n):
-                one[i & 1].replay()
-                _, w = part.gather(self.slab[i & 1], self.gathered[i & 1], async_op=True)
-                works.append((w, i & 1))
-                if len(works) > 1:
-                    w0, j = works.pop(0)
-                    if w0 is not None:
-                        w0.wait()
-                    part.assemble(self.gathered[j])
-            for w0, j in works:
-                if w0 is not None:
-                    w0.wait()
-                part.assemble(self.gathered[j])
+            for c in range(C):
+                self.compute(i, C, c, 0)
+                works.append(self.gather(C, c, 0, async_op=True))
+            for c, w in enumerate(works):
+                w.wait()
+                self.assemble(C, c, 0)
 
-        run(4)
-        if dist.is_initialized():
+
+def _max_over_ranks(t, dev):
+    import torch.distributed as dist
+    tt = torch.tensor([t], dtype=torch.float64, device=dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return float(tt.item())
+
+
+def time_sharded(ss: ShardStep, steps, warmup):
+    """{compute, overlap, chain_C...}: seconds per step, max over ranks (barrier on both sides)."""
+    import torch.distributed as dist
+    res = {}
+    if ss.cpu:
+        runs = [("compute", ss.cpu_compute), ("overlap", ss.cpu_overlap)] + \
+               [(f"chain{C}", (lambda n, C=C: ss.cpu_chain(n, C))) for C in ss.CHUNKS]
+        for key, run in runs:
+            run(max(1, warmup))
             dist.barrier()
-        torch.cuda.synchronize(self.dev)
+            t0 = time.perf_counter()
+            run(steps)
+            t = time.perf_counter() - t0
+            dist.barrier()
+            res[key] = _max_over_ranks(t, ss.dev) / steps
+        return res
+    graphs = [("compute", lambda n: ss.graph_compute(n)), ("overlap", lambda n: ss.graph_overlap(n))] + \
+             [(f"chain{C}", (lambda n, C=C: ss.graph_chain(n, C))) for C in ss.CHUNKS]
+    for key, make in graphs:
+        g = make(steps)
+        g.replay()
+        torch.cuda.synchronize(ss.dev)
+        res[key] = min(timed_replay(g, ss.dev, True) for _ in range(3)) / steps
+        del g
+    return res
+
+
+def time_unsharded(fmt, M, K, N, steps, warmup, dev, cpu):
+    """The whole matrix on this one device (rank 0's 1-GPU reference for speedup_vs_1gpu): the same
+    ShardStep compute as the ranks run, with world 1 (no process-group calls)."""
+    ss = ShardStep(fmt, M, K, N, dev, 1, 0, cpu=cpu)
+    if cpu:
+        ss.cpu_compute(max(1, warmup))
         t0 = time.perf_counter()
-        run(steps)
-        torch.cuda.synchronize(self.dev)
-        t = time.perf_counter() - t0
-        if dist.is_initialized():
-            tt = torch.tensor([t], device=self.dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            dist.barrier()
-            t = float(tt.item())
-        return t, how
+        ss.cpu_compute(steps)
+        return (time.perf_counter() - t0) / steps
+    g = ss.graph_compute(steps)
+    g.replay()
+    t = min(timed_replay(g, dev) for _ in range(3)) / steps
+    del ss, g
+    torch.cuda.empty_cache()
+    return t
+
+
+def bench_sharded(fmt, Mg, K, N, steps, warmup, dev, world, rank, cpu, unsharded=True):
+    """One row-sharded configuration over the group: compute-only, end-to-end with overlap and the
+    dependent chain (per chunk count; the best is `e2e_chain`), and -- rank 0, the other ranks
+    waiting -- the unsharded matrix on one device for speedup_vs_1gpu."""
+    import torch.distributed as dist
+    ss = ShardStep(fmt, Mg, K, N, dev, world, rank, cpu=cpu)
+    t = time_sharded(ss, steps, warmup)
+    rows_per_rank, ncopies = ss.R, ss.ncopies
+    del ss
+    if not cpu:
+        torch.cuda.empty_cache()
+    t1 = None
+    if unsharded:
+        dist.barrier()
+        if rank == 0:
+            t1 = time_unsharded(fmt, Mg, K, N, steps, warmup, dev, cpu)
+        dist.barrier()
+    chains = {C: t[f"chain{C}"] for C in ShardStep.CHUNKS}
+    best = min(chains, key=chains.get)
+    _, _, flops = model(fmt, Mg, K, N)
+    qk, nbytes = BLOCK[fmt]
+    wbytes = Mg * (K // qk) * nbytes
+    ms = lambda x: round(x * 1e3, 6)  # noqa: E731
+    out = {"config": f"{fmt}_{Mg}x{K}_m{N}", "fmt": fmt, "N_out_global": Mg, "K": K, "M_tok": N, "ranks": world,
+           "rows_per_rank": rows_per_rank, "weight_copies": ncopies,
+           "compute_ms_per_step": ms(t["compute"]), "e2e_overlap_ms_per_step": ms(t["overlap"]),
+           "e2e_chain_ms_per_step": ms(chains[best]), "e2e_chain_chunks": best,
+           "e2e_chain_ms_by_chunks": {str(C): ms(v) for C, v in chains.items()},
+           "compute_tflops": round(flops / t["compute"] / 1e12, 3),
+           "e2e_overlap_tflops": round(flops / t["overlap"] / 1e12, 3),
+           "e2e_chain_tflops": round(flops / chains[best] / 1e12, 3),
+           "e2e_chain_weight_GBps": round(wbytes / chains[best] / 1e9, 1),
+           "collective": f"all_gather_into_tensor per row chunk (backend {dist_backend()}) + assemble copy"}
+    if t1 is not None:
+        out["unsharded_1dev_ms_per_step"] = ms(t1)
+        out["speedup_vs_1gpu"] = {"compute": round(t1 / t["compute"], 3), "e2e_overlap": round(t1 / t["overlap"], 3),
+                                  "e2e_chain": round(t1 / chains[best], 3)}
+    return out
 
 
 def dist_backend():
     import torch.distributed as dist
     b = dist.get_backend() if dist.is_initialized() else "none"
     return "nccl = RCCL over xGMI" if b == "nccl" else b
-
-
-def bench_sharded(name, steps, warmup, dev, dist_on, world, rank, M_global=None):
-    """Row-sharded run of config `name` over the ranks: M_global rows in total (default: the
-    config's N_out, i.e. strong scaling; weak scaling passes world * N_out)."""
-    fmt, M, K, N = CONFIGS[name]
-    Mg = M_global or M
-    r = ShardedRunner(fmt, Mg, K, N, dev, world, rank, seed=0)
-    gw = r.capture(max(1, warmup))
-    gw.replay()
-    g = r.capture(steps)
-    g.replay()
-    t_c = min(timed_replay(g, dev, dist_on) for _ in range(3))
-    t_e, how = r.end_to_end(steps) if dist_on else (t_c, "graph (1 rank: no exchange)")
-    _, _, flops = model(fmt, Mg, K, N)
-    qk, nbytes = BLOCK[fmt]
-    wbytes = Mg * (K // qk) * nbytes
-    out = {"config": name, "fmt": fmt, "N_out_global": Mg, "K": K, "M_tok": N, "ranks": world,
-           "rows_per_rank": r.R, "ms_per_step": t_e / steps * 1e3, "compute_ms_per_step": t_c / steps * 1e3,
-           "tflops": flops / (t_e / steps) / 1e12, "compute_only_tflops": flops / (t_c / steps) / 1e12,
-           "weight_GBps": wbytes / (t_e / steps) / 1e9, "weight_copies": r.ncopies,
-           "collective": (f"all_gather_into_tensor (backend {dist_backend()}) + assemble" if dist_on
-                          else "none (1 rank)"), "timed_as": how}
-    del r, g, gw
-    torch.cuda.empty_cache()
-    return out
 
 
 def bench_config(name, steps, warmup, dev):
@@ -586,13 +738,80 @@ def compact(e):
     return o
 
 
+def eager_call_us(dev, n=1000):
+    """Median wall time of n eager drop-in calls kernels.mmq_q4_k.mmq_q4_k(A, B, 4096, 1, 4096)
+    (the reference's callers' form, /root/reference/test/test_mmq_q4_k.py:34): Python + ctypes
+    + output allocation + launch, each call synchronized."""
+    from kernels.mmq_q4_k import mmq_q4_k
+    A = device_random_blocks("q4_k", 4096, 4096, dev, seed=11)
+    B = torch.randn(1, 4096, device=dev).to(torch.float16)
+    for _ in range(20):
+        mmq_q4_k(A, B, 4096, 1, 4096)
+    torch.cuda.synchronize(dev)
+    ts = []
+    for _ in range(n):
+        t0 = time.perf_counter()
+        mmq_q4_k(A, B, 4096, 1, 4096)
+        torch.cuda.synchronize(dev)
+        ts.append(time.perf_counter() - t0)
+    return round(float(np.median(ts)) * 1e6, 2)
+
+
+def strong_line(args, world, rank, dev, cpu):
+    """The N > 1 line: Q6_K 28672x8192 (BASELINE configs[3]) row-sharded over the ranks at M_tok
+    1 and 128 (value = the 128-token dependent-chain end-to-end rate), weak scaling as an extra
+    field."""
+    fmt, M, K = REHEARSAL_STRONG if cpu else STRONG_SHAPE
+    toks = REHEARSAL_TOKENS if cpu else STRONG_TOKENS
+    pts = [bench_sharded(fmt, M, K, N, args.steps, args.warmup, dev, world, rank, cpu) for N in toks]
+    wf, wM, wK, wN = REHEARSAL_WEAK if cpu else WEAK_SHAPE
+    weak = bench_sharded(wf, world * wM, wK, wN, max(20, args.steps // 4) if not cpu else args.steps, args.warmup, dev,
+                         world, rank, cpu, unsharded=False)
+    head = pts[-1]
+    N = head["M_tok"]
+    if rank != 0:
+        return None
+    line = {
+        "metric": "effective fp16 TFLOPS (+ quant-weight GB/s) per GGUF type",
+        "value": head["e2e_chain_tflops"],
+        "unit": "TFLOP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": head["e2e_chain_ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f16",
+        "data": "synthetic (random packed blocks, N(0,1) fp16 activations)",
+        "config": {"workload": head["config"] + f"_rowshard{world}", "gguf_type": fmt, "N_out": M, "K": K, "M_tok": N,
+                   "parallelism": f"rowshard{world}", "rows_per_rank": head["rows_per_rank"],
+                   "value_is": "dependent-chain end-to-end (step i+1 waits for step i's assembled output), "
+                               "best row-chunk count"},
+        "compute_ms_per_step": head["compute_ms_per_step"],
+        "e2e_overlap_ms_per_step": head["e2e_overlap_ms_per_step"],
+        "e2e_chain_ms_per_step": head["e2e_chain_ms_per_step"],
+        "speedup_vs_1gpu": head.get("speedup_vs_1gpu"),
+        "weight_GBps": head["e2e_chain_weight_GBps"],
+        "roofline": dict(roofline(fmt, head["rows_per_rank"], K, N, head["compute_ms_per_step"] / 1e3),
+                         kernel="rank-local step on its rows (act quant + MMQ), compute only"),
+        "cpu_baseline": None,
+        "strong": pts,
+        "weak": weak,
+    }
+    if cpu:
+        line["rehearsal"] = ("CPU rehearsal (BENCH_REHEARSAL=1): gloo, the product's CPU MMQ, shapes scaled down; "
+                             "not a GPU measurement")
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default=DEFAULT, choices=sorted(CONFIGS))
-    ap.add_argument("--strong", action="store_true", help="headline = strong scaling of Q6_K 28672x8192 x128")
+    ap.add_argument("--strong", action="store_true", help="the N > 1 line (Q6_K 28672x8192 row-sharded) at any N")
     ap.add_argument("--quick", action="store_true", help="headline only: no per-type sweep")
     ap.add_argument("--sweep", action="store_true", help="(the default; kept for old command lines)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -600,51 +819,46 @@ def main():
                     help="print only the Q4_K_M layer sweep (fused and unfused), one JSON line")
     args = ap.parse_args()
 
+    # --gpus N > 1 outside torch.distributed: the N ranks run as a child process
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # BENCH_FORCE_DIST=1: the distributed code path even at world 1 (exercises RCCL graph
-    # capture on a 1-GPU box)
-    dist_on = world > 1 or os.environ.get("BENCH_FORCE_DIST") == "1"
-    # BENCH_BACKEND=gloo: rehearsal of the N > 1 path with every rank on the visible GPUs
-    # round-robin (e.g. 2 ranks on a 1-GPU box); the product path is "nccl" = RCCL over xGMI
-    backend = os.environ.get("BENCH_BACKEND", "nccl")
-    local = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
-    dev = torch.device("cuda", local)
-    if dist_on:
+    if world != args.gpus:
+        print(f"bench.py: world size {world} != --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+    # BENCH_REHEARSAL=1: the N > 1 path on the CPU (gloo, product CPU MMQ, small shapes) -- the
+    # CPU test of the launcher and the line; BENCH_FORCE_DIST=1: the N > 1 path at world 1 (RCCL
+    # graph capture on a 1-GPU box)
+    cpu = os.environ.get("BENCH_REHEARSAL") == "1"
+    multi = world > 1 or args.strong or os.environ.get("BENCH_FORCE_DIST") == "1"
+    dev = torch.device("cpu") if cpu else torch.device("cuda", local)
+    if multi:
         import torch.distributed as dist
-        torch.cuda.set_device(dev)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+        init = None if "MASTER_ADDR" in os.environ else f"tcp://127.0.0.1:{free_port()}"
+        if cpu:
+            dist.init_process_group("gloo", init_method=init, world_size=world, rank=rank)
         else:
-            dist.init_process_group(backend)
+            torch.cuda.set_device(dev)
+            dist.init_process_group("nccl", init_method=init, world_size=world, rank=rank, device_id=dev)
+        line = strong_line(args, world, rank, dev, cpu)
+        if line is not None:
+            print(json.dumps(line), flush=True)
+        dist.destroy_process_group()
+        return
     torch.cuda.set_device(dev)
     if args.layer_only:
         Ns = (1, 2, 4, 8, 16, 32, 64, 128, 256, 512)
         print(json.dumps([bench_layer(Ns, ("q8_1",), max(20, args.steps // 4), args.warmup, dev, fuse=f)
                           for f in (True, False)]), flush=True)
         return
-    name = STRONG[1] if args.strong else args.config
+    name = args.config
     fmt, M, K, N = CONFIGS[name]
     sweep_steps = max(20, args.steps // 4)
-
-    if args.strong:
-        head = bench_sharded(name, args.steps, args.warmup, dev, dist_on, world, rank)
-        R = head["rows_per_rank"]
-        head["roofline"] = dict(roofline(fmt, R, K, N, head["compute_ms_per_step"] / 1e3),
-                                kernel="per-rank local step on its R rows (act quant + MMQ), compute only")
-    elif dist_on:
-        head = bench_sharded(name, args.steps, args.warmup, dev, dist_on, world, rank, M_global=world * M)
-        head["roofline"] = dict(roofline(fmt, M, K, N, head["compute_ms_per_step"] / 1e3),
-                                kernel="per-rank local step (act quant + MMQ), compute only")
-    else:
-        head = bench_config(name, args.steps, args.warmup, dev)
-    strong = []
-    if dist_on and not args.strong:
-        for sname in STRONG:
-            strong.append(bench_sharded(sname, sweep_steps, args.warmup, dev, dist_on, world, rank))
+    head = bench_config(name, args.steps, args.warmup, dev)
     sweep = []
-    if not args.quick and not args.strong and not dist_on:
+    if not args.quick:
         for sname in CONFIGS:
             if sname != name:
                 sweep.append(bench_config(sname, sweep_steps, args.warmup, dev))
@@ -654,46 +868,36 @@ def main():
         sweep.append(bench_msweep(sweep_steps, args.warmup, dev))
         sweep.extend(bench_fp8(("q8_0_4096x4096_m128", "q4_k_11008x4096_m128", "q6_k_28672x8192_m128",
                                 "q4_k_4096x4096_m1"), sweep_steps, args.warmup, dev))
-    cpu, cpu_var = None, None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu, cpu_var = cpu_baseline(fmt, M, K, N)
-
-    if rank == 0:
-        line = {
-            "metric": "effective fp16 TFLOPS (+ quant-weight GB/s) per GGUF type",
-            "value": round(head["tflops"], 3),
-            "unit": "TFLOP/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(head["ms_per_step"], 6),
-            "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak",
-            "vs_baseline": None,
-            "dtype": "f16" if N > 4 else "i8",
-            "arith": "q8_1 activations x dequantized GGUF weights on fp16 MFMA, fp32 accumulate" if N > 4 else
-                     "q8_1 int8 activations x GGUF int codes on v_dot4_i32_i8, fp32 block scaling",
-            "data": "synthetic (random packed blocks, N(0,1) fp16 activations)",
-            "config": {"workload": name, "gguf_type": fmt, "N_out": M, "K": K, "M_tok": N,
-                       "global_N_out": M if args.strong else M * world,
-                       "parallelism": f"rowshard{world}" if world > 1 else "single",
-                       "weight_copies_rotated": head["weight_copies"]},
-            "weight_GBps": round(head["weight_GBps"], 1),
-            "roofline": head["roofline"],
-            "cpu_baseline": cpu,
-        }
-        if "compute_only_tflops" in head:
-            line["compute_only_tflops"] = round(head["compute_only_tflops"], 3)
-            line["compute_ms_per_step"] = round(head["compute_ms_per_step"], 6)
-        if cpu_var:
-            line["cpu_baseline_variants"] = cpu_var
-        if strong:
-            line["strong"] = [compact(e) for e in strong]
-        if sweep:
-            line["sweep"] = [compact(e) for e in sweep]
-        print(json.dumps(line), flush=True)
-    if dist_on:
-        torch.distributed.destroy_process_group()
+    eager = eager_call_us(dev)
+    cpu_b, cpu_var = (None, None) if args.no_cpu else cpu_baseline(fmt, M, K, N)
+    line = {
+        "metric": "effective fp16 TFLOPS (+ quant-weight GB/s) per GGUF type",
+        "value": round(head["tflops"], 3),
+        "unit": "TFLOP/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(head["ms_per_step"], 6),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f16" if N > 4 else "i8",
+        "arith": "q8_1 activations x dequantized GGUF weights on fp16 MFMA, fp32 accumulate" if N > 4 else
+                 "q8_1 int8 activations x GGUF int codes on v_dot4_i32_i8, fp32 block scaling",
+        "data": "synthetic (random packed blocks, N(0,1) fp16 activations)",
+        "config": {"workload": name, "gguf_type": fmt, "N_out": M, "K": K, "M_tok": N, "parallelism": "single",
+                   "weight_copies_rotated": head["weight_copies"]},
+        "weight_GBps": round(head["weight_GBps"], 1),
+        "roofline": head["roofline"],
+        "cpu_baseline": cpu_b,
+        "eager_us": eager,
+        "eager_us_is": "median of 1000 eager kernels.mmq_q4_k.mmq_q4_k(A, B, 4096, 1, 4096) calls, each synchronized",
+    }
+    if cpu_var:
+        line["cpu_baseline_variants"] = cpu_var
+    if sweep:
+        line["sweep"] = [compact(e) for e in sweep]
+    print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

@@ -263,7 +263,7 @@ size_t ws_bytes(int t, int act, int64_t M, int64_t N, int64_t K)
     const Route r = route(t, act, N, K);
     size_t b = act_bytes(act, N, K);
     if (r.blas) b += align_up((size_t)M * K * 2) + gq::blas_workspace_bytes(); // fp16 W + hipBLASLt
-    else if (!r.gemv && gq::gemm_supported(t, K)) {
+    else if (!r.gemv && gq::gemm_supported(t, K) && M > 0 && N > 0) {
         // split-K partials of the largest need over the launch shapes (full and remainder chunks)
         const int64_t mr = gemm_rows_per_launch(t, M, K), nt = gemm_toks_per_launch(N, K);
         size_t p = 0;
@@ -340,11 +340,19 @@ AllGatherFn shard_allgather()
     return fn;
 }
 
+// every rank's need: the local MMQ's workspace is not monotone in the row count (fewer rows ->
+// fewer tiles -> a larger split-K factor -> more partials), so it is the max over the ranks'
+// shard sizes, not rank 0's
 size_t sharded_ws(int t, int64_t M, int64_t N, int64_t K, int world)
 {
     int64_t row0, rows, R;
-    shard_geom(M, world, 0, row0, rows, R); // rank 0 holds the most rows
-    return align_up((size_t)N * R * 2) + align_up((size_t)world * N * R * 2) + ws_bytes(t, GQ_ACT_Q8_1, rows, N, K);
+    size_t local = 0;
+    for (int g = 0; g < world; ++g) {
+        shard_geom(M, world, g, row0, rows, R);
+        const size_t w = ws_bytes(t, GQ_ACT_Q8_1, rows, N, K);
+        local = w > local ? w : local;
+    }
+    return align_up((size_t)N * R * 2) + align_up((size_t)world * N * R * 2) + local;
 }
 
 } // namespace

@@ -110,7 +110,42 @@ class RowShardedMMQ:
             return out
         return C
 
-    def __call__(self, B: torch.Tensor, N: int) -> torch.Tensor:
+    def __call__(self, B: torch.Tensor, N: int, chunks: int = 1) -> torch.Tensor:
+        if chunks > 1:
+            return self.pipelined(B, N, chunks)
         slab = self.local(B, N)
         gathered, _ = self.gather(slab)
         return self.assemble(gathered)
+
+    def pipelined(self, B: torch.Tensor, N: int, chunks: int) -> torch.Tensor:
+        """The step in `chunks` row chunks of the shard (pipeline the all-gather):
+        chunk c's local MMQ, then its all_gather issued asynchronously (on a GPU it runs on the
+        collective's stream under chunk c+1's compute), each gathered chunk placed into its
+        column range of every rank's part; same values as one un-chunked step."""
+        if not dist.is_initialized() and self.world != 1:
+            raise RuntimeError("pipelined() needs an initialised process group for world > 1")
+        qk, nbytes = BLOCK[self.fmt]
+        rb = (self.K // qk) * nbytes
+        Rc = -(-self.R // chunks)
+        dev = B.device
+        out = torch.empty(N, self.world * self.R, dtype=torch.float16, device=dev)
+        parts = []
+        for c0 in range(0, self.R, Rc):
+            w = min(Rc, self.R - c0)
+            n = max(0, min(self.rows - c0, w))
+            slab = torch.zeros(N, w, dtype=torch.float16, device=dev)
+            if n > 0 and N > 0:
+                self.compute(self.A[c0 * rb:(c0 + n) * rb], B, n, N, self.K, slab[:, :n])
+            g = torch.empty(self.world, N, w, dtype=torch.float16, device=dev)
+            if dist.is_initialized():
+                work = dist.all_gather_into_tensor(g.view(self.world * N, w), slab, group=self.group, async_op=True)
+            else:
+                g[0].copy_(slab)
+                work = None
+            parts.append((c0, w, g, work))
+        view = out.view(N, self.world, self.R)
+        for c0, w, g, work in parts:
+            if work is not None:
+                work.wait()
+            view[:, :, c0:c0 + w].copy_(g.permute(1, 0, 2))
+        return out[:, :self.M]

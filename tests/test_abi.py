@@ -140,3 +140,19 @@ def test_sharded_host_argument_checks():
     assert L.gq_assemble_shards(None, None, 2, 4, 60, 100, 100, None) != 0  # R % 8
     assert L.gq_assemble_shards(None, None, 2, 4, 64, 129, 200, None) != 0  # M > world * R
     assert L.gq_mmq_sharded_workspace_size(0, 4096, 128, 4096, 8) > 8 * 128 * 512 * 2
+
+
+@pytest.mark.parametrize("t,M,N,K", [(2, 28672, 128, 8192), (1, 11008, 128, 4096), (0, 4200, 16, 4096),
+                                     (1, 300, 64, 4096), (2, 1000, 1, 8192)])
+def test_sharded_workspace_covers_every_rank(t, M, N, K):
+    """gq_mmq_sharded_workspace_size covers every rank's local MMQ workspace (not monotone in the
+    shard's row count: a smaller shard gets a larger split-K factor) plus its two slabs."""
+    import kernels._lib as kl
+    from dist.row_shard import shard_rows
+    L = kl.lib()
+    for world in (1, 2, 3, 4, 8):
+        need = L.gq_mmq_sharded_workspace_size(t, M, N, K, world)
+        for g in range(world):
+            _, rows, R = shard_rows(M, world, g)
+            local = kl.workspace_size(t, rows, N, K)  # (0 rows: an empty shard)
+            assert need >= local + (world + 1) * N * R * 2, (world, g, need, local)

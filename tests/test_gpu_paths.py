@@ -303,6 +303,25 @@ def test_assemble_shards_kernel(W, N, R, M, pad):
     assert torch.equal(got.view(torch.int16), want.view(torch.int16))
 
 
+@pytest.mark.parametrize("fmt,M,N,K,chunks", [("q6_k", 1000, 1, 8192, 3), ("q4_k", 4096, 128, 4096, 4),
+                                               ("q8_0", 300, 16, 1024, 2)])
+def test_row_sharded_pipelined_world1(fmt, M, N, K, chunks, tune):
+    """RowShardedMMQ.pipelined (row chunks of the shard, one all-gather per chunk) at world 1
+    through the HIP MMQ: the same bits as the unsharded call (split-K off: the chunk row count
+    does not change the arithmetic then)."""
+    from dist.row_shard import RowShardedMMQ
+    from kernels._lib import TYPES, mmq
+    tune(GQ_GEMM_SPLITS=1, GQ_WGEMM_SPLITS=1)
+    dev = _dev()
+    qA = random_blocks(fmt, M, K, seed=M + 3)
+    A_t = torch.from_numpy(qA.view(np.int8)).to(dev)
+    B_t = torch.from_numpy(random_activations(N, K, seed=K)).to(dev)
+    want = mmq(TYPES[fmt], A_t, B_t, M, N, K)
+    got = RowShardedMMQ(fmt, A_t, M, K, world=1, rank=0).pipelined(B_t, N, chunks)
+    torch.cuda.synchronize()
+    assert torch.equal(got.view(torch.int16), want.view(torch.int16))
+
+
 @pytest.mark.parametrize("fmt,M,N,K", [("q6_k", 1000, 1, 8192), ("q4_k", 4096, 128, 4096), ("q8_0", 300, 16, 1024)])
 def test_mmq_sharded_entry_point_world1(fmt, M, N, K):
     """gq_mmq_sharded through the C ABI at world 1 (no communicator): the same bits as gq_mmq."""
