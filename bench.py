@@ -627,7 +627,10 @@ def bench_config(name, steps, warmup, dev):
         gk = r.capture(r.kernel, steps)
         gk.replay()
         t_k = min(timed_replay(gk, dev) for _ in range(3)) / steps
-        kname = "gemm_kernel (+ gemm_reduce_kernel when split-K)"
+        # (the library's routing, csrc/gq_capi.hip use_wgemm: Q4_K from 33 tokens on takes the
+        # weight-register GEMM)
+        kname = ("wgemm_kernel (+ wreduce_kernel when split-K)" if fmt == "q4_k" and N >= 33
+                 else "gemm_kernel (+ gemm_reduce_kernel when split-K)")
     wbytes, alg_bytes, flops = model(fmt, M, K, N)
     per_step = t / steps
     out = {

@@ -85,9 +85,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int KC = 64;     // K elements per stage
 constexpr int LDS_MAX = 160 * 1024;
-#ifndef GQ_GEMM_FR_GROUP // fused split-K reduce: splits whose partial loads are issued together
-#define GQ_GEMM_FR_GROUP 8
-#endif
+constexpr int FR_GROUP = 8; // fused split-K reduce: splits whose partial loads are issued together
 
 __device__ __forceinline__ h2 as_h2(uint32_t v) { return __builtin_bit_cast(h2, v); }
 __device__ __forceinline__ uint32_t as_u32(h2 v) { return __builtin_bit_cast(uint32_t, v); }
@@ -111,14 +109,8 @@ __device__ __forceinline__ h2 pair13(uint32_t c) { return as_h2(__builtin_amdgcn
 // bytes per stage.  Q6_K super-blocks are only 2-byte aligned: each is moved as 16-byte pieces
 // read from its own first byte (2-byte aligned DMA sources) into a 240-B image whose every
 // field is aligned (the d piece repeated at 208..223, d at 222).
-// SPW = activation sub-stages per weight stage (4: one super-block).  GQ_GEMM_Q8_FINE=1 builds
-// Q8_0 with one 64-element sub-stage per weight stage (68 B per row as 5 pieces from its
-// 4-byte aligned first byte, 5 slots), so the first sub-stage waits for a quarter of the
-// weight bytes: parity-green but no faster (Q8_0 4096^2 x16..x256 within 1%,
-// profiles/r02/q8_0_fine_stages_ab.txt) -- the first wait is not the weight bytes.
-#ifndef GQ_GEMM_Q8_FINE
-#define GQ_GEMM_Q8_FINE 0
-#endif
+// SPW = activation sub-stages per weight stage (4: one super-block; one sub-stage per weight
+// stage for Q8_0 was measured no faster and removed: profiles/r02/q8_0_fine_stages_ab.txt).
 template <int F> struct WStage;
 template <> struct WStage<Q4_K> { static constexpr int RBW = 144, SB = 144, SPW = 4; };
 // Q6_K rows are padded to 240 B (15 pieces, the last a repeat of the d piece): a 224-B stride
@@ -126,7 +118,7 @@ template <> struct WStage<Q4_K> { static constexpr int RBW = 144, SB = 144, SPW 
 // conflicts, ~half of the LDS cycles measured); 60 dwords spread 16 rows over distinct banks.
 template <> struct WStage<Q6_K> { static constexpr int RBW = 240, SB = 210, SPW = 4; };
 template <> struct WStage<Q8_0> {
-    static constexpr int SPW = GQ_GEMM_Q8_FINE ? 1 : 4, RBW = GQ_GEMM_Q8_FINE ? 80 : 272, SB = SPW * 68;
+    static constexpr int SPW = 4, RBW = 272, SB = SPW * 68;
 };
 
 // Activation sub-stage c (64 elements) = sub-stage s4 = c & 3 of super-block c >> 2: the K
@@ -144,11 +136,10 @@ __device__ __forceinline__ uint32_t act_voff(int p) // byte offset of piece p (8
     return 16u * p;
 }
 
-#ifndef GQ_GEMM_NWAVE // multiplying waves per workgroup (experiment: 4 = one per SIMD, two row groups each)
-#define GQ_GEMM_NWAVE 8
-#endif
-constexpr int NWAVE = GQ_GEMM_NWAVE; // 8: 512 threads, two waves per SIMD
-constexpr int R1 = 8 / NWAVE;        // row groups per wave of a 128-row tile
+// multiplying waves per workgroup: 8 = 512 threads, two waves per SIMD (4 waves x two row
+// groups was measured slower and removed: DESIGN.md 5)
+constexpr int NWAVE = 8;
+constexpr int R1 = 1; // row groups per wave of a 128-row tile
 
 // AQ (in-kernel activation quantization, 16- and 32-token tiles): the loader waves q8_1-quantize
 // the tile's fp16 activations for the whole split into LDS (every sub-stage resident, AQ_SUB at
@@ -300,22 +291,8 @@ __device__ __forceinline__ void stage_frags<Q8_0>(const uint8_t *wr, int g, int 
     }
 }
 
-// AUX = cache policy of the DMA (2 = nt).  GQ_GEMM_WNT=1 sets nt on the weight stream: equal
-// on Q8_0, 2-7% slower on Q4_K/Q6_K with weights rotated over 1 GiB (profiles/r02/
-// gemm_weight_nt_ab_rejected.txt), so the default policy stays
-#ifndef GQ_GEMM_WNT
-#define GQ_GEMM_WNT 0
-#endif
-// GQ_GEMM_AFIRST=1: the prologue issues the activation sub-stages before the first weight stage
-// (the first sub-stage then waits for everything issued: vmcnt(0))
-#ifndef GQ_GEMM_AFIRST
-#define GQ_GEMM_AFIRST 0
-#endif
-// GQ_GEMM_PSER=1: the loader waves let the first weight stage land before issuing the
-// prologue's activation sub-stages (the two streams in flight together are super-additive)
-#ifndef GQ_GEMM_PSER
-#define GQ_GEMM_PSER 0
-#endif
+// AUX = cache policy of the DMA (2 = nt; nt on the weight stream measured 2-7% slower and was
+// removed, as were an activation-first and a serialized prologue: profiles/r02/*_rejected.txt)
 template <int AUX = 0>
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, uint8_t *lds_dst, uint32_t voff, uint32_t soff)
 {
@@ -454,7 +431,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
                 vo = wv[i] + 16u * wpc[i];
                 so = (uint32_t)(WStage<F>::SB * w);
             }
-            dma16<GQ_GEMM_WNT ? 2 : 0>(wrs, k < G::W_REAL ? dst + 1024 * k : lds + G::SCRATCH, vo, so);
+            dma16(wrs, k < G::W_REAL ? dst + 1024 * k : lds + G::SCRATCH, vo, so);
         }
     };
     auto issue_a = [&](int64_t a) {
@@ -480,10 +457,6 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
     // rel = a - a0: W issues in iterations [max(0, rel-NAS+1), rel-1] that are multiples of SPW
     auto wait_a = [&](int rel) {
         constexpr int na = ABL & 4 ? 0 : G::NA, nw = ABL & 2 ? 0 : G::NW; // (ablated streams issue nothing)
-        if (GQ_GEMM_AFIRST && rel == 0) { // prologue A(0..NAS-2) then W(w0): sub-stage 0 needs all of it
-            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-            return;
-        }
         constexpr int base = (G::NAS - 2) * na;
         const int lo = rel - G::NAS + 1 > 0 ? rel - G::NAS + 1 : 0, hi = rel - 1;
         const int w_after = hi >= lo ? hi / SPW - (lo + SPW - 1) / SPW + 1 : 0;
@@ -578,18 +551,10 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
     if (!AQ && loader) { // loader waves: the DMA schedule of the pipeline note, no multiply
         if (w0 < w1) {
             const int64_t a0 = 4 * sb0, a1 = 4 * sb1;
-            if constexpr (GQ_GEMM_AFIRST) {
 #pragma unroll
-                for (int i = 0; i < G::NAS - 1; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
+            for (int i = 0; i < G::NWS - 1; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
 #pragma unroll
-                for (int i = 0; i < G::NWS - 1; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
-            } else {
-#pragma unroll
-                for (int i = 0; i < G::NWS - 1; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
-                if constexpr (GQ_GEMM_PSER) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // weights landed first
-#pragma unroll
-                for (int i = 0; i < G::NAS - 1; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
-            }
+            for (int i = 0; i < G::NAS - 1; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
             for (int64_t a = a0; a < a1; ++a) {
                 wait_a((int)(a - a0)); // A(a) landed -> barrier: the compute waves take sub-stage a
                 issue_a(a + G::NAS - 1 < a1 ? a + G::NAS - 1 : a1 - 1);
@@ -601,17 +566,10 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
     }
     if (w0 < w1) {
         const int64_t a0 = 4 * sb0, a1 = 4 * sb1;
-        if constexpr (GQ_GEMM_AFIRST) {
 #pragma unroll
-            for (int i = 0; i < G::NAS - 1 && NL == 0; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
+        for (int i = 0; i < G::NWS - 1 && NL == 0; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
 #pragma unroll
-            for (int i = 0; i < G::NWS - 1 && NL == 0; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
-        } else {
-#pragma unroll
-            for (int i = 0; i < G::NWS - 1 && NL == 0; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
-#pragma unroll
-            for (int i = 0; i < G::NAS - 1 && NL == 0; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
-        }
+        for (int i = 0; i < G::NAS - 1 && NL == 0; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
 #ifdef GQ_GEMM_STAMPS
         t_issued = __builtin_amdgcn_s_memtime() - t_start;
 #endif
@@ -830,7 +788,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
                 constexpr int TPU = NB == 1 ? 1 : 2;      // token tiles per store unit
                 constexpr int UPR = NB == 1 ? 1 : NB / 2; // units per row group
                 constexpr int NU = RG * UPR;              // units this wave sums
-                constexpr int GS = RG == 2 ? 4 : GQ_GEMM_FR_GROUP; // splits whose loads are in flight together
+                constexpr int GS = RG == 2 ? 4 : FR_GROUP; // splits whose loads are in flight together
                 // every unit's loads of GS splits issued together (one round trip per GS splits);
                 // splits past S add nothing here, and one +0 at the end stands for the +0's the
                 // reduce kernel adds for them (S not a multiple of 8): x + 0 is x except -0 -> +0
@@ -1149,7 +1107,6 @@ bool gemm_supported(int /*fmt*/, int64_t K) { return K > 0 && K % 256 == 0; }
 
 bool gemm_aq_ok(const GemmPlan &p)
 {
-    if (GQ_GEMM_Q8_FINE) return false; // the in-kernel quantizer's loader schedule assumes super-block weight stages
     if (!tuning().gemm_aq) return false;
     // splits of at most two super-blocks: the quantization (a few passes of the loader waves)
     // then hides under the first weight stage; longer splits measured neutral to 2% slower
