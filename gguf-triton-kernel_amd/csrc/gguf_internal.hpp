@@ -31,6 +31,9 @@ struct Tuning {
     int wgemm_nb = 0;                         // GQ_WGEMM_NB: 2/4/8 (0: auto)
     int wgemm_splits = 0;                     // GQ_WGEMM_SPLITS (0: auto)
     int wgemm_wd = 0;                         // GQ_WGEMM_WD: weight super-blocks in registers, 2/3/4 (0: auto)
+    int skinny = -1;                          // GQ_SKINNY: 5..32-token kernel (-1 auto, 0 off, 1 every 1..32)
+    int skinny_rg = 0;                        // GQ_SKINNY_RG: fragments per workgroup, 1..4 (0: auto)
+    int skinny_d = 0;                         // GQ_SKINNY_D: super-blocks in the register ring, 2..4 (0: auto)
     int ablate = 0;                           // GQ_ABLATE (GQ_ABLATION diagnostic builds only)
 };
 const Tuning &tuning();
@@ -112,6 +115,17 @@ struct WGemmPlan {
 WGemmPlan plan_wgemm(int fmt, int64_t M, int64_t N, int64_t K, int rg, int nb, int splits);
 hipError_t launch_wgemm(int fmt, const uint8_t *A, const uint16_t *X, uint16_t *C, void *partials,
                         const WGemmPlan &plan, int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
+
+// Skinny-token MMQ (mmq_skinny.hip, 1..32 tokens, K % 256 == 0): 16*rg rows x 16*nb tokens per
+// workgroup, K split over its 8 waves (8/nb ranges x nb token tiles), weights and activations
+// (fp16 x~, DEQ form) streamed into registers through a d-deep super-block ring, one launch, no
+// partials.  rg in 1..4, d = 2.
+struct SkinnyPlan {
+    int rg = 1, nb = 1, d = 3;
+};
+SkinnyPlan plan_skinny(int fmt, int64_t M, int64_t N, int64_t K, int rg, int d);
+hipError_t launch_skinny(int fmt, const uint8_t *A, const uint16_t *X, uint16_t *C, const SkinnyPlan &plan, int64_t M,
+                         int64_t N, int64_t K, int64_t ldc, hipStream_t s);
 
 // Dequantization and the library GEMM (mmq_dequant.hip).  perm: store 4-groups as (0,2,1,3),
 // matching act_quant's DEQ form.  blas_gemm returns 0 or a negative code.

@@ -75,6 +75,15 @@ bool parse_key(Tuning &t, const char *key, long long v)
     } else if (k == "GQ_WGEMM_WD") {
         if (!in({0, 2, 3, 4})) return false;
         t.wgemm_wd = (int)v;
+    } else if (k == "GQ_SKINNY") {
+        if (!in({-1, 0, 1})) return false;
+        t.skinny = (int)v;
+    } else if (k == "GQ_SKINNY_RG") {
+        if (!in({0, 1, 2, 3, 4})) return false;
+        t.skinny_rg = (int)v;
+    } else if (k == "GQ_SKINNY_D") {
+        if (!in({0, 2, 3, 4})) return false;
+        t.skinny_d = (int)v;
     } else if (k == "GQ_ABLATE") t.ablate = (int)v;
     else return false;
     return true;
@@ -88,7 +97,7 @@ void tuning_from_env(Tuning &t)
                                        "GQ_GEMM_NB", "GQ_GEMM_RG", "GQ_GEMM_LOADERS", "GQ_GEMM_SPLITS",
                                        "GQ_GEMM_PARTIAL", "GQ_GEMM_FUSED_REDUCE", "GQ_GEMV_CAP", "GQ_GEMV_R",
                                        "GQ_WGEMM", "GQ_WGEMM_RG", "GQ_WGEMM_NB", "GQ_WGEMM_SPLITS", "GQ_WGEMM_WD",
-                                       "GQ_ABLATE"};
+                                       "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D", "GQ_ABLATE"};
     for (const char *k : keys) {
         const char *e = getenv(k); // the only getenv of the library: once per process
         if (!e || !*e) continue;
@@ -201,6 +210,26 @@ bool use_wgemm(int t, int form, int64_t N)
     if (w == 1) return true;
     return t == GQ_Q4_K && N >= kWgemmMinTokens;
 }
+// Skinny-token kernel (mmq_skinny.hip).  By type and token count only (a row subset runs the
+// same arithmetic as the whole matrix): by default Q4_K at 5..16 tokens, where it measured
+// faster than the LDS-DMA GEMM (profiles/r03/skinny_sweep.log, step incl. act_quant: 4096^2
+// x16 10.8 vs 12.1 us, 11008x4096 17.8 vs 22.6, 4096x11008 18.1 vs 20.2); Q8_0 is level, Q6_K
+// and 17..32 tokens are faster on the GEMM.  GQ_SKINNY=1: every type at 1..32 tokens the GEMM
+// path would take (tests), 0: off.
+constexpr int64_t kSkinnyMinTokens = 5, kSkinnyMaxTokens = 16, kSkinnyForcedMax = 32;
+bool use_skinny(int t, int form, int64_t N)
+{
+    const int sk = gq::tuning().skinny;
+    if (form != gq::AF_F16 || sk == 0) return false;
+    if (sk == 1) return N <= kSkinnyForcedMax;
+    return t == GQ_Q4_K && N >= kSkinnyMinTokens && N <= kSkinnyMaxTokens;
+}
+gq::SkinnyPlan skinny_plan(int t, int64_t M, int64_t N, int64_t K)
+{
+    const gq::Tuning &tu = gq::tuning();
+    return gq::plan_skinny(t, M, N, K, tu.skinny_rg, tu.skinny_d);
+}
+
 gq::WGemmPlan wgemm_plan(int t, int64_t M, int64_t N, int64_t K)
 {
     const gq::Tuning &tu = gq::tuning();
@@ -265,13 +294,16 @@ size_t ws_bytes(int t, int act, int64_t M, int64_t N, int64_t K)
     if (r.blas) b += align_up((size_t)M * K * 2) + gq::blas_workspace_bytes(); // fp16 W + hipBLASLt
     else if (!r.gemv && gq::gemm_supported(t, K) && M > 0 && N > 0) {
         // split-K partials of the largest need over the launch shapes (full and remainder chunks)
-        const int64_t mr = gemm_rows_per_launch(t, M, K), nt = gemm_toks_per_launch(N, K);
+        // (the kernel is chosen by the call's token count, so every chunk runs the same arithmetic)
+        const bool sk = use_skinny(t, r.form, N), wg = use_wgemm(t, r.form, N);
+        const int64_t mr = gemm_rows_per_launch(t, M, K), nt = sk ? N : gemm_toks_per_launch(N, K);
         size_t p = 0;
         for (int64_t mc : {mr, M % mr})
             for (int64_t nc : {nt, N % nt})
                 if (mc > 0 && nc > 0) {
-                    const size_t q = use_wgemm(t, r.form, nc) ? wgemm_plan(t, mc, nc, K).partial_bytes
-                                                            : gq::plan_gemm(t, mc, nc, K, r.form).partial_bytes;
+                    const size_t q = sk   ? 0
+                                     : wg ? wgemm_plan(t, mc, nc, K).partial_bytes
+                                          : gq::plan_gemm(t, mc, nc, K, r.form).partial_bytes;
                     p = q > p ? q : p;
                 }
         b += align_up(p);
@@ -476,12 +508,21 @@ static int compute(gq_type t, int act, const void *A, void *workspace, size_t wo
         e = gq::launch_gemv(t, (const uint8_t *)A, c.xq, c.xd, c.xs, (uint16_t *)C, M, N, K, ldc, s);
     } else {
         // chunks of < 2 GiB of weights and of activations per launch (32-bit buffer offsets)
-        const int64_t mr = gemm_rows_per_launch(t, M, K), nt = gemm_toks_per_launch(N, K);
+        // (the kernel is chosen by the call's token count: every chunk runs the same arithmetic)
+        // (<= 32 skinny tokens are never cut: their x~ is far below the guard, and the token
+        // count sets the kernel's K split)
+        const bool sk = use_skinny(t, r.form, N), wg = use_wgemm(t, r.form, N);
+        const int64_t mr = gemm_rows_per_launch(t, M, K), nt = sk ? N : gemm_toks_per_launch(N, K);
         e = hipSuccess;
         for (int64_t n0 = 0; n0 < N && e == hipSuccess; n0 += nt)
             for (int64_t m0 = 0; m0 < M && e == hipSuccess; m0 += mr) {
                 const int64_t mc = M - m0 < mr ? M - m0 : mr, nc = N - n0 < nt ? N - n0 : nt;
-                if (use_wgemm(t, r.form, nc)) {
+                if (sk) {
+                    e = gq::launch_skinny(t, (const uint8_t *)A + m0 * row_bytes_of(t, K), c.xdeq + n0 * K,
+                                          (uint16_t *)C + n0 * ldc + m0, skinny_plan(t, mc, nc, K), mc, nc, K, ldc, s);
+                    continue;
+                }
+                if (wg) {
                     e = gq::launch_wgemm(t, (const uint8_t *)A + m0 * row_bytes_of(t, K), c.xdeq + n0 * K,
                                          (uint16_t *)C + n0 * ldc + m0, c.partials, wgemm_plan(t, mc, nc, K), mc, nc,
                                          K, ldc, s);
@@ -523,7 +564,7 @@ int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int6
         if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (decode): %s", hipGetErrorString(e));
         return GQ_OK;
     }
-    if (!r.gemv && !r.blas && act == GQ_ACT_Q8_1 && r.form == gq::AF_F16 && !use_wgemm(t, r.form, N) &&
+    if (!r.gemv && !r.blas && act == GQ_ACT_Q8_1 && r.form == gq::AF_F16 && !use_wgemm(t, r.form, N) && !use_skinny(t, r.form, N) &&
         gemm_rows_per_launch(t, M, K) >= M &&
         gemm_toks_per_launch(N, K) >= N) {
         // 16/32-token tiles whose split fits LDS: the GEMM quantizes the activations itself (no
