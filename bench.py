@@ -646,12 +646,13 @@ def bench_config(name, steps, warmup, dev):
     return out
 
 
-def bench_layer(Ns, acts, steps, warmup, dev, fuse=True):
+def bench_layer(Ns, acts, steps, warmup, dev, fuse=True, grouped="auto"):
     """BASELINE configs[4]: the seven projections of a Llama-7B block under GGUF Q4_K_M (layer 0:
     attn_v and ffn_down in Q6_K, the rest Q4_K), shared inputs quantized once per group
     (kernels.layer_mix.LayerMix; fuse: q+k and gate+up as one call each), for each token count in
     Ns and activation format in acts ("q8_1": the reference's semantics; "fp8": the e4m3 variant).
-    Weights rotate over >= 1 GiB."""
+    Weights rotate over >= 1 GiB.  grouped: LayerMix's grouped-decode setting ("auto": the whole
+    layer as one gq_mmq_grouped launch at 1 token; True: at 1..4; False: one launch per set)."""
     from gguf import LLAMA_LAYER_SHAPES, q4_k_m_layer_types
     from kernels.layer_mix import GGUFLinear, LayerMix
     types = q4_k_m_layer_types(0, 32)
@@ -662,12 +663,15 @@ def bench_layer(Ns, acts, steps, warmup, dev, fuse=True):
              for n in LLAMA_LAYER_SHAPES} for c in range(ncopies)]
     res = []
     for act in acts:
-        layers = [LayerMix(lin, act=act, fuse=fuse) for lin in lins]
+        layers = [LayerMix(lin, act=act, fuse=fuse, grouped=grouped) for lin in lins]
         for N in Ns:
             g = torch.Generator(device=dev).manual_seed(7)
             x = torch.randn(N, 4096, device=dev, generator=g).to(torch.float16)
             h = torch.randn(N, 11008, device=dev, generator=g).to(torch.float16)
-            outs = {n: torch.empty(N, M, dtype=torch.float16, device=dev) for n, (M, K) in LLAMA_LAYER_SHAPES.items()}
+            # output buffers of the unfused projections (fused ones are column views of the
+            # layer's own buffer; a buffer for them would add a copy)
+            outs = {n: torch.empty(N, M, dtype=torch.float16, device=dev) for n, (M, K) in LLAMA_LAYER_SHAPES.items()
+                    if n not in layers[0].parts}
             flops = sum(2.0 * N * M * K for M, K in LLAMA_LAYER_SHAPES.values())
             for i in range(max(ncopies, warmup)):  # library handles, every copy's buffers: outside capture
                 layers[i % ncopies].forward(x, h, out=outs)
@@ -684,7 +688,9 @@ def bench_layer(Ns, acts, steps, warmup, dev, fuse=True):
                     layers[i % ncopies].forward(x, h, out=outs)
             gr.replay()
             t = min(timed_replay(gr, dev) for _ in range(3)) / steps
-            res.append({"config": f"q4_k_m_llama7b_layer_m{N}", "act": act, "fused": fuse, "fmt": "q4_k+q6_k", "M_tok": N,
+            res.append({"config": f"q4_k_m_llama7b_layer_m{N}", "act": act, "fused": fuse,
+                        "grouped": act == "q8_1" and N <= {"auto": 1, True: 4, False: 0}[grouped],
+                        "fmt": "q4_k+q6_k", "M_tok": N,
                         "us_per_step": round(t * 1e6, 2), "tflops": round(flops / t / 1e12, 3),
                         "weight_GBps": round(layer_bytes / t / 1e9, 1)})
             del gr

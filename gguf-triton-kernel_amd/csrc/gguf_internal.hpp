@@ -116,6 +116,22 @@ WGemmPlan plan_wgemm(int fmt, int64_t M, int64_t N, int64_t K, int rg, int nb, i
 hipError_t launch_wgemm(int fmt, const uint8_t *A, const uint16_t *X, uint16_t *C, void *partials,
                         const WGemmPlan &plan, int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
 
+// Grouped decode (mmq_decode.hip): several matrices -- each its own type, activations (N x K
+// fp16, row stride ldx) and output (N x M, stride ldc) -- in one launch per token tile, the
+// chip's waves split by weight bytes; each matrix's rows come out bit-identical to its own
+// launch_decode_fused.  N <= 4, every item decode_fused_ok, at most 16 (item, token group) parts.
+struct DecodeItem {
+    int fmt;
+    const uint8_t *A;
+    const uint16_t *X;
+    int64_t ldx;
+    uint16_t *C;
+    int64_t ldc;
+    int64_t M, K;
+};
+bool decode_grouped_ok(const DecodeItem *items, int n, int64_t N);
+hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipStream_t s);
+
 // Skinny-token MMQ (mmq_skinny.hip, 1..32 tokens, K % 256 == 0): 16*rg rows x 16*nb tokens per
 // workgroup, K split over its 8 waves (8/nb ranges x nb token tiles), weights and activations
 // (fp16 x~, DEQ form) streamed into registers through a d-deep super-block ring, one launch, no

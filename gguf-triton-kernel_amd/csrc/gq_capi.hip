@@ -704,6 +704,36 @@ size_t gq_mmq_sharded_workspace_size(gq_type t, int64_t M, int64_t N, int64_t K,
     return sharded_ws(t, M, N, K, world);
 }
 
+int gq_mmq_grouped(const gq_group_item *items, int n, int64_t N, void *stream)
+{
+    g_err.clear();
+    if (n < 0 || (n > 0 && !items)) return fail(GQ_EINVAL, "bad item list (n=%d, items=%p)", n, (const void *)items);
+    if (N < 0) return fail(GQ_EINVAL, "negative N");
+    gq::DecodeItem di[16];
+    int m = 0;
+    for (int i = 0; i < n; ++i) {
+        const gq_group_item &it = items[i];
+        const int rc = check_common(it.type, it.M, N, it.K);
+        if (rc != GQ_OK) return rc;
+        if (it.M == 0 || N == 0) continue;
+        if (it.K == 0) return fail(GQ_EINVAL, "item %d: K must be positive", i);
+        if (!it.A || !it.B || !it.C) return fail(GQ_EINVAL, "item %d: null pointer", i);
+        if (it.ldb < it.K) return fail(GQ_EINVAL, "item %d: ldb=%lld < K=%lld", i, (long long)it.ldb, (long long)it.K);
+        if (it.ldc < it.M) return fail(GQ_EINVAL, "item %d: ldc=%lld < M=%lld", i, (long long)it.ldc, (long long)it.M);
+        if (m == 16) return fail(GQ_EUNSUPPORTED, "more than 16 items");
+        di[m++] = gq::DecodeItem{it.type, (const uint8_t *)it.A, (const uint16_t *)it.B, it.ldb, (uint16_t *)it.C,
+                                 it.ldc, it.M, it.K};
+    }
+    if (m == 0) return GQ_OK;
+    if (!gq::decode_grouped_ok(di, m, N))
+        return fail(GQ_EUNSUPPORTED, "not a grouped-decode shape (N=%lld; N <= 4 and every item a one-launch decode)",
+                    (long long)N);
+    hipError_t e = gq::launch_decode_grouped(di, m, N, (hipStream_t)stream);
+    if (e == hipErrorInvalidValue) return fail(GQ_EUNSUPPORTED, "grouped decode: more than 16 parts");
+    if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (grouped decode): %s", hipGetErrorString(e));
+    return GQ_OK;
+}
+
 int gq_mmq_sharded(gq_type t, const void *A_shard, const void *B, void *C, int64_t M, int64_t N, int64_t K,
                    int64_t ldb, int64_t ldc, int world, int rank, void *nccl_comm, void *workspace,
                    size_t workspace_bytes, void *stream)

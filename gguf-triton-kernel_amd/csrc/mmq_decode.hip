@@ -147,22 +147,24 @@ __device__ __forceinline__ void act_from_lds(Act<F, NT> &a, const uint8_t *codes
 // ITC > 0: the lane's activations for its units u = (lane % P) + P*i, i < ITC, are loaded from
 // the LDS image once and kept in registers (every row multiplies the same units); ITC == 0:
 // read from LDS per unit.
+// The kernel body for one matrix: workgroup bx of gx over the matrix's row groups, token group by
+// (stream_decode_kernel: the grid itself; stream_decode_grouped_kernel: a slice of a grid shared
+// by several matrices).  A row's arithmetic depends on F, NT and K only -- not on bx, gx or the
+// geometry's rows per task -- so a matrix computed inside a group gives the same bits as alone.
 template <int F, int NT, int ITC>
-__global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *__restrict__ A,
-                                                                const uint16_t *__restrict__ X, int64_t ldx,
-                                                                uint16_t *__restrict__ C, int M, int64_t N, int K,
-                                                                int64_t ldc, DecodeGeom geo)
+__device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X, int64_t ldx,
+                                            uint16_t *__restrict__ C, int M, int64_t N, int K, int64_t ldc,
+                                            DecodeGeom geo, int bx, int gx, int by, uint8_t *smem)
 {
     using L = Layout<F>;
     constexpr int UPC = UPC_OF<F, NT>;
-    extern __shared__ __attribute__((aligned(1024))) uint8_t smem[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 #ifdef GQ_DECODE_STAMPS
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
     unsigned long long t_wait = 0, t_w0 = 0, t_c0 = 0;
 #endif
-    const int64_t tok0 = (int64_t)blockIdx.y * NT;
+    const int64_t tok0 = (int64_t)by * NT;
     const int nb = K / 32;
     const int kp = (K + 63) / 64 * 64;
     const uint32_t RB = (uint32_t)(K / L::QK) * L::BYTES;
@@ -177,8 +179,8 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
         __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, (int)(((uint32_t)M * RB + 15u) & ~15u), 0x00020000);
 
     // this wave's contiguous range of row groups, and its task count
-    const int W = (int)gridDim.x * DW;
-    const int gw = (int)blockIdx.x * DW + wave;
+    const int W = gx * DW;
+    const int gw = bx * DW + wave;
     const int per = geo.ngroups / W, rem = geo.ngroups % W;
     const int g_begin = gw * per + (gw < rem ? gw : rem);
     const int ntask = (per + (gw < rem ? 1 : 0)) * geo.nseg;
@@ -491,8 +493,8 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
     if (ntask == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifdef GQ_DECODE_STAMPS
     const unsigned long long t_end = __builtin_amdgcn_s_memtime();
-    const int gw_id = blockIdx.x * DW + wave;
-    if (lane == 0 && gw_id < 65536 && blockIdx.y == 0) {
+    const int gw_id = bx * DW + wave;
+    if (lane == 0 && gw_id < 65536 && by == 0) {
         g_dstamps[gw_id][0] = t_pro - t_start;
         g_dstamps[gw_id][1] = t_wait;
         g_dstamps[gw_id][2] = t_end - t_pro;
@@ -504,9 +506,19 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *_
         g_dstamps[gw_id][8] = t_w0;
         g_dstamps[gw_id][9] = t_c0 ? t_c0 : t_end;
         g_dstamps[gw_id][10] = t_pro;
-        g_dstamps[gw_id][11] = (unsigned long long)blockIdx.x;
+        g_dstamps[gw_id][11] = (unsigned long long)bx;
     }
 #endif
+}
+
+template <int F, int NT, int ITC>
+__global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *__restrict__ A,
+                                                                const uint16_t *__restrict__ X, int64_t ldx,
+                                                                uint16_t *__restrict__ C, int M, int64_t N, int K,
+                                                                int64_t ldc, DecodeGeom geo)
+{
+    extern __shared__ __attribute__((aligned(1024))) uint8_t smem[];
+    decode_body<F, NT, ITC>(A, X, ldx, C, M, N, K, ldc, geo, (int)blockIdx.x, (int)gridDim.x, (int)blockIdx.y, smem);
 }
 
 struct Pick {
@@ -528,7 +540,9 @@ int64_t row_bytes(int fmt, int64_t K)
     return fmt == Q8_0 ? K / 32 * 34 : (fmt == Q4_K ? K / 256 * 144 : K / 256 * 210);
 }
 
-bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p)
+// share: the fraction of the chip's waves the matrix gets (1: a launch of its own; a grouped
+// launch splits the chip by weight bytes)
+bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p, double share = 1.0)
 {
     // at most 4 tokens per workgroup (NT = 8 spills registers); N = 5..8 runs two token groups,
     // whose second pass over the weights is served largely by the Infinity Cache
@@ -555,7 +569,8 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p)
     const int64_t cpr = upr / upc_of(fmt, p.nt); // lane chunks per row
     const int64_t cap = NI * 1024 - 16;
     const int per_cu = (int)(LDS_CAP / p.lds) > 0 ? (int)(LDS_CAP / p.lds) : 1;
-    const int64_t W = (int64_t)256 * per_cu * DW; // waves the chip holds
+    int64_t W = (int64_t)256 * per_cu * DW; // waves the chip holds (its share of them)
+    if (share < 1.0) W = (int64_t)(W * share) > DW ? (int64_t)(W * share) : DW;
     DecodeGeom &g = p.geo;
     if (RB <= cap) {
         const int64_t gmax = cap / RB;
@@ -651,6 +666,75 @@ hipError_t launch_f(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *
     return hipErrorInvalidValue;
 }
 
+// ---- grouped decode: several matrices (own type, activations, output) in one launch ----
+constexpr int kMaxGroup = 16;
+struct GroupedProblem {
+    const uint8_t *A;
+    const uint16_t *X;
+    int64_t ldx;
+    uint16_t *C;
+    int64_t ldc;
+    int M, K;
+    DecodeGeom geo;
+    int code;       // fmt * 16 + itc
+    int block0, gx; // this (problem, token group)'s workgroups: [block0, block0 + gx)
+    int by;         // its token group
+};
+struct GroupedArgs {
+    int n;
+    int64_t N;
+    GroupedProblem p[kMaxGroup];
+};
+
+template <int NT>
+__global__ __launch_bounds__(DW * 64) void stream_decode_grouped_kernel(const GroupedArgs args)
+{
+    extern __shared__ __attribute__((aligned(1024))) uint8_t smem[];
+    const int b = (int)blockIdx.x;
+    int i = 0;
+    while (i + 1 < args.n && b >= args.p[i + 1].block0) ++i;
+    const GroupedProblem &q = args.p[i];
+    const int bx = b - q.block0;
+#define GQ_GB(f, itc)                                                                                                 \
+    case f * 16 + itc:                                                                                                 \
+        decode_body<f, NT, itc>(q.A, q.X, q.ldx, q.C, q.M, args.N, q.K, q.ldc, q.geo, bx, q.gx, q.by, smem);         \
+        return;
+    if constexpr (NT == 1) {
+        switch (q.code) {
+            GQ_GB(Q8_0, 0) GQ_GB(Q8_0, 1) GQ_GB(Q8_0, 2) GQ_GB(Q8_0, 3) GQ_GB(Q8_0, 4) GQ_GB(Q8_0, 5) GQ_GB(Q8_0, 6)
+            GQ_GB(Q8_0, 7) GQ_GB(Q4_K, 0) GQ_GB(Q4_K, 1) GQ_GB(Q4_K, 2) GQ_GB(Q4_K, 3) GQ_GB(Q4_K, 4) GQ_GB(Q4_K, 5)
+            GQ_GB(Q4_K, 6) GQ_GB(Q4_K, 7) GQ_GB(Q6_K, 0) GQ_GB(Q6_K, 1) GQ_GB(Q6_K, 2) GQ_GB(Q6_K, 3) GQ_GB(Q6_K, 4)
+        default: return;
+        }
+    } else if constexpr (NT == 2) {
+        switch (q.code) {
+            GQ_GB(Q8_0, 0) GQ_GB(Q8_0, 1) GQ_GB(Q8_0, 2) GQ_GB(Q8_0, 3) GQ_GB(Q8_0, 4) GQ_GB(Q4_K, 0) GQ_GB(Q4_K, 1)
+            GQ_GB(Q4_K, 2) GQ_GB(Q4_K, 3) GQ_GB(Q4_K, 4) GQ_GB(Q6_K, 0) GQ_GB(Q6_K, 1)
+        default: return;
+        }
+    } else {
+        switch (q.code) {
+            GQ_GB(Q8_0, 0) GQ_GB(Q8_0, 1) GQ_GB(Q4_K, 0) GQ_GB(Q4_K, 1) GQ_GB(Q6_K, 0) GQ_GB(Q6_K, 1)
+        default: return;
+        }
+    }
+#undef GQ_GB
+}
+
+template <int NT>
+hipError_t launch_grouped_nt(GroupedArgs &a, int blocks, size_t lds, hipStream_t s)
+{
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void *)stream_decode_grouped_kernel<NT>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, LDS_CAP);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    stream_decode_grouped_kernel<NT><<<dim3((unsigned)blocks), dim3(DW * 64), lds, s>>>(a);
+    return hipGetLastError();
+}
+
 } // namespace
 
 bool decode_fused_ok(int fmt, int64_t N, int64_t K)
@@ -679,6 +763,71 @@ hipError_t launch_decode_fused(int fmt, const uint8_t *A, const uint16_t *X, int
         case Q4_K: e = launch_f<Q4_K>(A + m0 * RB, X, ldx, C + m0, m, N, K, ldc, p, s); break;
         default: e = launch_f<Q6_K>(A + m0 * RB, X, ldx, C + m0, m, N, K, ldc, p, s); break;
         }
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+bool decode_grouped_ok(const DecodeItem *items, int n, int64_t N)
+{
+    if (n < 1 || n > kMaxGroup || N < 1 || N > 4) return false;
+    for (int i = 0; i < n; ++i) {
+        const DecodeItem &it = items[i];
+        if (it.M < 1 || !decode_fused_ok(it.fmt, N, it.K)) return false;
+        if (it.M * row_bytes(it.fmt, it.K) >= ((int64_t)1 << 31)) return false; // 32-bit buffer offsets
+    }
+    return true;
+}
+
+hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipStream_t s)
+{
+    if (!decode_grouped_ok(items, n, N)) return hipErrorInvalidValue;
+    // every item's token tile as a launch of its own would pick it (bit-identical rows); one
+    // launch per distinct tile (a Q6_K long-K item caps it at 2 tokens, so 3-4 tokens can take two)
+    Pick solo[kMaxGroup];
+    double bytes[kMaxGroup], total = 0;
+    for (int i = 0; i < n; ++i) {
+        if (!pick(items[i].fmt, items[i].M, N, items[i].K, solo[i])) return hipErrorInvalidValue;
+        const int tg = (int)((N + solo[i].nt - 1) / solo[i].nt);
+        bytes[i] = (double)items[i].M * (double)row_bytes(items[i].fmt, items[i].K) * tg;
+        total += bytes[i];
+    }
+    for (int nt : {1, 2, 4}) {
+        GroupedArgs a{};
+        a.N = N;
+        size_t lds = 0;
+        int blocks = 0, np = 0;
+        for (int i = 0; i < n; ++i) {
+            if (solo[i].nt != nt) continue;
+            // the chip's waves split by weight bytes (all parts finish together)
+            Pick p;
+            if (!pick(items[i].fmt, items[i].M, N, items[i].K, p, bytes[i] / total) || p.nt != nt)
+                return hipErrorInvalidValue;
+            const int tg = (int)((N + nt - 1) / nt);
+            for (int y = 0; y < tg; ++y) {
+                if (np == kMaxGroup) return hipErrorInvalidValue;
+                GroupedProblem &q = a.p[np++];
+                q.A = items[i].A;
+                q.X = items[i].X;
+                q.ldx = items[i].ldx;
+                q.C = items[i].C;
+                q.ldc = items[i].ldc;
+                q.M = (int)items[i].M;
+                q.K = (int)items[i].K;
+                q.geo = p.geo;
+                q.code = items[i].fmt * 16 + p.itc;
+                q.block0 = blocks;
+                q.gx = p.grid;
+                q.by = y;
+                blocks += p.grid;
+                lds = p.lds > lds ? p.lds : lds;
+            }
+        }
+        if (np == 0) continue;
+        a.n = np;
+        hipError_t e = nt == 1   ? launch_grouped_nt<1>(a, blocks, lds, s)
+                       : nt == 2 ? launch_grouped_nt<2>(a, blocks, lds, s)
+                                 : launch_grouped_nt<4>(a, blocks, lds, s);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;

@@ -24,6 +24,15 @@ BLOCK_BYTES = {GQ_Q8_0: 34, GQ_Q4_K: 144, GQ_Q6_K: 210}
 
 # symbol -> (argtypes, restype); mirrors include/gguf_mmq.h
 _P, _I64, _I, _SZ = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_size_t
+GQ_OK, GQ_EINVAL, GQ_EHIP, GQ_EUNSUPPORTED = 0, 1, 2, 3
+
+
+class GroupItem(ctypes.Structure):
+    """gq_group_item (include/gguf_mmq.h)."""
+    _fields_ = [("type", ctypes.c_int), ("A", _P), ("B", _P), ("ldb", _I64), ("C", _P), ("ldc", _I64),
+                ("M", _I64), ("K", _I64)]
+
+
 SIGNATURES = {
     "gq_block_elems": ([_I], _I),
     "gq_block_bytes": ([_I], _I),
@@ -43,6 +52,7 @@ SIGNATURES = {
     "gq_assemble_shards": ([_P, _P, _I, _I64, _I64, _I64, _I64, _P], _I),
     "gq_mmq_sharded_workspace_size": ([_I, _I64, _I64, _I64, _I], _SZ),
     "gq_mmq_sharded": ([_I, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _I, _P, _P, _SZ, _P], _I),
+    "gq_mmq_grouped": ([ctypes.POINTER(GroupItem), _I, _I64, _P], _I),
     "gq_last_error": ([], ctypes.c_char_p),
     "gq_version": ([], _I),
     "gq_debug_set_tuning": ([ctypes.c_char_p, ctypes.c_longlong], _I),
@@ -173,6 +183,34 @@ def mmq(gtype: int, A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int,
         _check(lib().gq_mmq_ex(gtype, ACTS[act], A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, B.stride(0),
                                C.stride(0), workspace.data_ptr(), workspace.numel(), stream))
     return C
+
+
+def mmq_grouped(items, N: int):
+    """One grouped decode launch (gq_mmq_grouped) for several MMQs with the same token count N
+    (1..4): items = [(gtype, A, B, M, K, out or None), ...], every B an fp16 (N, K) tensor.
+    Returns the (N, M) outputs (bit-identical to mmq() per item), or None when the library
+    reports the shapes unsupported (N > 4, or an item that is no one-launch decode shape) --
+    nothing was launched then and the caller runs mmq() per item."""
+    if not items:
+        return []
+    dev = items[0][1].device
+    arr = (GroupItem * len(items))()
+    outs, keep = [], []
+    for i, (gtype, A, B, M, K, out) in enumerate(items):
+        _check_weights(gtype, A, M, K)
+        if A.device != dev or B.device != dev:
+            raise RuntimeError("grouped items must share one device")
+        B = _check_acts(B, N, K)
+        C = _check_out(out, N, M, dev)
+        keep.append(B)
+        outs.append(C)
+        arr[i] = GroupItem(gtype, A.data_ptr(), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, K)
+    with torch.cuda.device(dev):
+        rc = lib().gq_mmq_grouped(arr, len(items), N, torch.cuda.current_stream(dev).cuda_stream)
+    if rc == GQ_EUNSUPPORTED:
+        return None
+    _check(rc)
+    return outs
 
 
 def quantize_q8_1_device(X: torch.Tensor) -> torch.Tensor:

@@ -8,8 +8,14 @@ copied end to end into one device buffer (the bytes are unchanged -- a packed ro
 blocks), so each such set is ONE call (one activation quantization, one launch, the split-K
 plan of the taller matrix) whose (N, sum M) output is returned as per-projection column views.
 Sets that share an input but differ in type quantize the input once (gq_act_prepare) and run
-gq_mmq_prepared per weight; at decode sizes (N <= 4) every call is the one-launch fused decode
-kernel (its quantizer is in-kernel).
+gq_mmq_prepared per weight.  At one token (q8_1 activations) every call of the layer goes into
+ONE grouped decode launch (gq_mmq_grouped: the chip's waves split over the matrices by weight
+bytes, each matrix's rows bit-identical to its own call).  Measured (Q4_K_M 7B layer 0,
+profiles/r03/grouped_decode.txt): 45 us graph-replayed, level with the five launches of the
+fused sets (44) and 16% under seven unfused ones (54) -- the decode kernel is bound by its
+per-wave DMA latency, not by launch ramps -- but one host call instead of five for eager
+callers; at 2 tokens the grouped launch measured slower (68 vs 53 us), so grouped="auto" takes
+it at one token only (True: 1..4 tokens, False: never).
 """
 from __future__ import annotations
 
@@ -41,8 +47,10 @@ class LayerMix:
 
     GROUPS = (("attn_q", "attn_k", "attn_v"), ("attn_output",), ("ffn_gate", "ffn_up"), ("ffn_down",))
 
-    def __init__(self, linears: dict, act: str = "q8_1", fuse: bool = True):
+    def __init__(self, linears: dict, act: str = "q8_1", fuse: bool = True, grouped="auto"):
         self.act = act  # "q8_1" (the reference's activation quantization) or "fp8" (e4m3 variant)
+        # one gq_mmq_grouped launch for the whole layer: "auto" at 1 token, True at 1..4, False never
+        self.max_grouped = {"auto": 1, True: 4, False: 0}[grouped]
         self.lin = {}     # name -> GGUFLinear (unfused projections)
         self.parts = {}   # name -> (fused key, first column, rows)
         # per input group: the calls to make, each (key, GGUFLinear); fused keys join names by "+"
@@ -71,7 +79,8 @@ class LayerMix:
         self._fused_out = {}
 
     @classmethod
-    def from_gguf(cls, tensors: dict, layer: int, device="cuda", act: str = "q8_1", fuse: bool = True):
+    def from_gguf(cls, tensors: dict, layer: int, device="cuda", act: str = "q8_1", fuse: bool = True,
+                  grouped="auto"):
         """From read_gguf() tensors named blk.<layer>.<proj>.weight."""
         lins = {}
         for group in cls.GROUPS:
@@ -79,7 +88,7 @@ class LayerMix:
                 t = tensors[f"blk.{layer}.{name}.weight"]
                 M, K = t.shape
                 lins[name] = GGUFLinear(t.type_name, t.to_device(device), M, K)
-        return cls(lins, act, fuse)
+        return cls(lins, act, fuse, grouped)
 
     def _out(self, key, L, N, dev, out):
         """Output buffer of one call: the caller's for an unfused projection, else ours."""
@@ -91,29 +100,48 @@ class LayerMix:
             self._fused_out[key] = buf
         return buf
 
-    def forward(self, x: torch.Tensor, h: torch.Tensor, attn: torch.Tensor | None = None,
+    def forward(self, x: torch.Tensor, h: torch.Tensor, *, attn: torch.Tensor | None = None,
                 x_ffn: torch.Tensor | None = None, out: dict | None = None) -> dict:
-        """{name: (N, M) fp16}.  Fused projections come back as column views of their set's
-        (N, sum M) output (kept by the layer and rewritten by the next forward); `out` supplies
-        the buffers of unfused ones."""
+        """{name: (N, M) fp16}.  Fused projections are computed as column ranges of their set's
+        (N, sum M) output (kept by the layer and rewritten by the next forward) and returned as
+        views of it -- or copied into out[name] when `out` supplies that name's buffer; unfused
+        ones are written into out[name] directly when given."""
         res = {}
         inputs = (x, x if attn is None else attn, x if x_ffn is None else x_ffn, h)
-        for calls, inp in zip(self.calls, inputs):
-            N, K = inp.shape
-            if (N <= 4 and self.act == "q8_1") or len(calls) == 1:
-                # decode (each call quantizes its tokens in-kernel), or a single call
+        done = False
+        if (self.act == "q8_1" and x.shape[0] <= self.max_grouped
+                and all(inp.shape[0] == x.shape[0] for inp in inputs)):
+            N = x.shape[0]
+            keys, items = [], []
+            for calls, inp in zip(self.calls, inputs):
                 for key, L in calls:
-                    res[key] = _lib.mmq(L.gtype, L.A, inp, L.M, N, K, out=self._out(key, L, N, inp.device, out),
-                                        act=self.act)
-            else:
-                ws_bytes = max(L.workspace_bytes(N, self.act) for _, L in calls)
-                ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=inp.device)
-                _lib.act_prepare(inp, N, K, ws, act=self.act)
-                for key, L in calls:
-                    res[key] = _lib.mmq_prepared(L.gtype, L.A, ws, L.M, N, K, self._out(key, L, N, inp.device, out),
-                                                 act=self.act)
+                    keys.append(key)
+                    items.append((L.gtype, L.A, inp, L.M, inp.shape[1], self._out(key, L, N, inp.device, out)))
+            outs = _lib.mmq_grouped(items, N)
+            if outs is not None:
+                res.update(zip(keys, outs))
+                done = True
+        if not done:
+            for calls, inp in zip(self.calls, inputs):
+                N, K = inp.shape
+                if (N <= 4 and self.act == "q8_1") or len(calls) == 1:
+                    # decode (each call quantizes its tokens in-kernel), or a single call
+                    for key, L in calls:
+                        res[key] = _lib.mmq(L.gtype, L.A, inp, L.M, N, K, out=self._out(key, L, N, inp.device, out),
+                                            act=self.act)
+                else:
+                    ws_bytes = max(L.workspace_bytes(N, self.act) for _, L in calls)
+                    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=inp.device)
+                    _lib.act_prepare(inp, N, K, ws, act=self.act)
+                    for key, L in calls:
+                        res[key] = _lib.mmq_prepared(L.gtype, L.A, ws, L.M, N, K,
+                                                     self._out(key, L, N, inp.device, out), act=self.act)
         for n, (key, col, rows) in self.parts.items():
-            res[n] = res[key][:, col:col + rows]
+            view = res[key][:, col:col + rows]
+            if out is not None and n in out:
+                out[n].copy_(view)
+                view = out[n]
+            res[n] = view
         for key in [k for k in res if "+" in k]:
             del res[key]
         return res

@@ -145,6 +145,30 @@ int gq_mmq_sharded(gq_type t, const void *A_shard, const void *B, void *C, int64
                    int64_t ldb, int64_t ldc, int world, int rank, void *nccl_comm, void *workspace,
                    size_t workspace_bytes, void *stream);
 
+/*
+ * Grouped decode: several MMQs of the same token count N (1..4) in one launch, e.g. the
+ * projections of one transformer block at decode time.  The reference has no counterpart (its
+ * kernels/mmq_*.py take one matrix per call); this is the launch the layer dispatcher
+ * (kernels/layer_mix.py) makes at 1..4 tokens.  Item i: weights A (M x K of
+ * `type`), fp16 activations B (N x K, row stride ldb, q8_1-quantized in the kernel as gq_mmq
+ * does), fp16 output C (N x M, row stride ldc); items may share B.  Every item's output is
+ * bit-identical to its own gq_mmq call.  The chip's waves are split over the items by weight
+ * bytes.  No workspace, no host sync.  GQ_EUNSUPPORTED (nothing launched) when N > 4, or when an
+ * item is not a decode shape for the one-launch kernel (its activations do not fit LDS, or
+ * >= 2 GiB of weights), or when the items need more than 16 parts (item x token group):
+ * call gq_mmq per item then.
+ */
+typedef struct gq_group_item {
+    gq_type type;
+    const void *A;
+    const void *B;
+    int64_t ldb;
+    void *C;
+    int64_t ldc;
+    int64_t M, K;
+} gq_group_item;
+int gq_mmq_grouped(const gq_group_item *items, int n, int64_t N, void *stream);
+
 /* Text of the last error on this thread ("" if none). */
 const char *gq_last_error(void);
 

@@ -156,3 +156,26 @@ def test_sharded_workspace_covers_every_rank(t, M, N, K):
             _, rows, R = shard_rows(M, world, g)
             local = kl.workspace_size(t, rows, N, K)  # (0 rows: an empty shard)
             assert need >= local + (world + 1) * N * R * 2, (world, g, need, local)
+
+
+def test_grouped_host_argument_checks():
+    """gq_mmq_grouped's argument checks, host-side (nothing launched, no device needed)."""
+    import ctypes
+
+    import kernels._lib as kl
+    L = kl.lib()
+    arr = (kl.GroupItem * 2)()
+    assert L.gq_mmq_grouped(None, 2, 1, None) == kl.GQ_EINVAL
+    assert L.gq_mmq_grouped(arr, 0, 1, None) == kl.GQ_OK          # nothing to do
+    assert L.gq_mmq_grouped(arr, 1, -1, None) == kl.GQ_EINVAL
+    fake = ctypes.c_void_p(0x1000).value
+    arr[0] = kl.GroupItem(kl.GQ_Q4_K, fake, fake, 4096, fake, 4096, 4096, 4096)
+    arr[1] = kl.GroupItem(kl.GQ_Q4_K, fake, fake, 100, fake, 4096, 4096, 4096)  # ldb < K
+    assert L.gq_mmq_grouped(arr, 2, 1, None) == kl.GQ_EINVAL
+    assert b"ldb" in L.gq_last_error()
+    arr[1] = kl.GroupItem(7, fake, fake, 4096, fake, 4096, 4096, 4096)           # unknown type
+    assert L.gq_mmq_grouped(arr, 2, 1, None) != kl.GQ_OK
+    arr[1] = kl.GroupItem(kl.GQ_Q4_K, fake, fake, 4096, fake, 4096, 0, 4096)     # M = 0: skipped
+    assert L.gq_mmq_grouped(arr, 2, 5, None) == kl.GQ_EUNSUPPORTED              # N = 5: not decode
+    arr[1] = kl.GroupItem(kl.GQ_Q4_K, None, fake, 4096, fake, 4096, 64, 4096)    # null A
+    assert L.gq_mmq_grouped(arr, 2, 1, None) == kl.GQ_EINVAL

@@ -1,0 +1,146 @@
+"""GPU tests of the grouped decode launch (gq_mmq_grouped, csrc/mmq_decode.hip
+stream_decode_grouped_kernel): several matrices of their own types, activations and outputs in
+one launch at 1..4 tokens.  Each projection vs the oracle (sampled rows, IDEAL at the decode
+tolerance and the reference's 1% gate vs EXACT) and bit for bit vs its own gq_mmq call; the
+Llama-7B Q4_K_M layer through LayerMix grouped and ungrouped; what is not a grouped shape is
+refused without launching."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from utils.synth import random_activations, random_blocks
+
+pytestmark = pytest.mark.gpu
+
+TIGHT_DEC = 3e-3  # int8 x int8 dots, fp32 block scaling: vs IDEAL (as tests/test_gpu_parity.py)
+
+
+def _dev():
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    return torch.device("cuda:0")
+
+
+def _layer(types, seed=0):
+    from gguf import LLAMA_LAYER_SHAPES
+    dev = _dev()
+    raw = {n: random_blocks(types[n], M, K, seed=seed + i) for i, (n, (M, K)) in enumerate(LLAMA_LAYER_SHAPES.items())}
+    dev_w = {n: torch.from_numpy(raw[n].view(np.int8)).to(dev) for n in raw}
+    return raw, dev_w
+
+
+@pytest.mark.parametrize("N", [1, 2, 3, 4])
+@pytest.mark.parametrize("layer", [0, 5])
+def test_grouped_llama_layer_bitexact(N, layer):
+    """The seven Llama-7B projections (Q4_K_M types of layer `layer`; layer 0: attn_v and
+    ffn_down in Q6_K) in one grouped call: every output bit-identical to its own mmq() call, and
+    sampled rows against the oracle.  At 3-4 tokens a Q4_K ffn_down (K = 11008) has no one-launch
+    decode form (its 4 tokens' activations do not fit LDS beside the ring; its own call is the
+    GEMV path), so layer 5's group is refused there."""
+    import kernels._lib as kl
+    from gguf import LLAMA_LAYER_SHAPES, q4_k_m_layer_types
+    dev = _dev()
+    types = q4_k_m_layer_types(layer, 32)
+    raw, A = _layer(types, seed=100 * layer)
+    x = random_activations(N, 4096, seed=1 + N)
+    h = random_activations(N, 11008, seed=2 + N)
+    xt, ht = torch.from_numpy(x).to(dev), torch.from_numpy(h).to(dev)
+    items, names = [], []
+    for n, (M, K) in LLAMA_LAYER_SHAPES.items():
+        names.append(n)
+        items.append((kl.TYPES[types[n]], A[n], ht if K == 11008 else xt, M, K, None))
+    outs = kl.mmq_grouped(items, N)
+    if N >= 3 and types["ffn_down"] == "q4_k":
+        assert outs is None
+        return
+    assert outs is not None, kl.lib().gq_last_error()
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(N)
+    for n, C in zip(names, outs):
+        M, K = LLAMA_LAYER_SHAPES[n]
+        solo = kl.mmq(kl.TYPES[types[n]], A[n], ht if K == 11008 else xt, M, N, K)
+        torch.cuda.synchronize()
+        assert torch.equal(C.view(torch.int16), solo.view(torch.int16)), n
+        rows = np.sort(rng.choice(M, size=24, replace=False))
+        rb = raw[n].size // M
+        sub = np.concatenate([raw[n][r * rb:(r + 1) * rb] for r in rows])
+        B = h if K == 11008 else x
+        got = C.cpu().numpy()[:, rows]
+        ideal = O.mmq_from_fp16(types[n], sub, B, len(rows), N, K, O.IDEAL)
+        assert O.max_rel_err(got, ideal) <= TIGHT_DEC, n
+        exact = O.mmq_from_fp16(types[n], sub, B, len(rows), N, K, O.EXACT)
+        assert O.allclose(exact, got, 0.01), n
+
+
+def test_grouped_mixed_formats_strides():
+    """Q8_0, Q4_K and Q6_K items with ragged rows, K not a multiple of 256 (Q8_0), a shared
+    activation tensor, a strided activation view and outputs written into column ranges of one
+    wide buffer (ldc > M): bit-identical to the per-item calls, nothing outside the ranges touched."""
+    import kernels._lib as kl
+    dev = _dev()
+    N = 3
+    specs = [("q8_0", 333, 1056), ("q4_k", 1000, 2048), ("q6_k", 257, 1536), ("q4_k", 64, 2048), ("q8_0", 4096, 4096)]
+    X = {K: torch.from_numpy(random_activations(N, K, seed=K)).to(dev) for K in {s[2] for s in specs}}
+    wide = torch.from_numpy(random_activations(N, 2 * 2048, seed=7)).to(dev)
+    X[2048] = wide[:, 1000:1000 + 2048]  # row stride 4096
+    width = sum(M for _, M, _ in specs) + 5
+    buf = torch.full((N, width), -7.0, dtype=torch.float16, device=dev)
+    items, col = [], 0
+    qs = []
+    for i, (fmt, M, K) in enumerate(specs):
+        qA = torch.from_numpy(random_blocks(fmt, M, K, seed=i).view(np.int8)).to(dev)
+        qs.append(qA)
+        items.append((kl.TYPES[fmt], qA, X[K], M, K, buf[:, col:col + M]))
+        col += M
+    outs = kl.mmq_grouped(items, N)
+    assert outs is not None, kl.lib().gq_last_error()
+    torch.cuda.synchronize()
+    col = 0
+    for (fmt, M, K), qA in zip(specs, qs):
+        solo = kl.mmq(kl.TYPES[fmt], qA, X[K], M, N, K)
+        torch.cuda.synchronize()
+        assert torch.equal(buf[:, col:col + M].view(torch.int16), solo.view(torch.int16)), fmt
+        col += M
+    assert torch.all(buf[:, col:] == -7.0)
+
+
+def test_grouped_refuses_non_decode_shapes():
+    """N = 5 (not a decode size) and an item whose activations do not fit LDS: refused (None),
+    nothing launched, the output untouched; mmq() per item is the caller's path then."""
+    import kernels._lib as kl
+    dev = _dev()
+    qA = torch.from_numpy(random_blocks("q4_k", 64, 1024, seed=1).view(np.int8)).to(dev)
+    for N, K in ((5, 1024),):
+        B = torch.from_numpy(random_activations(N, K, seed=2)).to(dev)
+        out = torch.full((N, 64), 3.0, dtype=torch.float16, device=dev)
+        assert kl.mmq_grouped([(kl.GQ_Q4_K, qA, B, 64, K, out)], N) is None
+        torch.cuda.synchronize()
+        assert torch.all(out == 3.0)
+    K = 131072  # 4 tokens x 128K codes: no room in LDS beside the ring
+    qB = torch.from_numpy(random_blocks("q8_0", 16, K, seed=3).view(np.int8)).to(dev)
+    B = torch.from_numpy(random_activations(4, K, seed=4)).to(dev)
+    assert kl.mmq_grouped([(kl.GQ_Q8_0, qB, B, 16, K, None)], 4) is None
+
+
+@pytest.mark.parametrize("N", [1, 2, 4])
+def test_layer_mix_grouped_matches_ungrouped(N):
+    """LayerMix at decode sizes: the grouped launch (default) gives the same bits as one call per
+    projection set; `out` buffers are honoured for fused projections too."""
+    from gguf import LLAMA_LAYER_SHAPES, q4_k_m_layer_types
+    from kernels.layer_mix import GGUFLinear, LayerMix
+    dev = _dev()
+    types = q4_k_m_layer_types(0, 32)
+    _, A = _layer(types, seed=3)
+    lins = {n: GGUFLinear(types[n], A[n], M, K) for n, (M, K) in LLAMA_LAYER_SHAPES.items()}
+    g, u = LayerMix(lins, grouped=True), LayerMix(lins, grouped=False)  # (True: grouped at 1..4 tokens)
+    x = torch.from_numpy(random_activations(N, 4096, seed=5)).to(dev)
+    a = torch.from_numpy(random_activations(N, 4096, seed=6)).to(dev)
+    y = torch.from_numpy(random_activations(N, 4096, seed=7)).to(dev)
+    h = torch.from_numpy(random_activations(N, 11008, seed=8)).to(dev)
+    out = {n: torch.empty(N, M, dtype=torch.float16, device=dev) for n, (M, K) in LLAMA_LAYER_SHAPES.items()}
+    rg = g.forward(x, h, attn=a, x_ffn=y, out=out)
+    ru = u.forward(x, h, attn=a, x_ffn=y)
+    torch.cuda.synchronize()
+    for n in LLAMA_LAYER_SHAPES:
+        assert rg[n].data_ptr() == out[n].data_ptr(), n
+        assert torch.equal(rg[n].view(torch.int16), ru[n].view(torch.int16)), n
