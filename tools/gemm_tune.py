@@ -31,14 +31,14 @@ if os.environ.get("GQ_TUNE_ROTATE"):  # weight-rotation bytes (default bench.ROT
     bench.ROTATE_BYTES = int(os.environ["GQ_TUNE_ROTATE"])
 
 dev = torch.device("cuda:0")
-KEYS = ("GQ_ABLATE", "GQ_GEMV_R", "GQ_GEMV_CAP", "GQ_GEMM_AQ_NB4", "GQ_GEMM_AQ", "GQ_DECODE_NT4_CACHE", "GQ_DECODE_MAXNT", "GQ_DECODE_WIDE_ROWS", "GQ_GEMM_I8", "GQ_GEMM_LOADERS", "GQ_GEMM_PARTIAL", "GQ_GEMM_RG", "GQ_GEMM_NB", "GQ_GEMM_SPLITS", "GQ_DECODE_CAP", "GQ_NO_FUSED_DECODE", "GQ_DECODE_NI", "GQ_DECODE_NS", "GQ_BLAS_MIN_TOKENS")
 for spec in args:
+    # overrides through the library's tuning entry point (the GQ_* environment is read once, at
+    # the first call, so setting os.environ here would not reach later specs)
     cfg, _, envs = spec.partition(":")
-    for k in KEYS:
-        os.environ.pop(k, None)
+    kl.reset_tuning()
     for kv in filter(None, envs.split(",")):
         k, v = kv.split("=")
-        os.environ[k] = v
+        kl.set_tuning(k, int(v))
     if cfg in bench.CONFIGS:
         fmt, M, K, N = bench.CONFIGS[cfg]
     else:  # fmt_MxK_mN, e.g. q4_k_28672x8192_m128

@@ -11,6 +11,9 @@
 #                                           (VARIANTS / CONFIGS: names in tools/wgemm_check.py)
 #   bash tools/gpu.sh ab SPEC...            interleaved A/B of tools/gemm_tune.py specs (AB_R rounds)
 #   bash tools/gpu.sh dist                  bench.py's N > 1 path at world 1 over RCCL (BENCH_FORCE_DIST)
+#   bash tools/gpu.sh round                 round-end measurements: FETCH_SIZE traffic per config (read by
+#                                           bench.py into roofline.traffic), the PMC passes of the shipping
+#                                           kernels, the default bench line, and rocprofv3 stats of that command
 #
 # Every GPU step runs under its own timeout; a failing step ends the script.
 set -u
@@ -66,6 +69,17 @@ for k, v in d.items(): print(f'{k:60s} min={min(v):7.2f} med={sorted(v)[len(v)//
 " ;;
 dist)
   BENCH_FORCE_DIST=1 timeout -k 10 400 python -u bench.py --steps ${STEPS:-50} --warmup 5 ;;
+round)
+  TCFGS=${TCFGS:-"q8_0_4096x4096_m128 q8_0_4096x4096_m1 q4_k_4096x4096_m1 q4_k_4096x4096_m16 q4_k_4096x4096_m128 q4_k_11008x4096_m1 q4_k_11008x4096_m16 q4_k_11008x4096_m128 q4_k_4096x11008_m1 q4_k_4096x11008_m128 q6_k_28672x8192_m1 q6_k_28672x8192_m128 q6_k_8192x28672_m1 q6_k_8192x28672_m128"}
+  PCFGS=${PCFGS:-"q8_0_4096x4096_m128 q4_k_4096x11008_m128 q6_k_28672x8192_m128 q4_k_11008x4096_m16"}
+  timeout -k 10 600 python3 tools/pmc_traffic.py $TCFGS > gpurun_out/round_traffic.log 2>&1 &&
+  PASSES="FETCH_SIZE|SQ_VALU_MFMA_BUSY_CYCLES,SQ_BUSY_CYCLES,GRBM_GUI_ACTIVE|TA_BUSY_avr,TCC_HIT_sum,TCC_MISS_sum|SQ_INSTS_LDS,SQ_INSTS_VMEM_RD,SQ_INSTS_VALU,SQ_INSTS_MFMA" \
+    bash tools/gpu.sh pmc $PCFGS > gpurun_out/round_pmc.log 2>&1 &&
+  timeout -k 10 600 python3 -u bench.py > gpurun_out/round_bench.json 2> gpurun_out/round_bench.err &&
+  mkdir -p gpurun_out/round_prof && cd /tmp && export TMPDIR=/tmp &&
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/round_prof" -o run -- \
+    python3 "$ROOT/bench.py" > "$ROOT/gpurun_out/round_prof/bench.json" 2> "$ROOT/gpurun_out/round_prof/bench.err" &&
+  python3 "$ROOT/tools/kstats.py" "$ROOT/gpurun_out/round_prof/run_kernel_stats.csv" > "$ROOT/gpurun_out/round_prof/kstats.txt" ;;
 *)
   echo "unknown recipe: $cmd" >&2; exit 2 ;;
 esac

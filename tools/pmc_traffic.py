@@ -4,7 +4,7 @@ Usage (GPU box):  python tools/pmc_traffic.py [CONFIG ...]
 For each config: one `rocprofv3 --pmc FETCH_SIZE --kernel-trace` pass (its own run, nothing
 else collected) over `tools/gemm_tune.py --step CONFIG`, then
     hbm_bytes_per_launch = mean FETCH_SIZE (KiB) * 1024 * 2
-of the dominant kernel (decode: the fused stream kernel; GEMM: gemm_kernel), the factor 2
+of the dominant kernel (the step's matmul launch: the one fetching the most), the factor 2
 being MI355X_MICROARCH.md's gfx950 correction (FETCH_SIZE counts 64 B per 128-B request of
 a wide streaming read).  Writes profiles/pmc_<config>.json, which bench.py reads into
 roofline.traffic.
@@ -39,10 +39,13 @@ def run(cfg):
                 continue
             vals.setdefault(k, []).append(float(r["Counter_Value"]))
     fmt, M, K, N = bench.CONFIGS[cfg]
-    key = "stream_decode_kernel" if N <= 4 else "gemm_kernel"
-    dom = [k for k in vals if key in k]
-    if not dom:
-        raise SystemExit(f"{cfg}: no {key} dispatch in the PMC output")
+    # the dominant kernel: the step's matmul launch (decode, skinny, or either GEMM -- the
+    # library routes by type and token count), i.e. the gq kernel that fetches the most
+    # (not act_quant, not the split-K reduce)
+    main = {k: v for k, v in vals.items() if "act_quant" not in k and "reduce" not in k}
+    if not main:
+        raise SystemExit(f"{cfg}: no matmul dispatch in the PMC output")
+    dom = [max(main, key=lambda k: sum(main[k]) / len(main[k]))]
     v = vals[dom[0]]
     hbm = sum(v) / len(v) * 1024 * 2
     wbytes, alg, _ = bench.model(fmt, M, K, N)
