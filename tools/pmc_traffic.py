@@ -49,7 +49,8 @@ def run(cfg):
     v = vals[dom[0]]
     hbm = sum(v) / len(v) * 1024 * 2
     wbytes, alg, _ = bench.model(fmt, M, K, N)
-    rec = {"config": cfg, "kernel": dom[0].split("(")[0], "dispatches": len(v),
+    name = dom[0].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+    rec = {"config": cfg, "kernel": name, "dispatches": len(v),
            "fetch_size_kib_mean": sum(v) / len(v), "hbm_bytes_per_launch": hbm,
            "alg_bytes_per_launch": alg, "traffic_over_alg": hbm / alg,
            "method": "rocprofv3 --pmc FETCH_SIZE (own pass), x1024 x2 (gfx950 correction)"}
