@@ -137,3 +137,24 @@ def test_skinny_default_route(tune):
     ideal = O.mmq_from_fp16(fmt, qA, B, M, N, K, O.IDEAL)
     assert O.max_rel_err(a, ideal) <= TIGHT and O.max_rel_err(b, ideal) <= TIGHT
     assert not np.array_equal(a.view(np.uint16), b.view(np.uint16))
+
+
+@pytest.mark.parametrize("fmt", FMTS)
+def test_skinny_strided_activations(fmt, tune):
+    """A strided activation view (ldb > K) through gq_mmq gives the same bits as the contiguous
+    copy and as gq_act_prepare + gq_mmq_prepared."""
+    import kernels._lib as kl
+    tune(GQ_SKINNY=1)
+    dev = _dev()
+    M, N, K = 700, 12, 2048
+    qA = torch.from_numpy(random_blocks(fmt, M, K, seed=21).view(np.int8)).to(dev)
+    wide = torch.from_numpy(random_activations(N, K + 512, seed=22)).to(dev)
+    Bv = wide[:, 256:256 + K]
+    a = kl.mmq(kl.TYPES[fmt], qA, Bv, M, N, K)
+    b = kl.mmq(kl.TYPES[fmt], qA, Bv.contiguous(), M, N, K)
+    ws = torch.empty(kl.workspace_size(kl.TYPES[fmt], M, N, K), dtype=torch.uint8, device=dev)
+    kl.act_prepare(Bv.contiguous(), N, K, ws)
+    c = kl.mmq_prepared(kl.TYPES[fmt], qA, ws, M, N, K)
+    torch.cuda.synchronize()
+    assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+    assert torch.equal(a.view(torch.int16), c.view(torch.int16))
