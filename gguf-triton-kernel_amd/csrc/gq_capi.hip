@@ -311,6 +311,17 @@ size_t ws_bytes(int t, int act, int64_t M, int64_t N, int64_t K)
     return b;
 }
 
+// gq_mmq_ex takes the one-launch fused decode (no workspace) for this call
+bool fused_decode_route(int t, int act, int64_t N, int64_t K)
+{
+    return route(t, act, N, K).gemv && gq::decode_fused_ok(t, N, K) && gq::tuning().fused_decode;
+}
+// what a gq_mmq_ex call itself needs (gq_act_prepare / gq_mmq_prepared need ws_bytes)
+size_t call_ws_bytes(int t, int act, int64_t M, int64_t N, int64_t K)
+{
+    return fused_decode_route(t, act, N, K) ? 0 : ws_bytes(t, act, M, N, K);
+}
+
 // ---- row sharding (gq_mmq_sharded) ----
 constexpr int64_t kShardAlign = 64; // dist/row_shard.py shard_rows(align=64)
 
@@ -405,6 +416,11 @@ int gq_block_bytes(gq_type t) { return block_bytes(t); }
 int gq_version(void) { return 101; }
 const char *gq_last_error(void) { return g_err.c_str(); }
 
+size_t gq_mmq_call_workspace_size(gq_type t, gq_act act, int64_t M, int64_t N, int64_t K)
+{
+    if (N <= 0 || K <= 0 || M < 0) return 0;
+    return call_ws_bytes(t, act, M, N, K);
+}
 size_t gq_mmq_workspace_size_ex(gq_type t, gq_act act, int64_t M, int64_t N, int64_t K)
 {
     if (N <= 0 || K <= 0 || M < 0) return 0;
@@ -552,12 +568,12 @@ int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int6
     if (K == 0) return fail(GQ_EINVAL, "K must be positive");
     if (!A || !B || !C) return fail(GQ_EINVAL, "null pointer (A=%p B=%p C=%p)", A, B, C);
     if (ldc < M) return fail(GQ_EINVAL, "ldc=%lld < M=%lld", (long long)ldc, (long long)M);
-    const size_t need = ws_bytes(t, act, M, N, K);
-    if (!workspace || workspace_bytes < need)
-        return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace ? workspace_bytes : (size_t)0, need);
     if (ldb < K) return fail(GQ_EINVAL, "ldb=%lld < K=%lld", (long long)ldb, (long long)K);
+    const size_t need = call_ws_bytes(t, act, M, N, K);
+    if (need && (!workspace || workspace_bytes < need))
+        return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace ? workspace_bytes : (size_t)0, need);
     const Route r = route(t, act, N, K);
-    if (r.gemv && gq::decode_fused_ok(t, N, K) && gq::tuning().fused_decode) {
+    if (fused_decode_route(t, act, N, K)) {
         // one launch: activation quantization in LDS + decode GEMV
         hipError_t e = gq::launch_decode_fused(t, (const uint8_t *)A, (const uint16_t *)B, ldb, (uint16_t *)C, M, N,
                                                K, ldc, (hipStream_t)stream);

@@ -43,6 +43,7 @@ SIGNATURES = {
     "gq_quantize_q8_1": ([_P, _P, _I64, _I64, _I64, _P], _I),
     "gq_dequantize": ([_I, _P, _P, _I64, _I64, _I64, _P], _I),
     "gq_mmq_workspace_size_ex": ([_I, _I, _I64, _I64, _I64], _SZ),
+    "gq_mmq_call_workspace_size": ([_I, _I, _I64, _I64, _I64], _SZ),
     "gq_mmq_ex": ([_I, _I, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P], _I),
     "gq_act_prepare_ex": ([_I, _P, _I64, _I64, _I64, _P, _SZ, _P], _I),
     "gq_mmq_prepared_ex": ([_I, _I, _P, _P, _SZ, _P, _I64, _I64, _I64, _I64, _P], _I),
@@ -163,25 +164,42 @@ def _check_workspace(ws: torch.Tensor, need: int, dev):
         raise RuntimeError(f"workspace has {ws.numel()} bytes, this call needs {need}")
 
 
+_call_ws = {}  # (gtype, act, M, N, K) -> bytes one gq_mmq_ex call needs (0: one-launch decode)
+
+
+def _stream(dev) -> int:
+    """torch's current HIP stream on `dev` (the raw handle: the Stream object costs ~2 us)."""
+    return torch._C._cuda_getCurrentRawStream(dev.index if dev.index is not None else torch.cuda.current_device())
+
+
 def mmq(gtype: int, A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int,
         out: torch.Tensor | None = None, workspace: torch.Tensor | None = None, act: str = "q8_1") -> torch.Tensor:
     """C = (A @ B^T)^T as fp16 (N, M) on A's device; the common body of mmq_q8_0/q4_k/q6_k.
     act="fp8": the fp8 activation variant (gq_mmq_ex, GQ_ACT_FP8_E4M3) instead of q8_1."""
     _check_weights(gtype, A, M, K)
     _require_device(B, "B")
-    if A.device != B.device:
-        raise RuntimeError(f"A on {A.device} but B on {B.device}")
+    dev = A.device
+    if B.device != dev:
+        raise RuntimeError(f"A on {dev} but B on {B.device}")
     B = _check_acts(B, N, K)
-    C = _check_out(out, N, M, A.device)
+    C = _check_out(out, N, M, dev)
     if M == 0 or N == 0:
         return C
-    need = workspace_size(gtype, M, N, K, act)
-    if workspace is None or workspace.numel() < need:
-        workspace = torch.empty(max(need, 1), dtype=torch.uint8, device=A.device)
-    with torch.cuda.device(A.device):
-        stream = torch.cuda.current_stream(A.device).cuda_stream
-        _check(lib().gq_mmq_ex(gtype, ACTS[act], A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, B.stride(0),
-                               C.stride(0), workspace.data_ptr(), workspace.numel(), stream))
+    key = (gtype, act, M, N, K)
+    need = _call_ws.get(key)
+    if need is None:
+        need = _call_ws[key] = int(lib().gq_mmq_call_workspace_size(gtype, ACTS[act], M, N, K))
+    if need and (workspace is None or workspace.numel() < need):
+        workspace = torch.empty(need, dtype=torch.uint8, device=dev)
+    wp, wn = (workspace.data_ptr(), workspace.numel()) if need else (None, 0)
+    if dev.index == torch.cuda.current_device():
+        rc = lib().gq_mmq_ex(gtype, ACTS[act], A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, B.stride(0),
+                             C.stride(0), wp, wn, _stream(dev))
+    else:
+        with torch.cuda.device(dev):
+            rc = lib().gq_mmq_ex(gtype, ACTS[act], A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, B.stride(0),
+                                 C.stride(0), wp, wn, _stream(dev))
+    _check(rc)
     return C
 
 

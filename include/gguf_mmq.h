@@ -52,9 +52,13 @@ enum {
 int gq_block_elems(gq_type t);
 int gq_block_bytes(gq_type t);
 
-/* Device workspace gq_mmq needs for this shape (bytes; the activation quantizer's output). */
+/* Device workspace for this shape (bytes; the activation quantizer's output and split-K
+ * partials): enough for gq_mmq and for gq_act_prepare + gq_mmq_prepared. */
 size_t gq_mmq_workspace_size(gq_type t, int64_t M, int64_t N, int64_t K);
 size_t gq_mmq_workspace_size_ex(gq_type t, gq_act act, int64_t M, int64_t N, int64_t K);
+/* The exact need of one gq_mmq_ex call (<= the above): 0 when the call is a one-launch decode
+ * (its quantizer works in LDS), and then workspace may be NULL. */
+size_t gq_mmq_call_workspace_size(gq_type t, gq_act act, int64_t M, int64_t N, int64_t K);
 
 /*
  * C[n * ldc + m] = sum_k W[m][k] * x~[n][k]  for m < M, n < N (fp16 out, fp32 accumulate)
@@ -63,7 +67,8 @@ size_t gq_mmq_workspace_size_ex(gq_type t, gq_act act, int64_t M, int64_t N, int
  *   x~: B quantized exactly as utils/quantize/q8_1.py does (int8 per 32 elements), the
  *       input the reference's parity oracle (kernels/cpu_impls) consumes.
  * K must be a multiple of gq_block_elems(t) (the reference asserts the same).
- * workspace: >= gq_mmq_workspace_size(t, M, N, K) bytes of device memory.
+ * workspace: >= gq_mmq_workspace_size(t, M, N, K) bytes of device memory
+ *            (exactly: gq_mmq_call_workspace_size(t, GQ_ACT_Q8_1, M, N, K); NULL when that is 0).
  * Returns GQ_OK or an error code (gq_last_error() has the text; nothing was launched).
  */
 int gq_mmq(gq_type t, const void *A, const void *B, void *C, int64_t M, int64_t N, int64_t K, int64_t ldb,

@@ -57,10 +57,14 @@ def test_host_argument_checks():
     assert L.gq_mmq(1, None, p, p, 4, 4, 256, 256, 4, p, 1 << 20, None) == 1
     assert L.gq_mmq(1, p, p, p, 4, 4, 256, 255, 4, p, 1 << 20, None) == 1
     assert L.gq_mmq(1, p, p, p, 4, 4, 256, 256, 3, p, 1 << 20, None) == 1
-    need = L.gq_mmq_workspace_size(1, 4, 4, 256)
-    assert need > 0
-    assert L.gq_mmq(1, p, p, p, 4, 4, 256, 256, 4, p, need - 1, None) == 1
+    # a GEMM-shaped call (64 tokens) needs its workspace; a one-launch decode (4 tokens) none
+    need = L.gq_mmq_call_workspace_size(1, 0, 4, 64, 256)
+    assert need > 0 and need <= L.gq_mmq_workspace_size(1, 4, 64, 256)
+    assert L.gq_mmq(1, p, p, p, 4, 64, 256, 256, 4, p, need - 1, None) == 1
     assert b"workspace" in L.gq_last_error()
+    assert L.gq_mmq(1, p, p, p, 4, 64, 256, 256, 4, None, 0, None) == 1
+    assert L.gq_mmq_call_workspace_size(1, 0, 4, 4, 256) == 0
+    assert L.gq_mmq_workspace_size(1, 4, 4, 256) > 0  # (the prepared path's activation form)
     assert L.gq_quantize_q8_1(p, p, 2, 40, 40, None) == 1
 
 
