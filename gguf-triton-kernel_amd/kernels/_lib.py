@@ -61,6 +61,7 @@ SIGNATURES = {
 }
 
 _lib = None
+_call_ws = {}  # (gtype, act, M, N, K) -> bytes one gq_mmq_ex call needs (0: one-launch decode)
 
 
 def lib():
@@ -83,11 +84,13 @@ def lib():
 def set_tuning(key: str, value: int):
     """Override one GQ_* tuning default by name for later calls (gq_debug_set_tuning; the
     library reads the environment once, so setting os.environ later has no effect)."""
+    _call_ws.clear()  # (the workspace a shape needs depends on the tuning)
     _check(lib().gq_debug_set_tuning(key.encode(), int(value)))
 
 
 def reset_tuning():
     """Back to the tuning values the environment gave at first use."""
+    _call_ws.clear()
     lib().gq_debug_reset_tuning()
 
 
@@ -162,9 +165,6 @@ def _check_workspace(ws: torch.Tensor, need: int, dev):
         raise RuntimeError("workspace must be a contiguous uint8 tensor on the weights' device")
     if ws.numel() < need:
         raise RuntimeError(f"workspace has {ws.numel()} bytes, this call needs {need}")
-
-
-_call_ws = {}  # (gtype, act, M, N, K) -> bytes one gq_mmq_ex call needs (0: one-launch decode)
 
 
 def _stream(dev) -> int:
