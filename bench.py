@@ -904,6 +904,13 @@ def main():
     }
     if cpu_var:
         line["cpu_baseline_variants"] = cpu_var
+    for e in sweep:  # the Q4_K_M 7B layer at one token (one grouped decode launch), up front
+        if e.get("config") == "q4_k_m_llama7b_layer_msweep":
+            for pt in e["points"]:
+                if pt["M_tok"] == 1 and pt["act"] == "q8_1" and pt["fused"]:
+                    line["q4_k_m_layer_m1_us"] = pt["us_per_step"]
+                    line["q4_k_m_layer_m1_GBps"] = pt["weight_GBps"]
+            break
     if sweep:
         line["sweep"] = [compact(e) for e in sweep]
     print(json.dumps(line), flush=True)
