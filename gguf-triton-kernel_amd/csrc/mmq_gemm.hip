@@ -62,7 +62,11 @@ __device__ unsigned long long g_gstamps[65536][8];
 // load and put back to zero by the wave that reads S - 1 from it, so every launch finds its
 // counters at zero with no memset node.  Each launch takes the next range of the pool (a host
 // cursor): launches on different streams use distinct counters unless 1 << 18 counters'
-// worth of launches lie between them.
+// worth of launches lie between them.  Limits of this opt-in (test / A-B only) form: the base is
+// taken at launch time, so a captured graph bakes it in -- two replays of one graph running at
+// the same time, or a graph replayed concurrently with eager launches that wrapped the ring onto
+// its range, would share counters.  Use it on one stream, one replay at a time; the default
+// (separate reduce launch) has no such state.
 constexpr int kSplitCounters = 1 << 18;
 __device__ unsigned g_split_cnt[kSplitCounters];
 
