@@ -97,4 +97,16 @@ __device__ __forceinline__ void q4k_sc_m(const uint32_t sw[3], int j, int &sc, i
     }
 }
 
+// s_waitcnt vmcnt(n) for a wave-uniform n <= MAXN (the immediate is an encoding field): the
+// steady-state count is the first compare, the pipeline tails walk down from it
+template <int MAXN> __device__ __attribute__((always_inline)) inline void vm_wait(int n)
+{
+    if constexpr (MAXN <= 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        if (n >= MAXN) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MAXN) : "memory");
+        else vm_wait<MAXN - 1>(n);
+    }
+}
+
 } // namespace gq

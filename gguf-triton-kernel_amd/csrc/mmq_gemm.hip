@@ -319,12 +319,12 @@ constexpr uint32_t DUMMY = 0u;
 //   prologue  W(0) .. W(NWS-2) A(0) .. A(NAS-2)
 //   iteration a: wait until A(a) (and so W(a/SPW)) landed -> barrier -> A(a+NAS-1) ->
 //                [a%SPW == 0: W(w+NWS-1)] -> multiply sub-stage a from W slot w%NWS, A slot a%NAS.
-// vmcnt counts in issue order, so "A(a) landed" = all but the ops issued after it: the NAS-2
-// younger activation sub-stages and the W(.) issued in iterations a-NAS+1 .. a-1 with
+// vmcnt counts in issue order, so "A(a) landed" = all but the ops issued after it: the (up to)
+// NAS-2 younger activation sub-stages and the W(.) issued in iterations a-NAS+1 .. a-1 with
 // index % SPW == 0 (after their A).  W(w) is issued in iteration SPW(w-NWS+1), after
-// A(SPW(w-NWS+1)+NAS-1), which is older than A(SPW w) iff NAS <= SPW(NWS-1).  Past the end the
-// indices are clamped (re-loads of identical bytes into the same slot) so every wave issues
-// the same sequence.
+// A(SPW(w-NWS+1)+NAS-1), which is older than A(SPW w) iff NAS <= SPW(NWS-1).  Nothing is
+// issued past the split's end (a split is often 2-8 weight stages: clamped re-loads there were
+// up to 40% more L2->LDS traffic), so the last NAS-1 waits count fewer younger ops (vm_wait).
 // ABL: ablation bitmask for performance diagnosis (diagnostic build -DGQ_ABLATION only; 0 in
 // production): 1 = no MFMA, 2 = no weight DMA, 4 = no activation DMA, 8 = no dequantization,
 // 16 = no epilogue, 32 = activation DMAs with the addresses of a sub-stage-blocked layout,
@@ -456,23 +456,23 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
             }
         }
     };
-    // vmcnt for "A(a) landed": (NAS-2) younger A's + the W's issued after A(a)
-    // rel = a - a0: W issues in iterations [max(0, rel-NAS+1), rel-1] that are multiples of 4
-    // rel = a - a0: W issues in iterations [max(0, rel-NAS+1), rel-1] that are multiples of SPW
-    auto wait_a = [&](int rel) {
+    // vmcnt for "A(a) landed": the DMA instructions issued after A(a) -- the younger A's
+    // (sub-stages a+1 .. a+NAS-2) and the W's issued in iterations a-NAS+1 .. a-1 (each after its
+    // iteration's A), nothing past the split's end (nrel sub-stages, nws weight stages)
+    auto wait_a = [&](int rel, int nrel, int nws) __attribute__((always_inline)) {
         constexpr int na = ABL & 4 ? 0 : G::NA, nw = ABL & 2 ? 0 : G::NW; // (ablated streams issue nothing)
-        constexpr int base = (G::NAS - 2) * na;
-        const int lo = rel - G::NAS + 1 > 0 ? rel - G::NAS + 1 : 0, hi = rel - 1;
+        const int ya = G::NAS - 2 < nrel - 1 - rel ? G::NAS - 2 : nrel - 1 - rel;
+        const int lo = rel - G::NAS + 1 > 0 ? rel - G::NAS + 1 : 0;
+        const int hi = rel - 1 < SPW * (nws - G::NWS + 1) - 1 ? rel - 1 : SPW * (nws - G::NWS + 1) - 1;
         const int w_after = hi >= lo ? hi / SPW - (lo + SPW - 1) / SPW + 1 : 0;
-        if constexpr ((ABL & 6) == 6) asm volatile("s_barrier" ::: "memory");
-        else if constexpr (ABL & 4) { // weights only: W(w) must land by sub-stage SPW w
-            if (rel % SPW == 0) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(nw) : "memory");
-            else asm volatile("s_barrier" ::: "memory");
-        } else if (w_after >= 4) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(base + 4 * nw) : "memory");
-        else if (w_after == 3) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(base + 3 * nw) : "memory");
-        else if (w_after == 2) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(base + 2 * nw) : "memory");
-        else if (w_after == 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(base + nw) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(base) : "memory");
+        if constexpr ((ABL & 6) == 6) {
+        } else if constexpr (ABL & 4) { // weights only: W(w) must land by sub-stage SPW w
+            const int w = rel / SPW, yw = G::NWS - 2 < nws - 1 - w ? G::NWS - 2 : nws - 1 - w;
+            if (rel % SPW == 0) vm_wait<(G::NWS - 2) * nw>(yw * nw);
+        } else {
+            vm_wait<(G::NAS - 2) * na + ((G::NAS - 1 + SPW - 1) / SPW) * nw>(ya * na + w_after * nw);
+        }
+        asm volatile("s_barrier" ::: "memory");
     };
     static_assert(AQ || (G::NAS - 1 + SPW - 1) / SPW <= 4, "W issues after an A: at most 4");
 
@@ -489,7 +489,8 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
         if (w0 < w1) {
             const int64_t a0 = 4 * sb0, a1 = 4 * sb1;
 #pragma unroll
-            for (int i = 0; i < G::NWS - 1; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
+            for (int i = 0; i < G::NWS - 1; ++i)
+                if (w0 + i < w1) issue_w(w0 + i);
             // 4 lanes per 32-element block (8 fp16 each), 64 blocks per pass over the 4 loader
             // waves; loads unconditional (clamped) and all issued before the first quantization
             constexpr int PMAX = (G::NAS * G::BN * 2 + 63) / 64;
@@ -541,9 +542,12 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
             for (int q = 0; q < PMAX; ++q) asm volatile("" ::"v"(xv[q].x), "v"(xv[q].y), "v"(xv[q].z), "v"(xv[q].w));
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the image is complete before barrier a0
             for (int64_t a = a0; a < a1; ++a) {
-                if ((a & 3) == 0) { // W(w) landed = all but the NWS-2 stages issued after it
-                    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((G::NWS - 2) * G::NW) : "memory");
-                    issue_w((a >> 2) + G::NWS - 1 < w1 ? (a >> 2) + G::NWS - 1 : w1 - 1);
+                if ((a & 3) == 0) { // W(w) landed = all but the (<= NWS-2) stages issued after it
+                    const int64_t w = a >> 2;
+                    const int yw = (int)(G::NWS - 2 < w1 - 1 - w ? G::NWS - 2 : w1 - 1 - w);
+                    vm_wait<(G::NWS - 2) * G::NW>(yw * G::NW);
+                    asm volatile("s_barrier" ::: "memory");
+                    if (w + G::NWS - 1 < w1) issue_w(w + G::NWS - 1);
                 } else {
                     asm volatile("s_barrier" ::: "memory");
                 }
@@ -556,13 +560,16 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
         if (w0 < w1) {
             const int64_t a0 = 4 * sb0, a1 = 4 * sb1;
 #pragma unroll
-            for (int i = 0; i < G::NWS - 1; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
+            for (int i = 0; i < G::NWS - 1; ++i)
+                if (w0 + i < w1) issue_w(w0 + i);
 #pragma unroll
-            for (int i = 0; i < G::NAS - 1; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
+            for (int i = 0; i < G::NAS - 1; ++i)
+                if (a0 + i < a1) issue_a(a0 + i);
             for (int64_t a = a0; a < a1; ++a) {
-                wait_a((int)(a - a0)); // A(a) landed -> barrier: the compute waves take sub-stage a
-                issue_a(a + G::NAS - 1 < a1 ? a + G::NAS - 1 : a1 - 1);
-                if (a % SPW == 0) issue_w(a / SPW + G::NWS - 1 < w1 ? a / SPW + G::NWS - 1 : w1 - 1);
+                // A(a) landed -> barrier: the compute waves take sub-stage a
+                wait_a((int)(a - a0), (int)(a1 - a0), (int)(w1 - w0));
+                if (a + G::NAS - 1 < a1) issue_a(a + G::NAS - 1);
+                if (a % SPW == 0 && a / SPW + G::NWS - 1 < w1) issue_w(a / SPW + G::NWS - 1);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -571,9 +578,11 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
     if (w0 < w1) {
         const int64_t a0 = 4 * sb0, a1 = 4 * sb1;
 #pragma unroll
-        for (int i = 0; i < G::NWS - 1 && NL == 0; ++i) issue_w(w0 + i < w1 ? w0 + i : w1 - 1);
+        for (int i = 0; i < G::NWS - 1 && NL == 0; ++i)
+            if (w0 + i < w1) issue_w(w0 + i);
 #pragma unroll
-        for (int i = 0; i < G::NAS - 1 && NL == 0; ++i) issue_a(a0 + i < a1 ? a0 + i : a1 - 1);
+        for (int i = 0; i < G::NAS - 1 && NL == 0; ++i)
+            if (a0 + i < a1) issue_a(a0 + i);
 #ifdef GQ_GEMM_STAMPS
         t_issued = __builtin_amdgcn_s_memtime() - t_start;
 #endif
@@ -583,7 +592,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
             const unsigned long long tw = __builtin_amdgcn_s_memtime();
 #endif
             if constexpr (NL > 0) asm volatile("s_barrier" ::: "memory"); // the loaders' wait_a
-            else wait_a((int)(a - a0));
+            else wait_a((int)(a - a0), (int)(a1 - a0), (int)(w1 - w0));
 #ifdef GQ_GEMM_STAMPS
             {
                 const unsigned long long tn = __builtin_amdgcn_s_memtime();
@@ -593,8 +602,8 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
 #endif
             const int64_t w = a / SPW;
             if constexpr (NL == 0) {
-                issue_a(a + G::NAS - 1 < a1 ? a + G::NAS - 1 : a1 - 1);
-                if (s4 == 0) issue_w(w + G::NWS - 1 < w1 ? w + G::NWS - 1 : w1 - 1);
+                if (a + G::NAS - 1 < a1) issue_a(a + G::NAS - 1);
+                if (s4 == 0 && w + G::NWS - 1 < w1) issue_w(w + G::NWS - 1);
             }
 
             const uint8_t *wr = lds + (int)(w % G::NWS) * G::W_SLOT + G::RBW * myrow;

@@ -38,6 +38,15 @@ namespace {
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// Diagnostic ablations (-DGQ_SKINNY_ABL in a separate build, never the product): 1 = every
+// activation DMA re-reads the wave's first super-block (cache hits: the activation stream
+// without its traffic), 2 = every weight load re-reads the first fragment's first super-block,
+// 4 = one activation DMA instruction per super-block instead of 8 (garbage results).
+#ifndef GQ_SKINNY_ABL
+#define GQ_SKINNY_ABL 0
+#endif
+constexpr int SABL = GQ_SKINNY_ABL;
+
 constexpr int SW = 8;     // waves per workgroup, each a contiguous K range of the workgroup's rows
 constexpr int kCUs = 256; // MI355X: 256 CUs
 
@@ -110,22 +119,24 @@ __global__ __launch_bounds__(64 * SW) void skinny_kernel(const uint8_t *__restri
     if (nsw > 0) {
         // the wave's stream: item j = (unit u0 + j / nsw, super-block sb0 + j % nsw), one ring
         // across the unit boundaries (the next unit's first super-blocks load under this one's
-        // last); clamped past the end (surplus re-reads hit the cache)
+        // last); nothing is loaded past the end (a wave often has only 2-4 items: surplus loads
+        // would double its activation traffic and hold the wave until they land)
         const int total = (u1 - u0) * nsw;
         W wb[D][RG];
         auto load = [&](int b, int j) __attribute__((always_inline)) {
-            const int jc = j < total ? j : total - 1;
-            const int u = u0 + jc / nsw, sb = sb0 + jc % nsw;
+            const int u = u0 + j / nsw, sb = sb0 + j % nsw;
 #pragma unroll
             for (int rf = 0; rf < RG; ++rf) {
-                const int row = u * 16 * RG + 16 * rf + c;
-                wb[b][rf].load(wrs, (uint32_t)((row < M ? row : M - 1) * row_bytes), g, (uint32_t)(sb * W::SB));
+                const int row = SABL & 2 ? c : u * 16 * RG + 16 * rf + c;
+                wb[b][rf].load(wrs, (uint32_t)((row < M ? row : M - 1) * row_bytes), g,
+                               (uint32_t)((SABL & 2 ? sb0 : sb) * W::SB));
             }
             uint8_t *dst = ring + b * XSLOT;
 #pragma unroll
             for (int i = 0; i < 8; ++i)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void *)(dst + 1024 * i), 16, xsrc[i],
-                                                         (uint32_t)(512 * sb), 0, 0);
+                if (!(SABL & 4) || i == 0)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void *)(dst + 1024 * i), 16, xsrc[i],
+                                                             (uint32_t)(512 * (SABL & 1 ? sb0 : sb)), 0, 0);
         };
         auto compute = [&](int b) __attribute__((always_inline)) {
             const uint8_t *xs = ring + b * XSLOT + c * 512;
@@ -139,25 +150,28 @@ __global__ __launch_bounds__(64 * SW) void skinny_kernel(const uint8_t *__restri
         };
         // item j sits in slot j % D; D bodies per loop iteration (static slots), the last < D items
         // after it, so the loop's back edge always follows the same code.  The slot's DMA has
-        // landed when at most the D - 1 younger items' loads are outstanding (loads return in
-        // order; a unit's output stores, issued in between, can only make this wait longer).
+        // landed when at most the younger items' loads are outstanding: D - 1 items', fewer in
+        // the last D - 1 (loads return in order; a unit's output stores, issued in between, can
+        // only make this wait longer).
         constexpr int PER_SB = RG * w_loads<F>() + 8;
         static_assert((D - 1) * PER_SB <= 63, "vmcnt range");
         // (sched_barrier around the waits: register-only work -- the dequantization -- would
         // otherwise move across them)
         auto body = [&](int j, int b) __attribute__((always_inline)) {
             __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * PER_SB) : "memory");
+            const int younger = total - 1 - j < D - 1 ? total - 1 - j : D - 1; // items issued after j
+            vm_wait<(D - 1) * PER_SB>(younger * PER_SB);
             __builtin_amdgcn_sched_barrier(0);
             compute(b);
             __builtin_amdgcn_sched_barrier(0);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the slot's reads are done: refill it
             __builtin_amdgcn_sched_barrier(0);
-            load(b, j + D);
+            if (j + D < total) load(b, j + D);
             if ((j + 1) % nsw == 0) finish(u0 + j / nsw);
         };
 #pragma unroll
-        for (int b = 0; b < D; ++b) load(b, b);
+        for (int b = 0; b < D; ++b)
+            if (b < total) load(b, b);
         int j = 0;
         for (; j + D - 1 < total; j += D) {
 #pragma unroll

@@ -128,21 +128,26 @@ __global__ __launch_bounds__(64 * (NWC + NL)) void wgemm_kernel(
             xv[i] = (uint32_t)tok * (uint32_t)K * 2u + 2u * (uint32_t)W::off(pc >> 2, pc & 3);
             kd[i] = 1024 * k;
         }
-        auto issue = [&](int a) __attribute__((always_inline)) { // sub-stage a (clamped source) into slot a % R
-            const int ac = a < nsub ? a : nsub - 1;
-            const uint32_t so = 2u * (uint32_t)(256 * (sb0 + (ac >> 2)) + W::base(ac & 3));
+        auto issue = [&](int a) __attribute__((always_inline)) { // sub-stage a into slot a % R
+            const uint32_t so = 2u * (uint32_t)(256 * (sb0 + (a >> 2)) + W::base(a & 3));
             uint8_t *dst = lds + (a % G::R) * G::SLOT;
 #pragma unroll
             for (int i = 0; i < G::DPL; ++i) {
                 if constexpr (!(ABL & 2)) dma16(xrs, dst + kd[i], xv[i], so);
             }
         };
+        // nothing past the split's end (a split is 8-16 sub-stages: clamped re-loads of the last
+        // one were up to 100% more activation DMA), so the last L - 1 waits count fewer younger ones
 #pragma unroll
-        for (int a = 0; a < G::L; ++a) issue(a);
+        for (int a = 0; a < G::L; ++a)
+            if (a < nsub) issue(a);
         for (int a = 0; a < nsub; ++a) {
-            if constexpr (ABL & 2) asm volatile("s_barrier" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((G::L - 1) * G::DPL) : "memory"); // sub-stage a landed
-            issue(a + G::L); // into the slot of sub-stage a + L - R = a - 2: read before the last barrier
+            if constexpr (!(ABL & 2)) { // sub-stage a landed: at most the younger sub-stages outstanding
+                const int young = G::L - 1 < nsub - 1 - a ? G::L - 1 : nsub - 1 - a;
+                vm_wait<(G::L - 1) * G::DPL>(young * G::DPL);
+            }
+            asm volatile("s_barrier" ::: "memory");
+            if (a + G::L < nsub) issue(a + G::L); // into the slot of sub-stage a + L - R = a - 2: read before the last barrier
         }
         vmcnt<0>(); // no DMA may land after the workgroup exits
         return;
@@ -167,7 +172,8 @@ __global__ __launch_bounds__(64 * (NWC + NL)) void wgemm_kernel(
 
     if (nsub > 0) {
         W wb[WD][RG]; // super-block ring: WD - 1 super-blocks of weights in flight
-        auto load_w = [&](int b, int sb) __attribute__((always_inline)) { // super-block sb (clamped: surplus re-reads hit the cache)
+        auto load_w = [&](int b, int sb) __attribute__((always_inline)) { // super-block sb (clamped: the WD - 1 surplus re-reads
+            // hit the cache; skipping them -- a branch around register loads -- measured 0-2% slower)
             const uint32_t s0 = (uint32_t)((sb < sb1 ? sb : sb1 - 1) * W::SB) & WMASK;
 #pragma unroll
             for (int rf = 0; rf < RG; ++rf) wb[b][rf].load(wrs, wv[rf], g, s0);

@@ -19,16 +19,19 @@ def main():
     ap.add_argument("--tokens", default="1,2,4,5,8,12,16,17,24,32,48,64")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--tune", default="", help="KEY=V,... library tuning overrides (gq_debug_set_tuning)")
+    ap.add_argument("--lib", default=None, help="another build of libgguf_mmq.so (diagnostic variants)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     import kernels._lib as kl
+    if a.lib:
+        kl.LIB_PATH = os.path.abspath(a.lib)
     for kv in filter(None, a.tune.split(",")):
         k, v = kv.split("=")
         kl.set_tuning(k, int(v))
     for shp in a.shapes.split(","):
         fmt, M, K = shp.split(":")
         M, K = int(M), int(K)
-        row = {"shape": shp, "tune": a.tune, "us": {}, "hbm_frac": {}}
+        row = {"shape": shp, "tune": a.tune, "lib": os.path.basename(kl.LIB_PATH), "us": {}, "hbm_frac": {}}
         for N in (int(t) for t in a.tokens.split(",")):
             r = bench.Runner(fmt, M, K, N, dev, a.steps)
             g = r.capture(r.step, a.steps)
