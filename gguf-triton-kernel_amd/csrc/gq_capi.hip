@@ -211,18 +211,20 @@ bool use_wgemm(int t, int form, int64_t N)
     return t == GQ_Q4_K && N >= kWgemmMinTokens;
 }
 // Skinny-token kernel (mmq_skinny.hip).  By type and token count only (a row subset runs the
-// same arithmetic as the whole matrix): by default Q4_K at 5..16 tokens, where it measured
-// faster than the LDS-DMA GEMM (profiles/r03/skinny_sweep.log, step incl. act_quant: 4096^2
-// x16 10.8 vs 12.1 us, 11008x4096 17.8 vs 22.6, 4096x11008 18.1 vs 20.2); Q8_0 is level, Q6_K
-// and 17..32 tokens are faster on the GEMM.  GQ_SKINNY=1: every type at 1..32 tokens the GEMM
-// path would take (tests), 0: off.
+// same arithmetic as the whole matrix): by default Q4_K and Q8_0 at 5..16 tokens, where it
+// measured faster than the LDS-DMA GEMM (profiles/r03/tails/route_sw.log, step incl. act_quant,
+// 16 tokens: Q4_K 4096^2 9.7 vs 12.0 us, 11008x4096 15.3 vs 22.2, 4096x11008 16.5 vs 19.6; Q8_0
+// 4096^2 11.3 vs 13.1, 11008x4096 19.4 vs 24.3).  Q6_K stays on the GEMM: faster on 4096-row
+// matrices (11.6 vs 13.0) but 28672x8192 72 vs 95, and the choice may not depend on M; 17..32
+// tokens: mixed (Q4_K +8% / -5% by shape), the GEMM.  GQ_SKINNY=1: every type at 1..32 tokens
+// the GEMM path would take (tests), 0: off.
 constexpr int64_t kSkinnyMinTokens = 5, kSkinnyMaxTokens = 16, kSkinnyForcedMax = 32;
 bool use_skinny(int t, int form, int64_t N)
 {
     const int sk = gq::tuning().skinny;
     if (form != gq::AF_F16 || sk == 0) return false;
     if (sk == 1) return N <= kSkinnyForcedMax;
-    return t == GQ_Q4_K && N >= kSkinnyMinTokens && N <= kSkinnyMaxTokens;
+    return (t == GQ_Q4_K || t == GQ_Q8_0) && N >= kSkinnyMinTokens && N <= kSkinnyMaxTokens;
 }
 gq::SkinnyPlan skinny_plan(int t, int64_t M, int64_t N, int64_t K)
 {

@@ -44,7 +44,8 @@ def _check(fmt, qA, B, M, N, K):
 @pytest.mark.parametrize("N", [5, 8, 16, 17, 32, 7, 23])
 @pytest.mark.parametrize("M,K", [(300, 1024), (64, 256), (1000, 2048), (129, 768)])
 def test_skinny_tokens(fmt, N, M, K, tune):
-    """Every type at 5..32 tokens through the kernel (forced: by default it takes Q4_K at 5..16)."""
+    """Every type at 5..32 tokens through the kernel (forced: by default it takes Q4_K and Q8_0
+    at 5..16)."""
     tune(GQ_SKINNY=1)
     qA = random_blocks(fmt, M, K, seed=M + N + K)
     B = random_activations(N, K, seed=K + 3 * N)
@@ -125,10 +126,12 @@ def test_skinny_prepared_and_chunked(fmt, tune):
     assert torch.equal(one.view(torch.int16), many.view(torch.int16))
 
 
-def test_skinny_default_route(tune):
-    """The default route takes the kernel for Q4_K at 5..16 tokens (GQ_SKINNY=0: the LDS-DMA GEMM):
-    both within tolerance, and the two routes differ in bits (the route really changed)."""
-    fmt, M, N, K = "q4_k", 512, 16, 2048
+@pytest.mark.parametrize("fmt,N", [("q4_k", 16), ("q4_k", 5), ("q8_0", 16), ("q8_0", 7)])
+def test_skinny_default_route(fmt, N, tune):
+    """The default route takes the kernel for Q4_K and Q8_0 at 5..16 tokens (GQ_SKINNY=0: the
+    LDS-DMA GEMM): both within tolerance, and the two routes differ in bits (the route really
+    changed)."""
+    M, K = 512, 2048
     qA = random_blocks(fmt, M, K, seed=3)
     B = random_activations(N, K, seed=4)
     a = _run(fmt, qA, B, M, N, K)
