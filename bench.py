@@ -651,10 +651,10 @@ def bench_layer(Ns, acts, steps, warmup, dev, fuse=True, grouped="auto"):
     attn_v and ffn_down in Q6_K, the rest Q4_K), shared inputs quantized once per group
     (kernels.layer_mix.LayerMix; fuse: q+k and gate+up as one call each), for each token count in
     Ns and activation format in acts ("q8_1": the reference's semantics; "fp8": the e4m3 variant).
-    Weights rotate over >= 1 GiB.  grouped: LayerMix's grouped-decode setting ("auto": the whole
-    layer as one gq_mmq_grouped launch at 1 token; True: at 1..4; False: one launch per set)."""
+    Weights rotate over >= 1 GiB.  grouped: LayerMix's grouped-decode setting ("auto" / True: the
+    whole layer as one gq_mmq_grouped launch at 1..4 tokens; False: one launch per set)."""
     from gguf import LLAMA_LAYER_SHAPES, q4_k_m_layer_types
-    from kernels.layer_mix import GGUFLinear, LayerMix
+    from kernels.layer_mix import GROUPED_MAX_TOKENS, GGUFLinear, LayerMix
     types = q4_k_m_layer_types(0, 32)
     one = {n: device_random_blocks(types[n], M, K, dev, seed=i) for i, (n, (M, K)) in enumerate(LLAMA_LAYER_SHAPES.items())}
     layer_bytes = sum(t.numel() for t in one.values())
@@ -689,7 +689,7 @@ def bench_layer(Ns, acts, steps, warmup, dev, fuse=True, grouped="auto"):
             gr.replay()
             t = min(timed_replay(gr, dev) for _ in range(3)) / steps
             res.append({"config": f"q4_k_m_llama7b_layer_m{N}", "act": act, "fused": fuse,
-                        "grouped": act == "q8_1" and N <= {"auto": 1, True: 4, False: 0}[grouped],
+                        "grouped": act == "q8_1" and N <= GROUPED_MAX_TOKENS[grouped],
                         "fmt": "q4_k+q6_k", "M_tok": N,
                         "us_per_step": round(t * 1e6, 2), "tflops": round(flops / t / 1e12, 3),
                         "weight_GBps": round(layer_bytes / t / 1e9, 1)})

@@ -540,9 +540,9 @@ int64_t row_bytes(int fmt, int64_t K)
     return fmt == Q8_0 ? K / 32 * 34 : (fmt == Q4_K ? K / 256 * 144 : K / 256 * 210);
 }
 
-// share: the fraction of the chip's waves the matrix gets (1: a launch of its own; a grouped
-// launch splits the chip by weight bytes)
-bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p, double share = 1.0)
+// wgs: the workgroups the matrix gets (0: a launch of its own, the whole chip; a grouped launch
+// splits the chip's workgroups by weight bytes)
+bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p, int wgs = 0)
 {
     // at most 4 tokens per workgroup (NT = 8 spills registers); N = 5..8 runs two token groups,
     // whose second pass over the weights is served largely by the Infinity Cache
@@ -569,8 +569,8 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p, double share = 1.0)
     const int64_t cpr = upr / upc_of(fmt, p.nt); // lane chunks per row
     const int64_t cap = NI * 1024 - 16;
     const int per_cu = (int)(LDS_CAP / p.lds) > 0 ? (int)(LDS_CAP / p.lds) : 1;
-    int64_t W = (int64_t)256 * per_cu * DW; // waves the chip holds (its share of them)
-    if (share < 1.0) W = (int64_t)(W * share) > DW ? (int64_t)(W * share) : DW;
+    int64_t W = (int64_t)256 * per_cu * DW; // waves the chip holds (or the granted workgroups')
+    if (wgs > 0) W = (int64_t)wgs * DW;
     DecodeGeom &g = p.geo;
     if (RB <= cap) {
         const int64_t gmax = cap / RB;
@@ -785,45 +785,81 @@ hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipS
     // every item's token tile as a launch of its own would pick it (bit-identical rows); one
     // launch per distinct tile (a Q6_K long-K item caps it at 2 tokens, so 3-4 tokens can take two)
     Pick solo[kMaxGroup];
-    double bytes[kMaxGroup], total = 0;
-    for (int i = 0; i < n; ++i) {
+    for (int i = 0; i < n; ++i)
         if (!pick(items[i].fmt, items[i].M, N, items[i].K, solo[i])) return hipErrorInvalidValue;
-        const int tg = (int)((N + solo[i].nt - 1) / solo[i].nt);
-        bytes[i] = (double)items[i].M * (double)row_bytes(items[i].fmt, items[i].K) * tg;
-        total += bytes[i];
-    }
     for (int nt : {1, 2, 4}) {
-        GroupedArgs a{};
-        a.N = N;
+        // the launch's parts: (item, token group); its LDS is the largest part's
+        int pi[kMaxGroup], py[kMaxGroup], np = 0;
         size_t lds = 0;
-        int blocks = 0, np = 0;
+        double bytes[kMaxGroup], total = 0;
         for (int i = 0; i < n; ++i) {
             if (solo[i].nt != nt) continue;
-            // the chip's waves split by weight bytes (all parts finish together)
-            Pick p;
-            if (!pick(items[i].fmt, items[i].M, N, items[i].K, p, bytes[i] / total) || p.nt != nt)
-                return hipErrorInvalidValue;
             const int tg = (int)((N + nt - 1) / nt);
             for (int y = 0; y < tg; ++y) {
                 if (np == kMaxGroup) return hipErrorInvalidValue;
-                GroupedProblem &q = a.p[np++];
-                q.A = items[i].A;
-                q.X = items[i].X;
-                q.ldx = items[i].ldx;
-                q.C = items[i].C;
-                q.ldc = items[i].ldc;
-                q.M = (int)items[i].M;
-                q.K = (int)items[i].K;
-                q.geo = p.geo;
-                q.code = items[i].fmt * 16 + p.itc;
-                q.block0 = blocks;
-                q.gx = p.grid;
-                q.by = y;
-                blocks += p.grid;
-                lds = p.lds > lds ? p.lds : lds;
+                pi[np] = i;
+                py[np] = y;
+                bytes[np] = (double)items[i].M * (double)row_bytes(items[i].fmt, items[i].K);
+                total += bytes[np];
+                lds = solo[i].lds > lds ? solo[i].lds : lds;
+                ++np;
             }
         }
         if (np == 0) continue;
+        // The chip's workgroups split by weight bytes (all parts finish together), whole
+        // workgroups by largest remainder, at least one each: never more than the chip holds at
+        // once -- rounding every part up had put a few workgroups into a second round (a 7B layer:
+        // 258 of 256), doubling the launch (44.5 -> 30.1 us at one token).  Weighting the bytes by
+        // each format's large-matrix streaming rate measured 1-5% slower (grouped_alloc_ab.log).
+        const int per_cu = (int)(LDS_CAP / lds) > 0 ? (int)(LDS_CAP / lds) : 1;
+        const int budget = 256 * per_cu;
+        int wg[kMaxGroup], used = 0;
+        double frac[kMaxGroup];
+        for (int j = 0; j < np; ++j) {
+            const double ideal = budget * bytes[j] / total;
+            wg[j] = (int)ideal > 1 ? (int)ideal : 1;
+            frac[j] = ideal - wg[j];
+            used += wg[j];
+        }
+        while (used < budget) { // the largest remainders get the rest
+            int best = 0;
+            for (int j = 1; j < np; ++j)
+                if (frac[j] > frac[best]) best = j;
+            ++wg[best];
+            frac[best] -= 1.0;
+            ++used;
+        }
+        while (used > budget) { // (more parts than workgroups cannot happen: np <= 16)
+            int best = -1;
+            for (int j = 0; j < np; ++j)
+                if (wg[j] > 1 && (best < 0 || frac[j] < frac[best])) best = j;
+            if (best < 0) break;
+            --wg[best];
+            frac[best] += 1.0;
+            --used;
+        }
+        GroupedArgs a{};
+        a.N = N;
+        int blocks = 0;
+        for (int j = 0; j < np; ++j) {
+            const int i = pi[j];
+            Pick p;
+            if (!pick(items[i].fmt, items[i].M, N, items[i].K, p, wg[j]) || p.nt != nt) return hipErrorInvalidValue;
+            GroupedProblem &q = a.p[j];
+            q.A = items[i].A;
+            q.X = items[i].X;
+            q.ldx = items[i].ldx;
+            q.C = items[i].C;
+            q.ldc = items[i].ldc;
+            q.M = (int)items[i].M;
+            q.K = (int)items[i].K;
+            q.geo = p.geo;
+            q.code = items[i].fmt * 16 + p.itc;
+            q.block0 = blocks;
+            q.gx = p.grid;
+            q.by = py[j];
+            blocks += p.grid;
+        }
         a.n = np;
         hipError_t e = nt == 1   ? launch_grouped_nt<1>(a, blocks, lds, s)
                        : nt == 2 ? launch_grouped_nt<2>(a, blocks, lds, s)

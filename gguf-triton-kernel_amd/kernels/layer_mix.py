@@ -8,20 +8,23 @@ copied end to end into one device buffer (the bytes are unchanged -- a packed ro
 blocks), so each such set is ONE call (one activation quantization, one launch, the split-K
 plan of the taller matrix) whose (N, sum M) output is returned as per-projection column views.
 Sets that share an input but differ in type quantize the input once (gq_act_prepare) and run
-gq_mmq_prepared per weight.  At one token (q8_1 activations) every call of the layer goes into
-ONE grouped decode launch (gq_mmq_grouped: the chip's waves split over the matrices by weight
-bytes, each matrix's rows bit-identical to its own call).  Measured (Q4_K_M 7B layer 0,
-profiles/r03/grouped_decode.txt): 45 us graph-replayed, level with the five launches of the
-fused sets (44) and 16% under seven unfused ones (54) -- the decode kernel is bound by its
-per-wave DMA latency, not by launch ramps -- but one host call instead of five for eager
-callers; at 2 tokens the grouped launch measured slower (68 vs 53 us), so grouped="auto" takes
-it at one token only (True: 1..4 tokens, False: never).
+gq_mmq_prepared per weight.  At 1..4 tokens (q8_1 activations) every call of the layer goes
+into ONE grouped decode launch (gq_mmq_grouped: the chip's workgroups split over the matrices by
+weight bytes, each matrix's rows bit-identical to its own call).  Measured (Q4_K_M 7B layer 0,
+graph-replayed, profiles/r03/tails/grouped_layer.log): 30.1 / 48.8 / 59.0 / 59.7 us at 1 / 2 /
+3 / 4 tokens vs 44.2 / 54.1 / 79.9 / 80.2 for the fused sets' own launches.  grouped="auto"
+and True take it at 1..4 tokens (a call the grouped launch refuses -- e.g. a long-K Q6_K item
+at 3..4 tokens -- runs the sets' own launches), False never.
 """
 from __future__ import annotations
 
 import torch
 
 from . import _lib
+
+
+# grouped= setting -> the most tokens LayerMix runs as one grouped decode launch
+GROUPED_MAX_TOKENS = {"auto": 4, True: 4, False: 0}
 
 
 class GGUFLinear:
@@ -49,8 +52,8 @@ class LayerMix:
 
     def __init__(self, linears: dict, act: str = "q8_1", fuse: bool = True, grouped="auto"):
         self.act = act  # "q8_1" (the reference's activation quantization) or "fp8" (e4m3 variant)
-        # one gq_mmq_grouped launch for the whole layer: "auto" at 1 token, True at 1..4, False never
-        self.max_grouped = {"auto": 1, True: 4, False: 0}[grouped]
+        # one gq_mmq_grouped launch for the whole layer: "auto" / True at 1..4 tokens, False never
+        self.max_grouped = GROUPED_MAX_TOKENS[grouped]
         self.lin = {}     # name -> GGUFLinear (unfused projections)
         self.parts = {}   # name -> (fused key, first column, rows)
         # per input group: the calls to make, each (key, GGUFLinear); fused keys join names by "+"

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Q4_K_M Llama-7B layer (bench.bench_layer) at decode sizes, grouped vs one launch per set."""
+"""Q4_K_M Llama-7B layer (bench.bench_layer) at decode sizes, grouped vs one launch per set.
+python tools/layer_time.py [Ns] [--lib other-build.so] [--grouped-only]"""
 import json
 import os
 import sys
@@ -10,8 +11,14 @@ import bench  # noqa: E402
 import torch  # noqa: E402
 
 dev = torch.device("cuda:0")
-Ns = tuple(int(n) for n in (sys.argv[1] if len(sys.argv) > 1 else "1,2,3,4").split(","))
-for grouped in (True, False):  # (True: grouped at 1..4 tokens)
+args = [a for a in sys.argv[1:]]
+lib = args[args.index("--lib") + 1] if "--lib" in args else None
+if lib:
+    import kernels._lib as kl
+    kl.LIB_PATH = os.path.abspath(lib)
+pos = [a for i, a in enumerate(args) if not a.startswith("--") and (i == 0 or args[i - 1] != "--lib")]
+Ns = tuple(int(n) for n in (pos[0] if pos else "1,2,3,4").split(","))
+for grouped in ((True,) if "--grouped-only" in args else (True, False)):  # (True: grouped at 1..4 tokens)
     r = bench.bench_layer(Ns, ("q8_1",), 50, 5, dev, fuse=True, grouped=grouped)
-    print(json.dumps({"grouped": grouped, "weight_bytes": r["weight_bytes"],
+    print(json.dumps({"grouped": grouped, "lib": os.path.basename(lib or "libgguf_mmq.so"), "weight_bytes": r["weight_bytes"],
                       "points": [(p["M_tok"], p["us_per_step"], p["weight_GBps"]) for p in r["points"]]}), flush=True)
