@@ -799,14 +799,18 @@ hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipS
                 if (np == kMaxGroup) return hipErrorInvalidValue;
                 pi[np] = i;
                 py[np] = y;
-                bytes[np] = (double)items[i].M * (double)row_bytes(items[i].fmt, items[i].K);
+                // Q6_K bytes weigh more at 1-2 tokens (their unpacking costs more per byte than
+                // Q4_K's): measured on the Q4_K_M 7B layer, profiles/r03/tails/grouped_q6k_weight_ab.log
+                const double q6w = nt == 1 ? 1.15 : (nt == 2 ? 1.5 : 1.0);
+                bytes[np] = (double)items[i].M * (double)row_bytes(items[i].fmt, items[i].K) *
+                            (items[i].fmt == Q6_K ? q6w : 1.0);
                 total += bytes[np];
                 lds = solo[i].lds > lds ? solo[i].lds : lds;
                 ++np;
             }
         }
         if (np == 0) continue;
-        // The chip's workgroups split by weight bytes (all parts finish together), whole
+        // The chip's workgroups split by (weighted) weight bytes (all parts finish together), whole
         // workgroups by largest remainder, at least one each: never more than the chip holds at
         // once -- rounding every part up had put a few workgroups into a second round (a 7B layer:
         // 258 of 256), doubling the launch (44.5 -> 30.1 us at one token).  Weighting the bytes by

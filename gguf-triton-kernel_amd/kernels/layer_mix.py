@@ -11,8 +11,8 @@ Sets that share an input but differ in type quantize the input once (gq_act_prep
 gq_mmq_prepared per weight.  At 1..4 tokens (q8_1 activations) every call of the layer goes
 into ONE grouped decode launch (gq_mmq_grouped: the chip's workgroups split over the matrices by
 weight bytes, each matrix's rows bit-identical to its own call).  Measured (Q4_K_M 7B layer 0,
-graph-replayed, profiles/r03/tails/grouped_layer.log): 30.1 / 48.8 / 59.0 / 59.7 us at 1 / 2 /
-3 / 4 tokens vs 44.2 / 54.1 / 79.9 / 80.2 for the fused sets' own launches.  grouped="auto"
+graph-replayed, profiles/r03/tails/grouped_q6k_weight_ab.log): 28.8 / 42.3 / 58.8 / 59.5 us at
+1 / 2 / 3 / 4 tokens vs 44.2 / 54.1 / 79.9 / 80.2 for the fused sets' own launches.  grouped="auto"
 and True take it at 1..4 tokens (a call the grouped launch refuses -- e.g. a long-K Q6_K item
 at 3..4 tokens -- runs the sets' own launches), False never.
 """
