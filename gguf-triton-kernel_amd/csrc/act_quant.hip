@@ -28,14 +28,15 @@
 
 namespace gq {
 
+// workgroup wg of a launch over one (rows, K) activation tensor: blocks 64 wg .. 64 wg + 63
 template <int MODE>
-__global__ __launch_bounds__(256) void act_quant_kernel(const uint16_t *__restrict__ X, int64_t ldx, int64_t rows,
-                                                        int64_t K, uint8_t *__restrict__ out, int8_t *__restrict__ codes,
-                                                        float *__restrict__ dout, float *__restrict__ sout,
-                                                        uint16_t *__restrict__ xdeq)
+__device__ __forceinline__ void act_quant_body(const uint16_t *__restrict__ X, int64_t ldx, int64_t rows, int64_t K,
+                                               uint8_t *__restrict__ out, int8_t *__restrict__ codes,
+                                               float *__restrict__ dout, float *__restrict__ sout,
+                                               uint16_t *__restrict__ xdeq, int64_t wg)
 {
     const int64_t nb = K / 32;
-    const int64_t blk = (int64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
+    const int64_t blk = wg * 64 + (threadIdx.x >> 2);
     const int sub = threadIdx.x & 3; // elements 8*sub .. 8*sub+7 of the block
     const bool live = blk < rows * nb;
     const int64_t row = live ? blk / nb : 0;
@@ -106,6 +107,47 @@ __global__ __launch_bounds__(256) void act_quant_kernel(const uint16_t *__restri
         }
         *(u32x4 *)(xdeq + row * K + 32 * j + 8 * sub) = (u32x4){o[0], o[1], o[2], o[3]};
     }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void act_quant_kernel(const uint16_t *__restrict__ X, int64_t ldx, int64_t rows,
+                                                        int64_t K, uint8_t *__restrict__ out, int8_t *__restrict__ codes,
+                                                        float *__restrict__ dout, float *__restrict__ sout,
+                                                        uint16_t *__restrict__ xdeq)
+{
+    act_quant_body<MODE>(X, ldx, rows, K, out, codes, dout, sout, xdeq, (int64_t)blockIdx.x);
+}
+
+// Several tensors' DEQ forms in one launch (gq_act_prepare_grouped): segment i owns workgroups
+// [wg0, wg0 + its blocks / 64), each running the one-tensor body -- bit-identical to its own launch.
+struct DeqSegs {
+    int n;
+    DeqSeg s[kMaxDeqSegs];
+};
+
+__global__ __launch_bounds__(256) void act_quant_deq_grouped_kernel(const DeqSegs a)
+{
+    const int64_t b = (int64_t)blockIdx.x;
+    int i = 0;
+    while (i + 1 < a.n && b >= a.s[i + 1].wg0) ++i;
+    const DeqSeg &q = a.s[i];
+    act_quant_body<ACT_DEQ>(q.X, q.ldx, q.rows, q.K, nullptr, nullptr, nullptr, nullptr, q.xdeq, b - q.wg0);
+}
+
+hipError_t launch_act_quant_deq_grouped(const DeqSeg *segs, int n, hipStream_t s)
+{
+    if (n < 1 || n > kMaxDeqSegs) return hipErrorInvalidValue;
+    DeqSegs a{};
+    a.n = n;
+    int64_t wg = 0;
+    for (int i = 0; i < n; ++i) {
+        a.s[i] = segs[i];
+        a.s[i].wg0 = wg;
+        wg += (segs[i].rows * (segs[i].K / 32) + 63) / 64;
+    }
+    if (wg == 0) return hipSuccess;
+    act_quant_deq_grouped_kernel<<<dim3((unsigned)wg), dim3(256), 0, s>>>(a);
+    return hipGetLastError();
 }
 
 hipError_t launch_act_quant(int mode, const uint16_t *X, int64_t ldx, int64_t rows, int64_t K, void *out0,

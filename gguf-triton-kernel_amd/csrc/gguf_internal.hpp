@@ -56,6 +56,16 @@ enum ActForm : int { AF_F16 = 0, AF_I8 = 1, AF_F8 = 2 };
 // max|x| <= 448 * 2^e over the block (2^0 for an all-zero block); code = e4m3(x / 2^e), RNE.
 hipError_t launch_act_quant(int mode, const uint16_t *X, int64_t ldx, int64_t rows, int64_t K, void *out0,
                             void *out1, void *out2, hipStream_t s);
+// The DEQ form of up to kMaxDeqSegs tensors in one launch (wg0 is set by the launcher),
+// bit-identical to launch_act_quant(ACT_DEQ, ...) per tensor.
+constexpr int kMaxDeqSegs = 8;
+struct DeqSeg {
+    const uint16_t *X;
+    int64_t ldx, rows, K;
+    uint16_t *xdeq;
+    int64_t wg0;
+};
+hipError_t launch_act_quant_deq_grouped(const DeqSeg *segs, int n, hipStream_t s);
 
 // Decode-shaped GEMV (mmq_gemv.hip): C[t][m] for t < N_tok <= 8 from SOA activations.
 hipError_t launch_gemv(int fmt, const uint8_t *A, const int8_t *xq, const float *xd, const float *xs, uint16_t *C,

@@ -415,7 +415,7 @@ void gq_debug_reset_tuning(void) { gq::reset_tuning(); }
 
 int gq_block_elems(gq_type t) { return block_elems(t); }
 int gq_block_bytes(gq_type t) { return block_bytes(t); }
-int gq_version(void) { return 101; }
+int gq_version(void) { return 102; }
 const char *gq_last_error(void) { return g_err.c_str(); }
 
 size_t gq_mmq_call_workspace_size(gq_type t, gq_act act, int64_t M, int64_t N, int64_t K)
@@ -630,6 +630,54 @@ int gq_act_prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *works
                    void *stream)
 {
     return gq_act_prepare_ex(GQ_ACT_Q8_1, B, N, K, ldb, workspace, workspace_bytes, stream);
+}
+
+int gq_act_prepare_grouped(gq_act act, const gq_prep_item *items, int n, void *stream)
+{
+    g_err.clear();
+    if (n < 0 || (n > 0 && !items)) return fail(GQ_EINVAL, "bad item list (n=%d, items=%p)", n, (const void *)items);
+    // every item checked first (gq_act_prepare_ex's checks, in its order): a bad item launches nothing
+    for (int i = 0; i < n; ++i) {
+        const gq_prep_item &it = items[i];
+        const int64_t N = it.N, K = it.K;
+        if (N < 0 || K < 0) return fail(GQ_EINVAL, "item %d: negative size", i);
+        if (K % 32 != 0) return fail(GQ_EINVAL, "item %d: K=%lld is not a multiple of 32", i, (long long)K);
+        const int rc = check_act(act, K);
+        if (rc != GQ_OK) return rc;
+        if (N == 0 || K == 0) continue;
+        if (!it.B) return fail(GQ_EINVAL, "item %d: null activation pointer", i);
+        if (it.ldb < K) return fail(GQ_EINVAL, "item %d: ldb=%lld < K=%lld", i, (long long)it.ldb, (long long)K);
+        const size_t need = act_bytes(act, N, K);
+        if (!it.workspace || it.workspace_bytes < need)
+            return fail(GQ_EINVAL, "item %d: workspace %zu bytes < required %zu", i,
+                        it.workspace ? it.workspace_bytes : (size_t)0, need);
+    }
+    const hipStream_t s = (hipStream_t)stream;
+    gq::DeqSeg segs[gq::kMaxDeqSegs];
+    int ns = 0;
+    auto flush = [&]() -> int {
+        if (ns == 0) return GQ_OK;
+        const hipError_t e = gq::launch_act_quant_deq_grouped(segs, ns, s);
+        ns = 0;
+        if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (grouped act_quant): %s", hipGetErrorString(e));
+        return GQ_OK;
+    };
+    for (int i = 0; i < n; ++i) {
+        const gq_prep_item &it = items[i];
+        const int64_t N = it.N, K = it.K;
+        if (N == 0 || K == 0) continue;
+        int rc;
+        if (act != GQ_ACT_Q8_1 || use_gemv(N, K) || use_i8(GQ_Q8_0, N, K)) { // its own launch(es), as gq_act_prepare_ex
+            if ((rc = prepare(act, it.B, N, K, it.ldb, it.workspace, it.workspace_bytes, s,
+                              use_i8(GQ_Q8_0, N, K) ? 3 : 1)) != GQ_OK)
+                return rc;
+            continue;
+        }
+        if (ns == gq::kMaxDeqSegs && (rc = flush()) != GQ_OK) return rc;
+        // the fp16 x~ form sits at the front of the workspace (carve)
+        segs[ns++] = gq::DeqSeg{(const uint16_t *)it.B, it.ldb, N, K, carve(act, it.workspace, N, K).xdeq, 0};
+    }
+    return flush();
 }
 
 int gq_mmq_prepared_ex(gq_type t, gq_act act, const void *A, void *workspace, size_t workspace_bytes, void *C,

@@ -33,6 +33,11 @@ class GroupItem(ctypes.Structure):
                 ("M", _I64), ("K", _I64)]
 
 
+class PrepItem(ctypes.Structure):
+    """gq_prep_item (include/gguf_mmq.h)."""
+    _fields_ = [("B", _P), ("N", _I64), ("K", _I64), ("ldb", _I64), ("workspace", _P), ("workspace_bytes", _SZ)]
+
+
 SIGNATURES = {
     "gq_block_elems": ([_I], _I),
     "gq_block_bytes": ([_I], _I),
@@ -54,6 +59,7 @@ SIGNATURES = {
     "gq_mmq_sharded_workspace_size": ([_I, _I64, _I64, _I64, _I], _SZ),
     "gq_mmq_sharded": ([_I, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _I, _P, _P, _SZ, _P], _I),
     "gq_mmq_grouped": ([ctypes.POINTER(GroupItem), _I, _I64, _P], _I),
+    "gq_act_prepare_grouped": ([_I, ctypes.POINTER(PrepItem), _I, _P], _I),
     "gq_last_error": ([], ctypes.c_char_p),
     "gq_version": ([], _I),
     "gq_debug_set_tuning": ([ctypes.c_char_p, ctypes.c_longlong], _I),
@@ -271,6 +277,26 @@ def act_prepare(B: torch.Tensor, N: int, K: int, workspace: torch.Tensor, act: s
         stream = torch.cuda.current_stream(B.device).cuda_stream
         _check(lib().gq_act_prepare_ex(ACTS[act], B.data_ptr(), N, K, B.stride(0), workspace.data_ptr(),
                                        workspace.numel(), stream))
+
+
+def act_prepare_grouped(items, act: str = "q8_1"):
+    """Several act_prepare calls in as few launches as possible (gq_act_prepare_grouped):
+    items = [(B, N, K, workspace), ...] -- each workspace gets exactly what act_prepare would
+    write; one launch per 8 items whose form is the GEMM paths' fp16 x~ (q8_1, N >= 5)."""
+    if not items:
+        return
+    dev = items[0][0].device
+    arr = (PrepItem * len(items))()
+    keep = []
+    for i, (B, N, K, ws) in enumerate(items):
+        B = _check_acts(B, N, K)
+        _check_workspace(ws, 0, B.device)
+        if B.device != dev:
+            raise RuntimeError("grouped items must share one device")
+        keep.append(B)
+        arr[i] = PrepItem(B.data_ptr(), N, K, B.stride(0), ws.data_ptr(), ws.numel())
+    with torch.cuda.device(dev):
+        _check(lib().gq_act_prepare_grouped(ACTS[act], arr, len(items), torch.cuda.current_stream(dev).cuda_stream))
 
 
 def mmq_prepared(gtype: int, A: torch.Tensor, workspace: torch.Tensor, M: int, N: int, K: int,

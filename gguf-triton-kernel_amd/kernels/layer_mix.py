@@ -14,7 +14,9 @@ weight bytes, each matrix's rows bit-identical to its own call).  Measured (Q4_K
 graph-replayed, profiles/r03/tails/grouped_q6k_weight_ab.log): 28.8 / 42.3 / 58.8 / 59.5 us at
 1 / 2 / 3 / 4 tokens vs 44.2 / 54.1 / 79.9 / 80.2 for the fused sets' own launches.  grouped="auto"
 and True take it at 1..4 tokens (a call the grouped launch refuses -- e.g. a long-K Q6_K item
-at 3..4 tokens -- runs the sets' own launches), False never.
+at 3..4 tokens -- runs the sets' own launches), False never.  From 5 tokens on (q8_1) the four
+inputs' activations are quantized in one launch (gq_act_prepare_grouped) and every call reads
+them prepared: one act_quant launch per layer instead of four.
 """
 from __future__ import annotations
 
@@ -124,6 +126,22 @@ class LayerMix:
             if outs is not None:
                 res.update(zip(keys, outs))
                 done = True
+        if not done and self.act == "q8_1" and all(inp.shape[0] == x.shape[0] for inp in inputs) and x.shape[0] > 4:
+            # every input group's activations quantized in ONE launch (gq_act_prepare_grouped),
+            # then every call prepared -- bit-identical to each call quantizing its own input
+            N = x.shape[0]
+            preps, wss = [], []
+            for calls, inp in zip(self.calls, inputs):
+                ws_bytes = max(L.workspace_bytes(N, self.act) for _, L in calls)
+                ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=inp.device)
+                preps.append((inp, N, inp.shape[1], ws))
+                wss.append(ws)
+            _lib.act_prepare_grouped(preps, act=self.act)
+            for calls, inp, ws in zip(self.calls, inputs, wss):
+                for key, L in calls:
+                    res[key] = _lib.mmq_prepared(L.gtype, L.A, ws, L.M, N, inp.shape[1],
+                                                 self._out(key, L, N, inp.device, out), act=self.act)
+            done = True
         if not done:
             for calls, inp in zip(self.calls, inputs):
                 N, K = inp.shape

@@ -99,6 +99,24 @@ int gq_mmq_prepared_ex(gq_type t, gq_act act, const void *A, void *workspace, si
                        int64_t M, int64_t N, int64_t K, int64_t ldc, void *stream);
 
 /*
+ * Several gq_act_prepare_ex calls in as few launches as possible, e.g. the four inputs of one
+ * transformer block's projections (no reference counterpart: the reference quantizes inside
+ * every matmul).  Item i prepares B_i (N_i x K_i fp16, row stride ldb_i) into its own
+ * workspace exactly as gq_act_prepare_ex(act, B_i, ...) would -- the same bytes, the same
+ * errors.  Items whose prepared form is the fp16 x~ of the GEMM paths (GQ_ACT_Q8_1, N >= 5)
+ * share one launch per 8 items; the others are prepared one by one.  Every item is checked
+ * before anything is launched: a bad item (GQ_EINVAL / GQ_EUNSUPPORTED) launches nothing.
+ * No host sync.
+ */
+typedef struct gq_prep_item {
+    const void *B;
+    int64_t N, K, ldb;
+    void *workspace;
+    size_t workspace_bytes;
+} gq_prep_item;
+int gq_act_prepare_grouped(gq_act act, const gq_prep_item *items, int n, void *stream);
+
+/*
  * Dequantize packed `t` weights to fp16: W[m * ldw + k] = w (the reference's block formulas,
  * utils/quantize/{q8_0,q4_k,q6_k}.py dequantize, evaluated in fp32, rounded once to fp16).
  * M rows of K (a multiple of the block) elements.  gq_mmq uses the same kernel for its

@@ -162,6 +162,37 @@ def test_sharded_workspace_covers_every_rank(t, M, N, K):
             assert need >= local + (world + 1) * N * R * 2, (world, g, need, local)
 
 
+def test_prepare_grouped_host_argument_checks():
+    """gq_act_prepare_grouped checks every item before launching anything (host-side, no device
+    needed): a bad item anywhere in the list returns its error and nothing runs."""
+    import ctypes
+
+    import kernels._lib as kl
+    L = kl.lib()
+    q81 = kl.GQ_ACT_Q8_1
+    arr = (kl.PrepItem * 3)()
+    assert L.gq_act_prepare_grouped(q81, None, 2, None) == kl.GQ_EINVAL
+    assert L.gq_act_prepare_grouped(q81, arr, -1, None) == kl.GQ_EINVAL
+    assert L.gq_act_prepare_grouped(q81, arr, 0, None) == kl.GQ_OK           # nothing to do
+    fake = ctypes.c_void_p(0x1000).value
+    big = 1 << 30
+    arr[0] = kl.PrepItem(fake, 8, 4096, 4096, fake, big)
+    arr[1] = kl.PrepItem(fake, 0, 4096, 4096, None, 0)                        # N = 0: skipped
+    arr[2] = kl.PrepItem(fake, 8, 4010, 4010, fake, big)                      # K % 32 != 0
+    assert L.gq_act_prepare_grouped(q81, arr, 3, None) == kl.GQ_EINVAL
+    assert b"item 2" in L.gq_last_error()
+    arr[2] = kl.PrepItem(fake, 8, 4096, 100, fake, big)                       # ldb < K
+    assert L.gq_act_prepare_grouped(q81, arr, 3, None) == kl.GQ_EINVAL
+    assert b"ldb" in L.gq_last_error()
+    arr[2] = kl.PrepItem(fake, 8, 4096, 4096, fake, 16)                       # short workspace
+    assert L.gq_act_prepare_grouped(q81, arr, 3, None) == kl.GQ_EINVAL
+    assert b"workspace" in L.gq_last_error()
+    arr[2] = kl.PrepItem(None, 8, 4096, 4096, fake, big)                      # null B
+    assert L.gq_act_prepare_grouped(q81, arr, 3, None) == kl.GQ_EINVAL
+    arr[2] = kl.PrepItem(fake, 8, 4096, 4096, fake, big)
+    assert L.gq_act_prepare_grouped(7, arr, 3, None) == kl.GQ_EUNSUPPORTED  # unknown activation format
+
+
 def test_grouped_host_argument_checks():
     """gq_mmq_grouped's argument checks, host-side (nothing launched, no device needed)."""
     import ctypes

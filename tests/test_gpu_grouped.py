@@ -3,7 +3,9 @@ stream_decode_grouped_kernel): several matrices of their own types, activations 
 one launch at 1..4 tokens.  Each projection vs the oracle (sampled rows, IDEAL at the decode
 tolerance and the reference's 1% gate vs EXACT) and bit for bit vs its own gq_mmq call; the
 Llama-7B Q4_K_M layer through LayerMix grouped and ungrouped; what is not a grouped shape is
-refused without launching."""
+refused without launching.  The grouped activation prepare (gq_act_prepare_grouped): the same
+workspace bytes as one gq_act_prepare per input, and LayerMix at 5+ tokens (one prepare launch
+for the layer) bit-identical to one mmq() per projection."""
 import numpy as np
 import pytest
 import torch
@@ -144,3 +146,55 @@ def test_layer_mix_grouped_matches_ungrouped(N):
     for n in LLAMA_LAYER_SHAPES:
         assert rg[n].data_ptr() == out[n].data_ptr(), n
         assert torch.equal(rg[n].view(torch.int16), ru[n].view(torch.int16)), n
+
+
+def test_act_prepare_grouped_matches_individual():
+    """gq_act_prepare_grouped writes exactly the bytes gq_act_prepare writes per item: GEMM-form
+    items (N >= 5, several per launch, more than one launch's 8), a strided activation view, a
+    decode-form item (N <= 4, prepared on its own), an empty item."""
+    import kernels._lib as kl
+    dev = _dev()
+    specs = [(8, 4096), (8, 11008), (3, 2048), (64, 1024), (0, 512), (16, 4096), (5, 2816), (128, 4096),
+             (7, 32), (9, 256), (12, 4096), (6, 11008)]
+    wide = torch.from_numpy(random_activations(8, 4096 + 512, seed=77)).to(dev)
+    items, ref = [], []
+    for i, (N, K) in enumerate(specs):
+        B = wide[:, 256:256 + K] if i == 0 else torch.from_numpy(random_activations(N, K, seed=i)).to(dev)
+        need = kl.workspace_size(kl.GQ_Q4_K, 256, N, K) if N else 16
+        ws, ws_ref = (torch.zeros(need, dtype=torch.uint8, device=dev) for _ in range(2))
+        items.append((B, N, K, ws))
+        if N:
+            kl.act_prepare(B, N, K, ws_ref)
+        ref.append(ws_ref)
+    kl.act_prepare_grouped(items)
+    torch.cuda.synchronize()
+    for (B, N, K, ws), ws_ref in zip(items, ref):
+        assert torch.equal(ws, ws_ref), (N, K)
+
+
+@pytest.mark.parametrize("N", [5, 8, 16, 64, 128])
+def test_layer_mix_prepared_matches_per_call(N):
+    """LayerMix from 5 tokens (the four inputs quantized in one gq_act_prepare_grouped launch, every
+    projection prepared): unfused, every projection bit-identical to its own mmq(); fused (q+k and
+    gate+up as one taller matrix, whose split-K plan may differ from the parts') within the GEMM
+    tolerance of the unfused result."""
+    import kernels._lib as kl
+    from gguf import LLAMA_LAYER_SHAPES, q4_k_m_layer_types
+    from kernels.layer_mix import GGUFLinear, LayerMix
+    dev = _dev()
+    types = q4_k_m_layer_types(0, 32)
+    _, A = _layer(types, seed=9)
+    lins = {n: GGUFLinear(types[n], A[n], M, K) for n, (M, K) in LLAMA_LAYER_SHAPES.items()}
+    x = torch.from_numpy(random_activations(N, 4096, seed=15)).to(dev)
+    a = torch.from_numpy(random_activations(N, 4096, seed=16)).to(dev)
+    y = torch.from_numpy(random_activations(N, 4096, seed=17)).to(dev)
+    h = torch.from_numpy(random_activations(N, 11008, seed=18)).to(dev)
+    res = LayerMix(lins, fuse=False).forward(x, h, attn=a, x_ffn=y)
+    fused = LayerMix(lins).forward(x, h, attn=a, x_ffn=y)
+    inp = {"attn_q": x, "attn_k": x, "attn_v": x, "attn_output": a, "ffn_gate": y, "ffn_up": y, "ffn_down": h}
+    torch.cuda.synchronize()
+    for n, (M, K) in LLAMA_LAYER_SHAPES.items():
+        solo = kl.mmq(kl.TYPES[types[n]], A[n], inp[n], M, N, K)
+        torch.cuda.synchronize()
+        assert torch.equal(res[n].view(torch.int16), solo.view(torch.int16)), n
+        assert O.max_rel_err(fused[n].cpu().numpy(), solo.cpu().numpy()) <= 4e-3, n
