@@ -175,6 +175,19 @@ template <> struct UnitLoad<Q6_K> {
         sc8 = (u32x2){s[0], s[1]};
         dbits = *(const uint16_t *)(p + 208);
     }
+    // from the decode ring's aligned image (mmq_decode.hip, kImgSB): super-blocks at a 224-byte
+    // stride, bytes 0..207 as packed, d at 222 -- every field at its natural alignment
+    __device__ __forceinline__ void load_img(const uint8_t *__restrict__ rowp, int u)
+    {
+        const int sb = u >> 2, h = (u >> 1) & 1, v = u & 1;
+        const uint8_t *p = rowp + 224 * sb;
+        l0 = *(const u32x4 *)(p + 64 * h + 32 * v);
+        l1 = *(const u32x4 *)(p + 64 * h + 32 * v + 16);
+        g0 = *(const u32x4 *)(p + 128 + 32 * h);
+        g1 = *(const u32x4 *)(p + 144 + 32 * h);
+        sc8 = *(const u32x2 *)(p + 192 + 8 * h);
+        dbits = *(const uint16_t *)(p + 222);
+    }
 };
 
 template <> struct UnitRaw<Q6_K> {

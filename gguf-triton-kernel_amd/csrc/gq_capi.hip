@@ -38,6 +38,10 @@ bool parse_key(Tuning &t, const char *key, long long v)
         if (v < 0 || v > 8) return false;
         t.decode_maxnt = (int)v;
     } else if (k == "GQ_DECODE_NT4_CACHE") t.decode_nt4_cache = v != 0;
+    else if (k == "GQ_DECODE_Q6_IMG") {
+        if (!in({-1, 0, 1})) return false;
+        t.decode_q6_img = (int)v;
+    }
     else if (k == "GQ_GEMM_AQ") t.gemm_aq = v != 0;
     else if (k == "GQ_GEMM_AQ_NB4") t.gemm_aq_nb4 = v != 0;
     else if (k == "GQ_GEMM_NB") {
@@ -93,7 +97,7 @@ void tuning_from_env(Tuning &t)
 {
     t = Tuning{};
     static const char *const keys[] = {"GQ_BLAS_MIN_TOKENS", "GQ_GEMM_MAX_BYTES", "GQ_GEMM_I8", "GQ_NO_FUSED_DECODE",
-                                       "GQ_DECODE_MAXNT", "GQ_DECODE_NT4_CACHE", "GQ_GEMM_AQ", "GQ_GEMM_AQ_NB4",
+                                       "GQ_DECODE_MAXNT", "GQ_DECODE_NT4_CACHE", "GQ_DECODE_Q6_IMG", "GQ_GEMM_AQ", "GQ_GEMM_AQ_NB4",
                                        "GQ_GEMM_NB", "GQ_GEMM_RG", "GQ_GEMM_LOADERS", "GQ_GEMM_SPLITS",
                                        "GQ_GEMM_PARTIAL", "GQ_GEMM_FUSED_REDUCE", "GQ_GEMV_CAP", "GQ_GEMV_R",
                                        "GQ_WGEMM", "GQ_WGEMM_RG", "GQ_WGEMM_NB", "GQ_WGEMM_SPLITS", "GQ_WGEMM_WD",

@@ -65,6 +65,26 @@ constexpr int LDS_CAP = 160 * 1024;
 template <int F, int NT> constexpr int UPC_OF = F == Q6_K && NT <= 2 ? 2 : 1;
 int upc_of(int fmt, int nt) { return fmt == Q6_K && nt <= 2 ? 2 : 1; }
 
+// Q6_K tasks land in the ring as an aligned image: every 210-byte super-block (2-byte aligned
+// in the tensor) becomes 224 bytes -- 13 pieces from its first byte (0..207) and one from byte
+// 194 (d at image byte 222) -- so the lanes' ql/qh/scale/d reads are naturally aligned LDS reads
+// (read from the packed bytes, ~90% of the kernel's LDS cycles were unaligned-access stalls).
+// Each lane's DMA source is per piece (2-byte aligned); a K = 8192 row is exactly 7 KiB.
+// Both rings give the same bits, so the choice is by speed alone (profiles/r03/q6_img_ab.log, us
+// packed -> image): K <= 4096 at every token count (4096^2 x1 7.1 -> 5.9, 11008x4096 x1/x4
+// 12.6 -> 11.4 / 17.3 -> 15.1); longer rows at 2-4 tokens (4096x11008 x2/x4 18.9 -> 17.3 /
+// 34.9 -> 32.3) except whole 7 KiB rows (K a multiple of 8192: 28672x8192 x2 39.4 -> 41.1),
+// where the packed ring's aligned 16-byte windows stream faster than per-piece misaligned
+// sources -- as at one token (4096x11008 12.2 -> 13.1, 28672x8192 36.8 -> 37.3).
+// GQ_DECODE_Q6_IMG=0/1 forces it.
+constexpr int kImgSB = 224;
+bool img_of(int fmt, int64_t K, int nt)
+{
+    if (fmt != Q6_K) return false;
+    if (tuning().decode_q6_img >= 0) return tuning().decode_q6_img == 1;
+    return K <= 4096 || (nt >= 2 && K % 8192 != 0);
+}
+
 struct DecodeGeom {
     int ngroups; // row groups (nseg == 1) or rows (nseg > 1)
     int G;       // rows per group (nseg == 1)
@@ -151,7 +171,7 @@ __device__ __forceinline__ void act_from_lds(Act<F, NT> &a, const uint8_t *codes
 // (stream_decode_kernel: the grid itself; stream_decode_grouped_kernel: a slice of a grid shared
 // by several matrices).  A row's arithmetic depends on F, NT and K only -- not on bx, gx or the
 // geometry's rows per task -- so a matrix computed inside a group gives the same bits as alone.
-template <int F, int NT, int ITC>
+template <int F, int NT, int ITC, int IM = 0>
 __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X, int64_t ldx,
                                             uint16_t *__restrict__ C, int M, int64_t N, int K, int64_t ldc,
                                             DecodeGeom geo, int bx, int gx, int by, uint8_t *smem)
@@ -177,6 +197,18 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
 
     const __amdgpu_buffer_rsrc_t wrs =
         __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, (int)(((uint32_t)M * RB + 15u) & ~15u), 0x00020000);
+    constexpr bool IMG = F == Q6_K && IM != 0;
+    const uint32_t RBI = IMG ? (uint32_t)(K / 256) * kImgSB : RB; // ring bytes per row
+    // IMG: the source offset, from the task's first byte, of the piece this lane moves in DMA
+    // instruction k (piece p = 64k + lane: super-block p / 14, piece p % 14)
+    uint32_t rel[IMG ? NI : 1];
+    if constexpr (IMG) {
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            const uint32_t p = 64u * k + (uint32_t)lane, sb = p / 14u, pc = p - 14u * sb;
+            rel[k] = 210u * sb + (pc < 13u ? 16u * pc : 194u);
+        }
+    }
 
     // this wave's contiguous range of row groups, and its task count
     const int W = gx * DW;
@@ -213,6 +245,12 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
         const uint32_t ws = st & ~15u, we = st + len;
         uint8_t *dst = ring + (j % NS) * SLOT;
         const bool real = j < ntask;
+        if constexpr (IMG) {
+#pragma unroll
+            for (int k = 0; k < NI; ++k) // pieces past the task re-read its first bytes (L2 hit)
+                dma16(wrs, dst + 1024 * k, real ? st + (rel[k] < len ? rel[k] : 0u) : 0x80000000u);
+            return;
+        }
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
             uint32_t o = ws + 1024u * k + 16u * lane;
@@ -358,10 +396,15 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
             // because direct reads here made the waitcnt pass add a vmcnt(0) before them, i.e.
             // wait for the task DMA just issued -- tools/check_waits.py)
             UnitLoad<Q6_K> l0, l1;
-            // (plain 2-byte aligned reads: the dword-aligned form, UnitLoad::load_lds, cut the
-            // unaligned-LDS stalls but measured 7-10% slower here -- profiles/r02/decode_lds_align_ab.txt)
-            l0.load(rowp, 2 * c, nb);
-            l1.load(rowp, 2 * c + 1, nb);
+            // (IMG = 0: plain 2-byte aligned reads; the dword-aligned form, UnitLoad::load_lds,
+            // cut the unaligned-LDS stalls but measured 7-10% slower -- profiles/r02/decode_lds_align_ab.txt)
+            if constexpr (IMG) {
+                l0.load_img(rowp, 2 * c);
+                l1.load_img(rowp, 2 * c + 1);
+            } else {
+                l0.load(rowp, 2 * c, nb);
+                l1.load(rowp, 2 * c + 1, nb);
+            }
             unit(l0, 2 * c, 2 * i, acc);
             unit(l1, 2 * c + 1, 2 * i + 1, acc);
             return;
@@ -376,6 +419,7 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
         // Q8_0: dword-aligned reads and a 2-byte shift (4096^2 decode 6.6 -> 5.6 us); Q4_K
         // blocks are 16-byte aligned in the ring; Q6_K: see above
         if constexpr (F == Q8_0) l.load_lds(rowp, u, nb);
+        else if constexpr (IMG) l.load_img(rowp, u);
         else l.load(rowp, u, nb);
 #endif
 #ifdef GQ_ABL_NODOT
@@ -414,7 +458,7 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
         const int g = gc, s = sc;
         window(g, s, st, len);
         next(gc, sc);
-        const uint8_t *base = ring + (j % NS) * SLOT + (st & 15u);
+        const uint8_t *base = ring + (j % NS) * SLOT + (IMG ? 0u : (st & 15u));
 #ifdef GQ_ABL_NOCOMP
         acc[0] += (float)base[lane];
         if (j == ntask - 1 && acc[0] == 1234.5f) C[0] = 0;
@@ -427,7 +471,7 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
             auto pass = [&](int rp, float (&a)[NT]) {
                 const int r = rp + lrow;
                 const bool valid = r < nr;
-                const uint8_t *rowp = base + (uint32_t)(valid ? r : 0) * RB;
+                const uint8_t *rowp = base + (uint32_t)(valid ? r : 0) * RBI;
                 if constexpr (ITC > 0) {
 #pragma unroll
                     for (int i = 0; i < ITC; ++i) {
@@ -466,7 +510,7 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
             }
         } else {
             const int u0 = s * geo.segu, c0 = u0 / UPC, c1 = c0 + geo.segu / UPC;
-            const uint8_t *rowp = base - unit_byte<F>(u0, nb);
+            const uint8_t *rowp = base - (IMG ? (uint32_t)kImgSB * (uint32_t)(u0 >> 2) : unit_byte<F>(u0, nb));
             if constexpr (ITC > 0) {
 #pragma unroll
                 for (int i = 0; i < ITC; ++i) {
@@ -511,18 +555,19 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
 #endif
 }
 
-template <int F, int NT, int ITC>
+template <int F, int NT, int ITC, int IM>
 __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *__restrict__ A,
                                                                 const uint16_t *__restrict__ X, int64_t ldx,
                                                                 uint16_t *__restrict__ C, int M, int64_t N, int K,
                                                                 int64_t ldc, DecodeGeom geo)
 {
     extern __shared__ __attribute__((aligned(1024))) uint8_t smem[];
-    decode_body<F, NT, ITC>(A, X, ldx, C, M, N, K, ldc, geo, (int)blockIdx.x, (int)gridDim.x, (int)blockIdx.y, smem);
+    decode_body<F, NT, ITC, IM>(A, X, ldx, C, M, N, K, ldc, geo, (int)blockIdx.x, (int)gridDim.x, (int)blockIdx.y, smem);
 }
 
 struct Pick {
     int nt, itc;
+    bool img = false;       // Q6_K: the aligned ring image (kImgSB)
     bool lds_split = false; // fewer tokens per workgroup than wanted: the activations do not fit LDS
     size_t lds;
     DecodeGeom geo;
@@ -564,10 +609,13 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p, int wgs = 0)
         p.lds_split = true;
     }
     p.lds = (size_t)RING + act_lds(fmt, p.nt, K);
-    const int64_t RB = row_bytes(fmt, K);
+    // ring bytes per row and per task (the 16-byte aligned window of a packed task may start up
+    // to 14 bytes before it; the Q6_K image starts at the slot)
+    const bool img = p.img = img_of(fmt, K, p.nt);
+    const int64_t RB = img ? K / 256 * kImgSB : row_bytes(fmt, K);
     const int64_t upr = (K + 63) / 64;
     const int64_t cpr = upr / upc_of(fmt, p.nt); // lane chunks per row
-    const int64_t cap = NI * 1024 - 16;
+    const int64_t cap = img ? NI * 1024 : NI * 1024 - 16;
     const int per_cu = (int)(LDS_CAP / p.lds) > 0 ? (int)(LDS_CAP / p.lds) : 1;
     int64_t W = (int64_t)256 * per_cu * DW; // waves the chip holds (or the granted workgroups')
     if (wgs > 0) W = (int64_t)wgs * DW;
@@ -587,7 +635,7 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p, int wgs = 0)
         while ((1 << lp2) < cpr && lp2 < 6) ++lp2;
         g.lp2 = lp2;
     } else {
-        const int64_t unit64 = fmt == Q8_0 ? 64 * 68 : (fmt == Q4_K ? 64 * 36 : 64 * 210 / 4);
+        const int64_t unit64 = fmt == Q8_0 ? 64 * 68 : (fmt == Q4_K ? 64 * 36 : 64 * (img ? kImgSB : 210) / 4);
         if (cap < unit64) return false; // a 64-unit segment must fit one task (tuning builds with small NI)
         g.G = 1;
         g.segu = (int)(64 * (cap / unit64));
@@ -608,19 +656,19 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p, int wgs = 0)
     return true;
 }
 
-template <int F, int NT, int ITC>
+template <int F, int NT, int ITC, int IM = 0>
 hipError_t launch_t(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, int64_t M, int64_t N, int64_t K,
                     int64_t ldc, const Pick &p, hipStream_t s)
 {
     static bool attr = false; // raise the dynamic LDS limit once per instantiation
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void *)stream_decode_kernel<F, NT, ITC>,
+        hipError_t e = hipFuncSetAttribute((const void *)stream_decode_kernel<F, NT, ITC, IM>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, LDS_CAP);
         if (e != hipSuccess) return e;
         attr = true;
     }
     dim3 grid((unsigned)p.grid, (unsigned)((N + NT - 1) / NT)), block(DW * 64);
-    stream_decode_kernel<F, NT, ITC><<<grid, block, p.lds, s>>>(A, X, ldx, C, (int)M, N, (int)K, ldc, p.geo);
+    stream_decode_kernel<F, NT, ITC, IM><<<grid, block, p.lds, s>>>(A, X, ldx, C, (int)M, N, (int)K, ldc, p.geo);
     return hipGetLastError();
 }
 
@@ -629,7 +677,20 @@ hipError_t launch_f(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *
                     int64_t ldc, const Pick &p, hipStream_t s)
 {
 #define GQ_LT(nt, itc) launch_t<F, nt, itc>(A, X, ldx, C, M, N, K, ldc, p, s)
+#define GQ_LTI(nt, itc) launch_t<F, nt, itc, 1>(A, X, ldx, C, M, N, K, ldc, p, s)
     if constexpr (F == Q6_K) { // pick(): at most 8 cached units (4 chunks), 2 with two tokens
+        if (p.img) switch (p.nt * 8 + p.itc) {
+            case 8: return GQ_LTI(1, 0);
+            case 9: return GQ_LTI(1, 1);
+            case 10: return GQ_LTI(1, 2);
+            case 11: return GQ_LTI(1, 3);
+            case 12: return GQ_LTI(1, 4);
+            case 16: return GQ_LTI(2, 0);
+            case 17: return GQ_LTI(2, 1);
+            case 32: return GQ_LTI(4, 0);
+            case 33: return GQ_LTI(4, 1);
+            default: return hipErrorInvalidValue;
+            }
         switch (p.nt * 8 + p.itc) {
         case 8: return GQ_LT(1, 0);
         case 9: return GQ_LT(1, 1);
@@ -663,6 +724,7 @@ hipError_t launch_f(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *
         }
     }
 #undef GQ_LT
+#undef GQ_LTI
     return hipErrorInvalidValue;
 }
 
@@ -676,7 +738,7 @@ struct GroupedProblem {
     int64_t ldc;
     int M, K;
     DecodeGeom geo;
-    int code;       // fmt * 16 + itc
+    int code;       // fmt * 16 + itc (+ 8: the Q6_K aligned image)
     int block0, gx; // this (problem, token group)'s workgroups: [block0, block0 + gx)
     int by;         // its token group
 };
@@ -699,26 +761,32 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_grouped_kernel(const Gr
     case f * 16 + itc:                                                                                                 \
         decode_body<f, NT, itc>(q.A, q.X, q.ldx, q.C, q.M, args.N, q.K, q.ldc, q.geo, bx, q.gx, q.by, smem);         \
         return;
+#define GQ_GBI(itc)                                                                                                    \
+    case Q6_K * 16 + 8 + itc:                                                                                          \
+        decode_body<Q6_K, NT, itc, 1>(q.A, q.X, q.ldx, q.C, q.M, args.N, q.K, q.ldc, q.geo, bx, q.gx, q.by, smem);   \
+        return;
     if constexpr (NT == 1) {
         switch (q.code) {
             GQ_GB(Q8_0, 0) GQ_GB(Q8_0, 1) GQ_GB(Q8_0, 2) GQ_GB(Q8_0, 3) GQ_GB(Q8_0, 4) GQ_GB(Q8_0, 5) GQ_GB(Q8_0, 6)
             GQ_GB(Q8_0, 7) GQ_GB(Q4_K, 0) GQ_GB(Q4_K, 1) GQ_GB(Q4_K, 2) GQ_GB(Q4_K, 3) GQ_GB(Q4_K, 4) GQ_GB(Q4_K, 5)
             GQ_GB(Q4_K, 6) GQ_GB(Q4_K, 7) GQ_GB(Q6_K, 0) GQ_GB(Q6_K, 1) GQ_GB(Q6_K, 2) GQ_GB(Q6_K, 3) GQ_GB(Q6_K, 4)
+            GQ_GBI(0) GQ_GBI(1) GQ_GBI(2) GQ_GBI(3) GQ_GBI(4)
         default: return;
         }
     } else if constexpr (NT == 2) {
         switch (q.code) {
             GQ_GB(Q8_0, 0) GQ_GB(Q8_0, 1) GQ_GB(Q8_0, 2) GQ_GB(Q8_0, 3) GQ_GB(Q8_0, 4) GQ_GB(Q4_K, 0) GQ_GB(Q4_K, 1)
-            GQ_GB(Q4_K, 2) GQ_GB(Q4_K, 3) GQ_GB(Q4_K, 4) GQ_GB(Q6_K, 0) GQ_GB(Q6_K, 1)
+            GQ_GB(Q4_K, 2) GQ_GB(Q4_K, 3) GQ_GB(Q4_K, 4) GQ_GB(Q6_K, 0) GQ_GB(Q6_K, 1) GQ_GBI(0) GQ_GBI(1)
         default: return;
         }
     } else {
         switch (q.code) {
-            GQ_GB(Q8_0, 0) GQ_GB(Q8_0, 1) GQ_GB(Q4_K, 0) GQ_GB(Q4_K, 1) GQ_GB(Q6_K, 0) GQ_GB(Q6_K, 1)
+            GQ_GB(Q8_0, 0) GQ_GB(Q8_0, 1) GQ_GB(Q4_K, 0) GQ_GB(Q4_K, 1) GQ_GB(Q6_K, 0) GQ_GB(Q6_K, 1) GQ_GBI(0) GQ_GBI(1)
         default: return;
         }
     }
 #undef GQ_GB
+#undef GQ_GBI
 }
 
 template <int NT>
@@ -858,7 +926,7 @@ hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipS
             q.M = (int)items[i].M;
             q.K = (int)items[i].K;
             q.geo = p.geo;
-            q.code = items[i].fmt * 16 + p.itc;
+            q.code = items[i].fmt * 16 + p.itc + (p.img ? 8 : 0);
             q.block0 = blocks;
             q.gx = p.grid;
             q.by = py[j];

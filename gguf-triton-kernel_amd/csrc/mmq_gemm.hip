@@ -160,7 +160,12 @@ struct Cfg {
     // NL > 0: NL more waves that only issue the DMAs (loader waves); 0: every wave issues its share
     static constexpr int BN = 16 * NB, BM = 16 * NWAVE * RG;
     static constexpr int ISSUERS = NL > 0 ? NL : NWAVE, THREADS = 64 * (NWAVE + NL);
-    static constexpr int RBW = WStage<F>::RBW, NPW = RBW / 16, SPW = WStage<F>::SPW;
+    // Q6_K 256-row tiles: 224-B row images (14 pieces, no repeated d piece) so that two weight
+    // slots and three activation slots fit the 160 KiB; rows 8..15 of every 16 store their
+    // pieces pairwise swapped (LDS byte offset ^ 16), which keeps the 56-dword row stride's
+    // rows l and l+8 of a fragment read on distinct banks
+    static constexpr bool Q6S = F == Q6_K && RG == 2;
+    static constexpr int RBW = Q6S ? 224 : WStage<F>::RBW, NPW = RBW / 16, SPW = WStage<F>::SPW;
     static constexpr int W_REAL = BM * NPW / 64;                              // DMA instructions per stage
     // code-form (AF_I8 / AF_F8) activation sub-stage: BN x 64 code bytes (CI instructions), then
     // one instruction for the tile's scales of the sub-stage's two blocks (2 x BN floats)
@@ -211,12 +216,13 @@ struct Cfg {
 // ---------------------------------------------------------------------------------------
 // A fragments of sub-stage s4 for this lane's row: frag[s] = the 8 weights (fragment element
 // order) of k-step s, k-group g.  wr = the row's stage bytes in LDS (block byte 0).
+// sx: byte-offset XOR of the row's image (Q6_K 256-row tiles, Cfg::Q6S; 0 otherwise).
 template <int F>
-__device__ __forceinline__ void stage_frags(const uint8_t *wr, int g, int s4, f16x8 (&frag)[2]);
+__device__ __forceinline__ void stage_frags(const uint8_t *wr, int g, int s4, f16x8 (&frag)[2], int sx);
 
 // Q4_K sub-stage q: sub-blocks 2q (low nibbles) and 2q+1 (high nibbles) of qs bytes 32q..+32.
 template <>
-__device__ __forceinline__ void stage_frags<Q4_K>(const uint8_t *wr, int g, int q, f16x8 (&frag)[2])
+__device__ __forceinline__ void stage_frags<Q4_K>(const uint8_t *wr, int g, int q, f16x8 (&frag)[2], int)
 {
     const u32x4 hdr = *(const u32x4 *)wr;
     const float d = h2f(hdr.x & 0xffffu), dmin = h2f(hdr.x >> 16);
@@ -241,17 +247,17 @@ __device__ __forceinline__ void stage_frags<Q4_K>(const uint8_t *wr, int g, int 
 // Q6_K sub-stage s4 = (h, v): k-step 0 = elements 128h+32v+[0,32) (ql[64h+32v..] low nibbles,
 // qh bits 2v), k-step 1 = 128h+64+32v+[0,32) (same ql bytes, high nibbles; qh bits 4+2v).
 template <>
-__device__ __forceinline__ void stage_frags<Q6_K>(const uint8_t *wr, int g, int s4, f16x8 (&frag)[2])
+__device__ __forceinline__ void stage_frags<Q6_K>(const uint8_t *wr, int g, int s4, f16x8 (&frag)[2], int sx)
 {
     const int h = s4 >> 1, v = s4 & 1;
-    const float d = h2f(*(const uint16_t *)(wr + 222)); // image: d at 222 (see issue_w)
-    const u32x2 ql = *(const u32x2 *)(wr + 64 * h + 32 * v + 8 * g);
-    const u32x2 qh = *(const u32x2 *)(wr + 128 + 32 * h + 8 * g);
+    const float d = h2f(*(const uint16_t *)(wr + (222 ^ sx))); // image: d at 222 (see issue_w)
+    const u32x2 ql = *(const u32x2 *)(wr + ((64 * h + 32 * v + 8 * g) ^ sx));
+    const u32x2 qh = *(const u32x2 *)(wr + ((128 + 32 * h + 8 * g) ^ sx));
     const h2 bias = splat(-1056.f); // 1024 + 32
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
         // sub-block of elements 128h + 64n + 32v + 8g..: 8h + 4n + 2v + (g >> 1)
-        const float scv = (float)*(const int8_t *)(wr + 192 + 8 * h + 4 * n + 2 * v + (g >> 1));
+        const float scv = (float)*(const int8_t *)(wr + ((192 + 8 * h + 4 * n + 2 * v + (g >> 1)) ^ sx));
         const h2 dsc = splat(d * scv);
         const int sq = 4 * n + 2 * v;
         const uint32_t c0 = ((ql.x >> (4 * n)) & 0x0f0f0f0fu) | (((qh.x >> sq) & 0x03030303u) << 4);
@@ -269,7 +275,7 @@ __device__ __forceinline__ void stage_frags<Q6_K>(const uint8_t *wr, int g, int 
 #define GQ_Q8_UNALIGNED 0
 #endif
 template <>
-__device__ __forceinline__ void stage_frags<Q8_0>(const uint8_t *wr, int g, int u, f16x8 (&frag)[2])
+__device__ __forceinline__ void stage_frags<Q8_0>(const uint8_t *wr, int g, int u, f16x8 (&frag)[2], int)
 {
     const h2 bias = splat(-1152.f); // codes biased by +128 (xor 0x80)
 #pragma unroll
@@ -380,7 +386,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
 #pragma unroll
     for (int i = 0; i < G::NW; ++i) {
         const int p = 64 * (iw + G::ISSUERS * i) + lane, r = p / G::NPW;
-        wpc[i] = p - r * G::NPW;
+        wpc[i] = (p - r * G::NPW) ^ (G::Q6S ? (r >> 3) & 1 : 0); // the piece that lands at this lane's slot
         const int64_t row = m0 + r < M ? m0 + r : M - 1;
         wv[i] = r < G::BM ? (uint32_t)(row * row_bytes) : DUMMY;
     }
@@ -639,6 +645,32 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
                     }
                 continue;
             }
+            if constexpr (RG == 2 && AM == AF_F16 && (ABL & (8 | 128)) == 0) {
+                // 256-row tiles (12 waves: at most 168 VGPRs a wave): the weight fragments of both
+                // row groups, then per k-step its 8 activation fragments and 16 MFMAs -- holding the
+                // whole sub-stage's activation fragments as below spilled 82-114 VGPRs
+                f16x8 af[RG][2];
+#pragma unroll
+                for (int rg = 0; rg < RG; ++rg)
+                    stage_frags<F>(wr + 16 * G::RBW * rg, g, s4, af[rg], G::Q6S ? ((l16 >> 3) & 1) << 4 : 0);
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    f16x8 bk[NB];
+#pragma unroll
+                    for (int t = 0; t < NB; ++t) {
+                        const int r = 16 * t + l16;
+                        bk[t] = *(const f16x8 *)(xs + 128 * r + 16 * ((4 * s + g) ^ act_swz(r)));
+                    }
+#pragma unroll
+                    for (int rg = 0; rg < RG; ++rg)
+#pragma unroll
+                        for (int t = 0; t < NB; ++t) {
+                            if constexpr (ABL & 1) acc[rg][t][0] += (float)af[rg][s][t & 7] * (float)bk[t][0];
+                            else acc[rg][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[rg][s], bk[t], acc[rg][t], 0, 0, 0);
+                        }
+                }
+                continue;
+            }
             // all of the sub-stage's activation fragments first (one LDS round trip), the
             // dequantization beside them, then the MFMAs
             f16x8 bfr[2][NB];
@@ -670,7 +702,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
                     af[rg][0] = *(const f16x8 *)(wrg + 0);
                     af[rg][1] = *(const f16x8 *)(wrg + 16);
                 } else {
-                    stage_frags<F>(wrg, g, s4, af[rg]);
+                    stage_frags<F>(wrg, g, s4, af[rg], G::Q6S ? ((l16 >> 3) & 1) << 4 : 0);
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -778,7 +810,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
                     }
                 }
             }
-            if (cbase >= 0) {
+            if (RG == 1 && cbase >= 0) { // (128-row tiles only: the 256-row form's registers)
                 // fused reduce: the wave that arrives last at this (tile, wave) row group sums
                 // the row group's S partials in split order -- the arithmetic of
                 // gemm_reduce_f16_kernel, so the two forms give identical bits -- and writes C.
@@ -1042,7 +1074,7 @@ hipError_t launch_cfg(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P,
     const int cps = pl.chunks_per_split;
     const void *X = AQ ? (const void *)x.xraw : (G::CODES ? (const void *)x.xq : (const void *)x.xdeq);
     const int64_t ldd = AQ ? x.ldx : x.ldd;
-    const bool fused = pl.splits > 1 && pl.pf16 && pl.fused_reduce;
+    const bool fused = pl.splits > 1 && pl.pf16 && pl.fused_reduce && RG == 1;
     const int cb = fused ? split_counters((int)(grid.x * grid.y) * NWAVE) : -1;
 #ifdef GQ_ABLATION
     const int abl = tuning().ablate;
@@ -1075,7 +1107,7 @@ template <int F>
 hipError_t launch_fmt(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P, const GemmPlan &pl, int64_t M,
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
-    if constexpr (F == Q4_K)
+    if constexpr (F == Q4_K || F == Q6_K)
         if (pl.rg == 2 * R1 && pl.nb == 8)
             return pl.loaders == 4 ? launch_cfg<F, 8, 2 * R1, AF_F16, 4>(A, x, C, P, pl, M, N, K, ldc, s)
                                    : launch_cfg<F, 8, 2 * R1>(A, x, C, P, pl, M, N, K, ldc, s);
@@ -1139,9 +1171,13 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, int act)
     if (tuning().gemm_nb) p.nb = tuning().gemm_nb; // (validated: 1, 2, 4 or 8)
     // two 16-row groups per wave (256-row tiles: half the activation traffic per weight) for
     // tall matrices at full token tiles
-    // (Q4_K only: Q6_K's padded 240-B rows and Q8_0's 272-B rows do not fit 256 rows twice)
-    p.rg = (fmt == Q4_K && p.nb == 8 && M >= 8192) ? 2 * R1 : R1; // measured: 11008 rows 5% faster
-    if (tuning().gemm_rg) p.rg = (fmt == Q4_K && p.nb == 8 && tuning().gemm_rg == 2) ? 2 * R1 : R1;
+    // (Q4_K; Q6_K as a 224-B row image, Cfg::Q6S, only on request: half the activation re-reads
+    // but a 3-deep activation ring, measured slower -- 28672x8192 x128 116.5 vs 105.7 us,
+    // 8192x28672 106.0 vs 103.9, 4096^2 21.9 vs 16.8: profiles/r03/gemm_q6k_rg2_rejected.log;
+    // Q8_0's 272-B rows do not fit 256 rows twice)
+    const bool rg2_ok = (fmt == Q4_K || fmt == Q6_K) && p.nb == 8;
+    p.rg = (fmt == Q4_K && rg2_ok && M >= 8192) ? 2 * R1 : R1; // measured: Q4_K 11008 rows 5% faster
+    if (tuning().gemm_rg) p.rg = (rg2_ok && tuning().gemm_rg == 2) ? 2 * R1 : R1;
     if (p.act != AF_F16) p.rg = 1; // the code forms run 128-row tiles
     // four loader waves (DMA issue off the multiplying waves' path) for the 128-row fp16 form:
     // Q6_K 28672x8192x128 116.5 -> 103.7 us, Q4_K 4096^2x128 17.4 -> 16.7, Q8_0 4096^2x128

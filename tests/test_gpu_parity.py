@@ -286,12 +286,13 @@ def test_layer_mix_from_gguf(tmp_path, fuse):
             assert O.max_rel_err(out[n].cpu().numpy(), ideal) <= tight(N), (n, N)
 
 
-@pytest.mark.parametrize("fmt", ("q4_k",))
+@pytest.mark.parametrize("fmt", ("q4_k", "q6_k"))
 def test_gemm_256_row_tiles(fmt, tune):
     """Two 16-row groups per wave (256-row tiles) of the LDS-DMA GEMM, with and without split-K,
-    ragged edges."""
+    ragged edges (Q6_K: the 224-B pair-swizzled row image, mmq_gemm.hip Cfg::Q6S); without
+    split-K the same bits as 128-row tiles (a row's MFMA chain does not depend on the tile)."""
     tune(GQ_GEMM_RG=2, GQ_WGEMM=0)
-    for M, N, K, splits in ((600, 100, 1024, None), (300, 128, 2048, "4")):
+    for M, N, K, splits in ((600, 100, 1024, None), (300, 128, 2048, "4"), (8200, 128, 768, "3"), (530, 97, 1536, "1")):
         if splits:
             tune(GQ_GEMM_SPLITS=splits)
         qA = random_blocks(fmt, M, K, seed=M)
@@ -299,3 +300,7 @@ def test_gemm_256_row_tiles(fmt, tune):
         got = run(fmt, qA, B, M, N, K)
         ideal = O.mmq_from_fp16(fmt, qA, B, M, N, K, O.IDEAL)
         assert O.max_rel_err(got, ideal) <= TIGHT_GEMM, (M, N, K, O.max_rel_err(got, ideal))
+        if splits == "1":
+            tune(GQ_GEMM_RG=1)
+            assert np.array_equal(run(fmt, qA, B, M, N, K).view(np.int16), got.view(np.int16))
+            tune(GQ_GEMM_RG=2)

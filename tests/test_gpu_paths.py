@@ -371,3 +371,29 @@ def test_mmq_sharded_entry_point_rccl_one_rank():
         assert torch.equal(C.view(torch.int16), want.view(torch.int16))
     finally:
         rccl.ncclCommDestroy(comm)
+
+
+@pytest.mark.parametrize("M,K", [(300, 4096), (4096, 4096), (97, 2048), (1000, 8192), (64, 11008), (40, 28672), (33, 256)])
+def test_q6_k_decode_aligned_image_bit_identical(M, K, tune):
+    """The Q6_K decode ring as an aligned image (224-B super-blocks, per-piece DMA sources:
+    mmq_decode.hip kImgSB; the default for K <= 4096) gives the same bits as the packed ring at
+    1-4 tokens -- whole-row tasks of 1..16 rows, row segments (K = 11008, 28672), short rows --
+    alone and inside a grouped launch, and matches the oracle."""
+    from kernels._lib import TYPES, mmq, mmq_grouped
+    dev = _dev()
+    qA = random_blocks("q6_k", M, K, seed=M + K)
+    A_t = torch.from_numpy(qA.view(np.int8)).to(dev)
+    for N in (1, 2, 3, 4):
+        B = random_activations(N, K, seed=N + K)
+        B_t = torch.from_numpy(B).to(dev)
+        outs = {}
+        for img in (0, 1):
+            tune(GQ_DECODE_Q6_IMG=img)
+            outs[img] = mmq(TYPES["q6_k"], A_t, B_t, M, N, K)
+            g = mmq_grouped([(TYPES["q6_k"], A_t, B_t, M, K, None), (TYPES["q4_k"], A_t[: 144 * (K // 256)], B_t, 1, K, None)], N)
+            if g is not None:
+                assert torch.equal(g[0].view(torch.int16), outs[img].view(torch.int16)), (img, N)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16)), N
+        ideal = O.mmq_from_fp16("q6_k", qA, B, M, N, K, O.IDEAL)
+        assert O.max_rel_err(outs[1].cpu().numpy(), ideal) <= TIGHT_GEMV
