@@ -22,6 +22,9 @@
 //          block), codes = OCP e4m3 (e4m3fn) of x / X, round to nearest even; codes [rows][K]
 //          with each 4-group stored (0,2,1,3) (the GEMM's fragment order), X as float in the
 //          I8 form's block-major layout
+//   F8DEQ: the fp8 variant's x~ = fp16(code * X) in the DEQ layout: the F8 codes widened by
+//          v_cvt_scalef32_pk_f16_fp8 (code * 2^e is exact in fp16), so every fp16-activation
+//          kernel (skinny, GEMMs, hipBLASLt) runs the fp8 variant unchanged
 #include "gguf_blocks.hpp"
 #include "gguf_internal.hpp"
 #include "gguf_q8_1.hpp"
@@ -44,7 +47,7 @@ __device__ __forceinline__ void act_quant_body(const uint16_t *__restrict__ X, i
 
     u32x4 v = {0, 0, 0, 0};
     if (live) v = ld16(X + row * ldx + 32 * j + 8 * sub);
-    if constexpr (MODE == ACT_F8) {
+    if constexpr (MODE == ACT_F8 || MODE == ACT_F8DEQ) {
         const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
         float x[8], amax = 0.f;
 #pragma unroll
@@ -68,6 +71,18 @@ __device__ __forceinline__ void act_quant_body(const uint16_t *__restrict__ X, i
             int w = __builtin_amdgcn_cvt_pk_fp8_f32(x[4 * h] * inv, x[4 * h + 2] * inv, 0, false);
             w = __builtin_amdgcn_cvt_pk_fp8_f32(x[4 * h + 1] * inv, x[4 * h + 3] * inv, w, true);
             o[h] = (uint32_t)w;
+        }
+        if constexpr (MODE == ACT_F8DEQ) { // pairs (0,2), (1,3) of each 4-group, as the DEQ form
+            const float X = __builtin_bit_cast(float, (uint32_t)(127 + e) << 23);
+            typedef _Float16 h2t __attribute__((ext_vector_type(2)));
+            uint32_t d[4];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                d[2 * h] = __builtin_bit_cast(uint32_t, (h2t)__builtin_amdgcn_cvt_scalef32_pk_f16_fp8(o[h], X, false));
+                d[2 * h + 1] = __builtin_bit_cast(uint32_t, (h2t)__builtin_amdgcn_cvt_scalef32_pk_f16_fp8(o[h], X, true));
+            }
+            *(u32x4 *)(xdeq + row * K + 32 * j + 8 * sub) = (u32x4){d[0], d[1], d[2], d[3]};
+            return;
         }
         *(u32x2 *)(codes + row * K + 32 * j + 8 * sub) = (u32x2){o[0], o[1]};
         if (sub == 0) dout[j * ((rows + 3) & ~(int64_t)3) + row] = __builtin_bit_cast(float, (uint32_t)(127 + e) << 23);
@@ -168,6 +183,10 @@ hipError_t launch_act_quant(int mode, const uint16_t *X, int64_t ldx, int64_t ro
     case ACT_F8:
         act_quant_kernel<ACT_F8><<<grid, block, 0, s>>>(X, ldx, rows, K, nullptr, (int8_t *)out0, (float *)out1,
                                                          nullptr, nullptr);
+        break;
+    case ACT_F8DEQ:
+        act_quant_kernel<ACT_F8DEQ><<<grid, block, 0, s>>>(X, ldx, rows, K, nullptr, nullptr, nullptr, nullptr,
+                                                            (uint16_t *)out0);
         break;
     case ACT_I8:
         act_quant_kernel<ACT_I8><<<grid, block, 0, s>>>(X, ldx, rows, K, nullptr, (int8_t *)out0, (float *)out1,

@@ -44,10 +44,10 @@ const Tuning &tuning();
 int set_tuning(const char *key, long long value);
 void reset_tuning();
 
-enum ActMode : int { ACT_AOS = 0, ACT_SOA = 1, ACT_DEQ = 2, ACT_I8 = 3, ACT_F8 = 4 };
-// Activation form the MFMA GEMM reads (mmq_gemm.hip): fp16 x~, q8_1 codes (Q8_0 int8 MFMA),
-// or the fp8 variant's e4m3 codes.
-enum ActForm : int { AF_F16 = 0, AF_I8 = 1, AF_F8 = 2 };
+enum ActMode : int { ACT_AOS = 0, ACT_SOA = 1, ACT_DEQ = 2, ACT_I8 = 3, ACT_F8 = 4, ACT_F8DEQ = 5 };
+// Activation form the MFMA GEMM reads (mmq_gemm.hip): fp16 x~ (q8_1's, or the fp8 variant's
+// widened e4m3 codes) or q8_1 codes (Q8_0 int8 MFMA).
+enum ActForm : int { AF_F16 = 0, AF_I8 = 1 };
 
 // Activation quantizer (act_quant.hip).  AOS: out0 = q8_1 bytes.  SOA: out0 = int8 codes
 // [rows][K], out1 = float d [rows][K/32], out2 = float s [rows][K/32].  DEQ: out0 = fp16 x~.
@@ -55,6 +55,7 @@ enum ActForm : int { AF_F16 = 0, AF_I8 = 1, AF_F8 = 2 };
 // F8 (the fp8 activation variant, not q8_1): out0 = OCP e4m3 codes [rows][K], each 4-element
 // group stored (0,2,1,3); out1 = float 2^e [K/32][(rows + 3) & ~3], e the smallest integer with
 // max|x| <= 448 * 2^e over the block (2^0 for an all-zero block); code = e4m3(x / 2^e), RNE.
+// F8DEQ: out0 = fp16 code * 2^e [rows][K] in the DEQ layout (the fp8 variant's GEMM input).
 hipError_t launch_act_quant(int mode, const uint16_t *X, int64_t ldx, int64_t rows, int64_t K, void *out0,
                             void *out1, void *out2, hipStream_t s);
 // The DEQ form of up to kMaxDeqSegs tensors in one launch (wg0 is set by the launcher),

@@ -223,12 +223,14 @@ bool use_wgemm(int t, int form, int64_t N)
 // tokens: mixed (Q4_K +8% / -5% by shape), the GEMM.  GQ_SKINNY=1: every type at 1..32 tokens
 // the GEMM path would take (tests), 0: off.
 constexpr int64_t kSkinnyMinTokens = 5, kSkinnyMaxTokens = 16, kSkinnyForcedMax = 32;
-bool use_skinny(int t, int form, int64_t N)
+bool use_skinny(int t, int form, int64_t N, int act = GQ_ACT_Q8_1)
 {
     const int sk = gq::tuning().skinny;
     if (form != gq::AF_F16 || sk == 0) return false;
     if (sk == 1) return N <= kSkinnyForcedMax;
-    return (t == GQ_Q4_K || t == GQ_Q8_0) && N >= kSkinnyMinTokens && N <= kSkinnyMaxTokens;
+    // the fp8 variant has no decode kernel: its 1..4 tokens take the skinny kernel too
+    const int64_t lo = act == GQ_ACT_FP8_E4M3 ? 1 : kSkinnyMinTokens;
+    return (t == GQ_Q4_K || t == GQ_Q8_0) && N >= lo && N <= kSkinnyMaxTokens;
 }
 gq::SkinnyPlan skinny_plan(int t, int64_t M, int64_t N, int64_t K)
 {
@@ -255,8 +257,11 @@ bool use_i8(int t, int64_t N, int64_t K)
 }
 
 // Which kernels a call runs.  The q8_1 activations (the reference's semantics) go to the fused
-// decode / GEMV (N <= 4), the MFMA GEMM or, from blas_min_tokens(), dequant + hipBLASLt; the
-// fp8 variant (GQ_ACT_FP8_E4M3) always runs the MFMA GEMM on e4m3 codes.
+// decode / GEMV (N <= 4), the MFMA GEMMs or, from blas_min_tokens(), dequant + hipBLASLt; the
+// fp8 variant (GQ_ACT_FP8_E4M3) is quantized to e4m3 codes and widened to fp16 x~ by act_quant
+// (ACT_F8DEQ), then runs every fp16-activation kernel as q8_1's x~ does (skinny from one token:
+// there is no fp8 decode kernel).  (Widening the codes inside the GEMM instead, the round-2
+// AF_F8 form, cost 12-55% over the q8_1 path: profiles/r03/s3/fp8_deq_route.log.)
 struct Route {
     bool gemv = false, blas = false;
     int form = gq::AF_F16; // GEMM activation form
@@ -265,7 +270,7 @@ Route route(int t, int act, int64_t N, int64_t K)
 {
     Route r;
     if (act == GQ_ACT_FP8_E4M3) {
-        r.form = gq::AF_F8;
+        r.blas = use_blas(N, K);
         return r;
     }
     r.gemv = use_gemv(N, K);
@@ -284,7 +289,7 @@ size_t scale_bytes(int64_t N, int64_t K) { return align_up((size_t)(K / 32) * (s
 // Activation part of the workspace (what gq_act_prepare[_ex] writes); depends on act, N, K only.
 size_t act_bytes(int act, int64_t N, int64_t K)
 {
-    if (act == GQ_ACT_FP8_E4M3) return code_bytes(N, K) + scale_bytes(N, K);
+    if (act == GQ_ACT_FP8_E4M3) return deq_bytes(N, K); // the fp8 variant's x~
     if (use_gemv(N, K)) {
         // SOA q8_1: codes + d + s
         return align_up((size_t)N * K) + 2 * align_up((size_t)N * (K / 32) * sizeof(float));
@@ -301,7 +306,7 @@ size_t ws_bytes(int t, int act, int64_t M, int64_t N, int64_t K)
     else if (!r.gemv && gq::gemm_supported(t, K) && M > 0 && N > 0) {
         // split-K partials of the largest need over the launch shapes (full and remainder chunks)
         // (the kernel is chosen by the call's token count, so every chunk runs the same arithmetic)
-        const bool sk = use_skinny(t, r.form, N), wg = use_wgemm(t, r.form, N);
+        const bool sk = use_skinny(t, r.form, N, act), wg = use_wgemm(t, r.form, N);
         const int64_t mr = gemm_rows_per_launch(t, M, K), nt = sk ? N : gemm_toks_per_launch(N, K);
         size_t p = 0;
         for (int64_t mc : {mr, M % mr})
@@ -467,8 +472,7 @@ static Carved carve(int act, void *workspace, int64_t N, int64_t K)
     uint8_t *ws = (uint8_t *)workspace;
     Carved c{};
     if (act == GQ_ACT_FP8_E4M3) {
-        c.xq = (int8_t *)ws;
-        c.xd = (float *)(ws + code_bytes(N, K));
+        c.xdeq = (uint16_t *)ws;
     } else if (use_gemv(N, K)) {
         c.xq = (int8_t *)ws;
         c.xd = (float *)(ws + align_up((size_t)N * K));
@@ -495,7 +499,7 @@ static int prepare(int act, const void *B, int64_t N, int64_t K, int64_t ldb, vo
     Carved c = carve(act, workspace, N, K);
     hipError_t e = hipSuccess;
     if (act == GQ_ACT_FP8_E4M3) {
-        e = gq::launch_act_quant(gq::ACT_F8, (const uint16_t *)B, ldb, N, K, c.xq, c.xd, nullptr, s);
+        e = gq::launch_act_quant(gq::ACT_F8DEQ, (const uint16_t *)B, ldb, N, K, c.xdeq, nullptr, nullptr, s);
     } else if (use_gemv(N, K)) {
         e = gq::launch_act_quant(gq::ACT_SOA, (const uint16_t *)B, ldb, N, K, c.xq, c.xd, c.xs, s);
     } else {
@@ -533,7 +537,7 @@ static int compute(gq_type t, int act, const void *A, void *workspace, size_t wo
         // (the kernel is chosen by the call's token count: every chunk runs the same arithmetic)
         // (<= 32 skinny tokens are never cut: their x~ is far below the guard, and the token
         // count sets the kernel's K split)
-        const bool sk = use_skinny(t, r.form, N), wg = use_wgemm(t, r.form, N);
+        const bool sk = use_skinny(t, r.form, N, act), wg = use_wgemm(t, r.form, N);
         const int64_t mr = gemm_rows_per_launch(t, M, K), nt = sk ? N : gemm_toks_per_launch(N, K);
         e = hipSuccess;
         for (int64_t n0 = 0; n0 < N && e == hipSuccess; n0 += nt)
@@ -552,8 +556,8 @@ static int compute(gq_type t, int act, const void *A, void *workspace, size_t wo
                 }
                 gq::GemmAct x;
                 x.xdeq = c.xdeq ? c.xdeq + n0 * K : nullptr;
-                x.xq = c.xq + n0 * K;
-                x.xd = c.xd + n0;
+                x.xq = c.xq ? c.xq + n0 * K : nullptr;
+                x.xd = c.xd ? c.xd + n0 : nullptr;
                 x.ldd = scale_ld(N);
                 e = gq::launch_gemm(t, (const uint8_t *)A + m0 * row_bytes_of(t, K), x, (uint16_t *)C + n0 * ldc + m0,
                                     c.partials, gq::plan_gemm(t, mc, nc, K, r.form), mc, nc, K, ldc, s);

@@ -12,11 +12,10 @@
 //          they are (one 32-element block = one MFMA k-step, the reference's int dot,
 //          mmq_q8_0.py:85-88) and every block's int32 tile is scaled by dA[row]*dB[token] into
 //          the fp32 accumulators: no weight dequantization, half the activation bytes;
-//   AF_F8: the fp8 activation variant (BASELINE configs[4]): OCP e4m3 codes with a power-of-two
-//          scale per 32-element block (act_quant F8 form), widened to fp16 in registers by
-//          v_cvt_scalef32_pk_f16_fp8 (code * 2^e is exact in fp16) into the same fp16 MFMA.
-// AF_I8 and AF_F8 stage the same bytes: per token and sub-stage 64 code bytes, and the tile's
-// per-block fp32 scales (d, or 2^e) from a block-major [K/32][ldd] array.
+// AF_I8 stages per token and sub-stage 64 code bytes, and the tile's per-block fp32 d from a
+// block-major [K/32][ldd] array.  (The fp8 activation variant arrives as AF_F16: act_quant's
+// F8DEQ form widens its e4m3 codes to fp16 x~ once; widening them here per fragment -- round 2's
+// AF_F8 form -- cost 12-55% more than the q8_1 path and was removed.)
 //
 // Workgroup = 8 waves = BM = 128*RG weight rows x BN = 16*NB tokens.  Wave w owns rows
 // 16*(RG*w + rg) + [0,16) (rg < RG) and every token of the tile: each weight is dequantized
@@ -29,7 +28,7 @@
 // LDS-DMA (global_load_lds_dwordx4: no VGPRs, no ds_write):
 //   weights     : per row the stage's raw block bytes (WStage<F> below), 16-byte pieces at
 //                 whatever (2-byte) alignment the blocks have (gfx950 runs unaligned);
-//   activations : BN token rows x 128 B (AF_I8/AF_F8: x 64 B of codes + the tile's scales), 16-byte pieces
+//   activations : BN token rows x 128 B (AF_I8: x 64 B of codes + the tile's scales), 16-byte pieces
 //                 XOR-swizzled on the SOURCE side (the DMA destination is lane-linear) so the
 //                 MFMA fragment reads of a lane group hit distinct banks.
 // Two weight-stage slots and an activation ring of up to 4 slots (Cfg below) keep the next
@@ -167,7 +166,7 @@ struct Cfg {
     static constexpr bool Q6S = F == Q6_K && RG == 2;
     static constexpr int RBW = Q6S ? 224 : WStage<F>::RBW, NPW = RBW / 16, SPW = WStage<F>::SPW;
     static constexpr int W_REAL = BM * NPW / 64;                              // DMA instructions per stage
-    // code-form (AF_I8 / AF_F8) activation sub-stage: BN x 64 code bytes (CI instructions), then
+    // code-form (AF_I8) activation sub-stage: BN x 64 code bytes (CI instructions), then
     // one instruction for the tile's scales of the sub-stage's two blocks (2 x BN floats)
     static constexpr bool CODES = AM != AF_F16;
     static constexpr int CI = BN * 64 / 1024 > 0 ? BN * 64 / 1024 : 1;
@@ -336,7 +335,7 @@ constexpr uint32_t DUMMY = 0u;
 // 16 = no epilogue, 32 = activation DMAs with the addresses of a sub-stage-blocked layout,
 // 64 = weight DMAs with the addresses of a stage-contiguous (tiled) layout, 128 = a quarter of
 // the activation fragment reads.
-// AF_I8 / AF_F8: X = codes [N][K], XD = block-major scales [K/32][ldd]; AF_F16: X = fp16 x~.
+// AF_I8: X = codes [N][K], XD = block-major scales [K/32][ldd]; AF_F16: X = fp16 x~.
 template <int F, int NB, int RG, int ABL = 0, int AM = AF_F16, int NL = 0, int AQ = 0>
 __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *__restrict__ A, const void *__restrict__ X,
                                                    const float *__restrict__ XD, uint16_t *__restrict__ C,
@@ -679,15 +678,7 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
 #pragma unroll
                 for (int t = 0; t < NB; ++t) {
                     const int r = 16 * t + l16;
-                    if constexpr (AM == AF_F8) {
-                        // 8 e4m3 codes (stored in fragment order) and the block's 2^e scale
-                        const u32x2 c = *(const u32x2 *)(xs + 64 * r + 16 * ((2 * s + (g >> 1)) ^ i8_swz(r)) + 8 * (g & 1));
-                        const float sc = *(const float *)(xs + G::D_OFF + 4 * (G::BN * s + r));
-                        bfr[s][t] = frag4(__builtin_amdgcn_cvt_scalef32_pk_f16_fp8(c.x, sc, false),
-                                          __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(c.x, sc, true),
-                                          __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(c.y, sc, false),
-                                          __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(c.y, sc, true));
-                    } else if constexpr ((ABL & 128) != 0) { // diagnostic: a quarter of the fragment reads
+                    if constexpr ((ABL & 128) != 0) { // diagnostic: a quarter of the fragment reads
                         bfr[s][t] = t < NB / 4 || NB < 4 ? *(const f16x8 *)(xs + 128 * r + 16 * ((4 * s + g) ^ act_swz(r)))
                                                          : bfr[s][t % (NB / 4)];
                     } else {
@@ -1118,12 +1109,6 @@ hipError_t launch_fmt(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P,
             case 4: return launch_cfg<F, 4, 1, AF_I8>(A, x, C, P, pl, M, N, K, ldc, s);
             default: return launch_cfg<F, 8, 1, AF_I8>(A, x, C, P, pl, M, N, K, ldc, s);
             }
-    if (pl.act == AF_F8) switch (pl.nb) {
-        case 1: return launch_cfg<F, 1, 1, AF_F8>(A, x, C, P, pl, M, N, K, ldc, s);
-        case 2: return launch_cfg<F, 2, 1, AF_F8>(A, x, C, P, pl, M, N, K, ldc, s);
-        case 4: return launch_cfg<F, 4, 1, AF_F8>(A, x, C, P, pl, M, N, K, ldc, s);
-        default: return launch_cfg<F, 8, 1, AF_F8>(A, x, C, P, pl, M, N, K, ldc, s);
-        }
     if (pl.aq && pl.loaders == 4 && pl.rg == R1 && pl.act == AF_F16) switch (pl.nb) {
         case 1: return launch_cfg<F, 1, R1, AF_F16, 4, 1>(A, x, C, P, pl, M, N, K, ldc, s);
         case 2: return launch_cfg<F, 2, R1, AF_F16, 4, 1>(A, x, C, P, pl, M, N, K, ldc, s);

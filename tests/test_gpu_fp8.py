@@ -2,7 +2,8 @@
 reference has no fp8 code).  Checked against oracle/oracle.py's fp8 checker:
 
   * the device quantizer (gq_quantize_fp8) bit for bit: e4m3fn codes (in the (0,2,1,3) group
-    order the GEMM reads) and the power-of-two block scales;
+    order) and the power-of-two block scales; the MMQ path widens the same codes to fp16 x~
+    (act_quant F8DEQ: code * 2^e, exact) for the fp16-activation kernels;
   * the MMQ against mmq_fp8_ideal (fp32 dequantized weights x the same e4m3 activations,
     float64 sum): max|d| <= TIGHT_FP8 * max|C|, the fp16-MFMA bound of the q8_1 path (weights
     rounded to fp16 in registers);
@@ -48,8 +49,11 @@ def test_device_fp8_quantizer_bit_exact():
 
 @pytest.mark.parametrize("fmt", ("q8_0", "q4_k", "q6_k"))
 @pytest.mark.parametrize("M,N,K", [(96, 1, 256), (130, 5, 512), (200, 64, 1024), (257, 128, 2048), (64, 300, 768),
-                                   (300, 77, 4096)])
+                                   (300, 77, 4096), (520, 2, 4096), (129, 3, 768), (1000, 4, 2048), (333, 16, 1024),
+                                   (77, 800, 512)])
 def test_fp8_mmq(fmt, M, N, K):
+    """Every route of the fp8 variant's x~ (act_quant F8DEQ): the skinny kernel from one token
+    (Q4_K, Q8_0), the LDS-DMA and weight-register GEMMs, dequant + hipBLASLt (800 tokens)."""
     from kernels._lib import TYPES, mmq
     dev = _dev()
     qA = random_blocks(fmt, M, K, seed=M + N)
