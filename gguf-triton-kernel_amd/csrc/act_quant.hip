@@ -133,25 +133,27 @@ __global__ __launch_bounds__(256) void act_quant_kernel(const uint16_t *__restri
     act_quant_body<MODE>(X, ldx, rows, K, out, codes, dout, sout, xdeq, (int64_t)blockIdx.x);
 }
 
-// Several tensors' DEQ forms in one launch (gq_act_prepare_grouped): segment i owns workgroups
-// [wg0, wg0 + its blocks / 64), each running the one-tensor body -- bit-identical to its own launch.
+// Several tensors' DEQ (q8_1) or F8DEQ (fp8 variant) forms in one launch (gq_act_prepare_grouped):
+// segment i owns workgroups [wg0, wg0 + its blocks / 64), each running the one-tensor body --
+// bit-identical to its own launch.
 struct DeqSegs {
     int n;
     DeqSeg s[kMaxDeqSegs];
 };
 
+template <int MODE>
 __global__ __launch_bounds__(256) void act_quant_deq_grouped_kernel(const DeqSegs a)
 {
     const int64_t b = (int64_t)blockIdx.x;
     int i = 0;
     while (i + 1 < a.n && b >= a.s[i + 1].wg0) ++i;
     const DeqSeg &q = a.s[i];
-    act_quant_body<ACT_DEQ>(q.X, q.ldx, q.rows, q.K, nullptr, nullptr, nullptr, nullptr, q.xdeq, b - q.wg0);
+    act_quant_body<MODE>(q.X, q.ldx, q.rows, q.K, nullptr, nullptr, nullptr, nullptr, q.xdeq, b - q.wg0);
 }
 
-hipError_t launch_act_quant_deq_grouped(const DeqSeg *segs, int n, hipStream_t s)
+hipError_t launch_act_quant_deq_grouped(const DeqSeg *segs, int n, hipStream_t s, int mode)
 {
-    if (n < 1 || n > kMaxDeqSegs) return hipErrorInvalidValue;
+    if (n < 1 || n > kMaxDeqSegs || (mode != ACT_DEQ && mode != ACT_F8DEQ)) return hipErrorInvalidValue;
     DeqSegs a{};
     a.n = n;
     int64_t wg = 0;
@@ -161,7 +163,8 @@ hipError_t launch_act_quant_deq_grouped(const DeqSeg *segs, int n, hipStream_t s
         wg += (segs[i].rows * (segs[i].K / 32) + 63) / 64;
     }
     if (wg == 0) return hipSuccess;
-    act_quant_deq_grouped_kernel<<<dim3((unsigned)wg), dim3(256), 0, s>>>(a);
+    if (mode == ACT_F8DEQ) act_quant_deq_grouped_kernel<ACT_F8DEQ><<<dim3((unsigned)wg), dim3(256), 0, s>>>(a);
+    else act_quant_deq_grouped_kernel<ACT_DEQ><<<dim3((unsigned)wg), dim3(256), 0, s>>>(a);
     return hipGetLastError();
 }
 

@@ -67,7 +67,7 @@ struct DeqSeg {
     uint16_t *xdeq;
     int64_t wg0;
 };
-hipError_t launch_act_quant_deq_grouped(const DeqSeg *segs, int n, hipStream_t s);
+hipError_t launch_act_quant_deq_grouped(const DeqSeg *segs, int n, hipStream_t s, int mode = ACT_DEQ); // or ACT_F8DEQ
 
 // Decode-shaped GEMV (mmq_gemv.hip): C[t][m] for t < N_tok <= 8 from SOA activations.
 hipError_t launch_gemv(int fmt, const uint8_t *A, const int8_t *xq, const float *xd, const float *xs, uint16_t *C,

@@ -665,7 +665,7 @@ int gq_act_prepare_grouped(gq_act act, const gq_prep_item *items, int n, void *s
     int ns = 0;
     auto flush = [&]() -> int {
         if (ns == 0) return GQ_OK;
-        const hipError_t e = gq::launch_act_quant_deq_grouped(segs, ns, s);
+        const hipError_t e = gq::launch_act_quant_deq_grouped(segs, ns, s, act == GQ_ACT_FP8_E4M3 ? gq::ACT_F8DEQ : gq::ACT_DEQ);
         ns = 0;
         if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (grouped act_quant): %s", hipGetErrorString(e));
         return GQ_OK;
@@ -675,7 +675,7 @@ int gq_act_prepare_grouped(gq_act act, const gq_prep_item *items, int n, void *s
         const int64_t N = it.N, K = it.K;
         if (N == 0 || K == 0) continue;
         int rc;
-        if (act != GQ_ACT_Q8_1 || use_gemv(N, K) || use_i8(GQ_Q8_0, N, K)) { // its own launch(es), as gq_act_prepare_ex
+        if (act == GQ_ACT_Q8_1 && (use_gemv(N, K) || use_i8(GQ_Q8_0, N, K))) { // its own launch(es), as gq_act_prepare_ex
             if ((rc = prepare(act, it.B, N, K, it.ldb, it.workspace, it.workspace_bytes, s,
                               use_i8(GQ_Q8_0, N, K) ? 3 : 1)) != GQ_OK)
                 return rc;

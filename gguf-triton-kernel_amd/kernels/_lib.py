@@ -282,7 +282,8 @@ def act_prepare(B: torch.Tensor, N: int, K: int, workspace: torch.Tensor, act: s
 def act_prepare_grouped(items, act: str = "q8_1"):
     """Several act_prepare calls in as few launches as possible (gq_act_prepare_grouped):
     items = [(B, N, K, workspace), ...] -- each workspace gets exactly what act_prepare would
-    write; one launch per 8 items whose form is the GEMM paths' fp16 x~ (q8_1, N >= 5)."""
+    write; one launch per 8 items whose form is the GEMM paths' fp16 x~ (q8_1 at N >= 5; the fp8
+    variant's widened codes at every N)."""
     if not items:
         return
     dev = items[0][0].device

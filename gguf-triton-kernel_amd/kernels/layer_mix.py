@@ -126,9 +126,10 @@ class LayerMix:
             if outs is not None:
                 res.update(zip(keys, outs))
                 done = True
-        if not done and self.act == "q8_1" and all(inp.shape[0] == x.shape[0] for inp in inputs) and x.shape[0] > 4:
+        if not done and all(inp.shape[0] == x.shape[0] for inp in inputs) and (x.shape[0] > 4 or self.act == "fp8"):
             # every input group's activations quantized in ONE launch (gq_act_prepare_grouped),
             # then every call prepared -- bit-identical to each call quantizing its own input
+            # (fp8: at every token count -- it has no decode kernel)
             N = x.shape[0]
             preps, wss = [], []
             for calls, inp in zip(self.calls, inputs):

@@ -103,8 +103,9 @@ int gq_mmq_prepared_ex(gq_type t, gq_act act, const void *A, void *workspace, si
  * transformer block's projections (no reference counterpart: the reference quantizes inside
  * every matmul).  Item i prepares B_i (N_i x K_i fp16, row stride ldb_i) into its own
  * workspace exactly as gq_act_prepare_ex(act, B_i, ...) would -- the same bytes, the same
- * errors.  Items whose prepared form is the fp16 x~ of the GEMM paths (GQ_ACT_Q8_1, N >= 5)
- * share one launch per 8 items; the others are prepared one by one.  Every item is checked
+ * errors.  Items whose prepared form is the fp16 x~ of the GEMM paths (GQ_ACT_Q8_1 at N >= 5;
+ * GQ_ACT_FP8_E4M3's widened codes at every N) share one launch per 8 items; the others are
+ * prepared one by one.  Every item is checked
  * before anything is launched: a bad item (GQ_EINVAL / GQ_EUNSUPPORTED) launches nothing.
  * No host sync.
  */

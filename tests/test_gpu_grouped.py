@@ -148,32 +148,36 @@ def test_layer_mix_grouped_matches_ungrouped(N):
         assert torch.equal(rg[n].view(torch.int16), ru[n].view(torch.int16)), n
 
 
-def test_act_prepare_grouped_matches_individual():
+@pytest.mark.parametrize("act", ["q8_1", "fp8"])
+def test_act_prepare_grouped_matches_individual(act):
     """gq_act_prepare_grouped writes exactly the bytes gq_act_prepare writes per item: GEMM-form
     items (N >= 5, several per launch, more than one launch's 8), a strided activation view, a
-    decode-form item (N <= 4, prepared on its own), an empty item."""
+    decode-form item (N <= 4, prepared on its own; fp8: grouped like the rest), an empty item."""
     import kernels._lib as kl
     dev = _dev()
     specs = [(8, 4096), (8, 11008), (3, 2048), (64, 1024), (0, 512), (16, 4096), (5, 2816), (128, 4096),
-             (7, 32), (9, 256), (12, 4096), (6, 11008)]
+             (7, 32), (9, 256), (12, 4096), (6, 11008), (1, 4096), (2, 768)]
+    if act == "fp8":  # (K % 256 == 0)
+        specs = [(N, K) for N, K in specs if K % 256 == 0]
     wide = torch.from_numpy(random_activations(8, 4096 + 512, seed=77)).to(dev)
     items, ref = [], []
     for i, (N, K) in enumerate(specs):
         B = wide[:, 256:256 + K] if i == 0 else torch.from_numpy(random_activations(N, K, seed=i)).to(dev)
-        need = kl.workspace_size(kl.GQ_Q4_K, 256, N, K) if N else 16
+        need = kl.workspace_size(kl.GQ_Q4_K, 256, N, K, act) if N else 16
         ws, ws_ref = (torch.zeros(need, dtype=torch.uint8, device=dev) for _ in range(2))
         items.append((B, N, K, ws))
         if N:
-            kl.act_prepare(B, N, K, ws_ref)
+            kl.act_prepare(B, N, K, ws_ref, act=act)
         ref.append(ws_ref)
-    kl.act_prepare_grouped(items)
+    kl.act_prepare_grouped(items, act=act)
     torch.cuda.synchronize()
     for (B, N, K, ws), ws_ref in zip(items, ref):
         assert torch.equal(ws, ws_ref), (N, K)
 
 
-@pytest.mark.parametrize("N", [5, 8, 16, 64, 128])
-def test_layer_mix_prepared_matches_per_call(N):
+@pytest.mark.parametrize("N,act", [(5, "q8_1"), (8, "q8_1"), (16, "q8_1"), (64, "q8_1"), (128, "q8_1"),
+                                   (1, "fp8"), (3, "fp8"), (8, "fp8"), (128, "fp8")])
+def test_layer_mix_prepared_matches_per_call(N, act):
     """LayerMix from 5 tokens (the four inputs quantized in one gq_act_prepare_grouped launch, every
     projection prepared): unfused, every projection bit-identical to its own mmq(); fused (q+k and
     gate+up as one taller matrix, whose split-K plan may differ from the parts') within the GEMM
@@ -189,12 +193,12 @@ def test_layer_mix_prepared_matches_per_call(N):
     a = torch.from_numpy(random_activations(N, 4096, seed=16)).to(dev)
     y = torch.from_numpy(random_activations(N, 4096, seed=17)).to(dev)
     h = torch.from_numpy(random_activations(N, 11008, seed=18)).to(dev)
-    res = LayerMix(lins, fuse=False).forward(x, h, attn=a, x_ffn=y)
-    fused = LayerMix(lins).forward(x, h, attn=a, x_ffn=y)
+    res = LayerMix(lins, act=act, fuse=False).forward(x, h, attn=a, x_ffn=y)
+    fused = LayerMix(lins, act=act).forward(x, h, attn=a, x_ffn=y)
     inp = {"attn_q": x, "attn_k": x, "attn_v": x, "attn_output": a, "ffn_gate": y, "ffn_up": y, "ffn_down": h}
     torch.cuda.synchronize()
     for n, (M, K) in LLAMA_LAYER_SHAPES.items():
-        solo = kl.mmq(kl.TYPES[types[n]], A[n], inp[n], M, N, K)
+        solo = kl.mmq(kl.TYPES[types[n]], A[n], inp[n], M, N, K, act=act)
         torch.cuda.synchronize()
         assert torch.equal(res[n].view(torch.int16), solo.view(torch.int16)), n
         assert O.max_rel_err(fused[n].cpu().numpy(), solo.cpu().numpy()) <= 4e-3, n
