@@ -48,44 +48,14 @@ __device__ __forceinline__ void act_quant_body(const uint16_t *__restrict__ X, i
     u32x4 v = {0, 0, 0, 0};
     if (live) v = ld16(X + row * ldx + 32 * j + 8 * sub);
     if constexpr (MODE == ACT_F8 || MODE == ACT_F8DEQ) {
-        const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
-        float x[8], amax = 0.f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            x[2 * i] = h2f(wd[i] & 0xffff);
-            x[2 * i + 1] = h2f(wd[i] >> 16);
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(x[i]));
-        amax = fmaxf(amax, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax), 0xb1, 0xf, 0xf, false)));
-        amax = fmaxf(amax, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax), 0x4e, 0xf, 0xf, false)));
+        const F8Quad f = f8_quad(v); // (every lane: DPP quad groups)
         if (!live) return;
-        // amax = m * 2^E, m in [0.5, 1): amax <= 448 * 2^e  <=>  e >= E - 9 + (m > 0.875)
-        const uint32_t ab = __builtin_bit_cast(uint32_t, amax);
-        const int E = (int)((ab >> 23) & 0xff) - 126;
-        const int e = amax == 0.f ? 0 : E - 9 + ((ab & 0x7fffffu) > 0x600000u ? 1 : 0);
-        const float inv = __builtin_bit_cast(float, (uint32_t)(127 - e) << 23); // 2^-e, exact
-        uint32_t o[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) { // elements 4h..4h+3 -> bytes (0,2,1,3)
-            int w = __builtin_amdgcn_cvt_pk_fp8_f32(x[4 * h] * inv, x[4 * h + 2] * inv, 0, false);
-            w = __builtin_amdgcn_cvt_pk_fp8_f32(x[4 * h + 1] * inv, x[4 * h + 3] * inv, w, true);
-            o[h] = (uint32_t)w;
-        }
-        if constexpr (MODE == ACT_F8DEQ) { // pairs (0,2), (1,3) of each 4-group, as the DEQ form
-            const float X = __builtin_bit_cast(float, (uint32_t)(127 + e) << 23);
-            typedef _Float16 h2t __attribute__((ext_vector_type(2)));
-            uint32_t d[4];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                d[2 * h] = __builtin_bit_cast(uint32_t, (h2t)__builtin_amdgcn_cvt_scalef32_pk_f16_fp8(o[h], X, false));
-                d[2 * h + 1] = __builtin_bit_cast(uint32_t, (h2t)__builtin_amdgcn_cvt_scalef32_pk_f16_fp8(o[h], X, true));
-            }
-            *(u32x4 *)(xdeq + row * K + 32 * j + 8 * sub) = (u32x4){d[0], d[1], d[2], d[3]};
+        if constexpr (MODE == ACT_F8DEQ) {
+            *(u32x4 *)(xdeq + row * K + 32 * j + 8 * sub) = (u32x4){f.xt[0], f.xt[1], f.xt[2], f.xt[3]};
             return;
         }
-        *(u32x2 *)(codes + row * K + 32 * j + 8 * sub) = (u32x2){o[0], o[1]};
-        if (sub == 0) dout[j * ((rows + 3) & ~(int64_t)3) + row] = __builtin_bit_cast(float, (uint32_t)(127 + e) << 23);
+        *(u32x2 *)(codes + row * K + 32 * j + 8 * sub) = (u32x2){f.codes[0], f.codes[1]};
+        if (sub == 0) dout[j * ((rows + 3) & ~(int64_t)3) + row] = __builtin_bit_cast(float, (uint32_t)(127 + f.e) << 23);
         return;
     }
     const Q81Quad q = q8_1_quad(v);

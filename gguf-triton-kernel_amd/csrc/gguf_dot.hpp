@@ -107,6 +107,90 @@ __device__ __forceinline__ void dot_unit(const UnitRaw<F> &r, const Act<F, NT> &
     }
 }
 
+// ---- the fp8 variant's decode (mmq_decode.hip, FP8 = 1) ----
+// The unit's activations as fp16 x~ = e4m3 code * 2^e (gguf_q8_1.hpp f8_quad): 64 values as 32
+// pair words in the DEQ order (word 2k = (x4k, x4k+2), 2k+1 = (x4k+1, x4k+3); Q6_K: run A then
+// run B), and the fp32 sums of x~ over the unit's four 16-element quarters.  The weights' codes
+// enter v_dot2_f32_f16 as fp16 pairs 1024 + byte (one v_perm / v_and_or per pair, no bias
+// subtraction): sum (1024 + c) x = sum c x + 1024 sum x, taken out with the quarter sums.
+template <int NT> struct ActH {
+    uint32_t x[NT][32];
+    float s[NT][4];
+};
+
+typedef _Float16 hh2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float fdot2u(uint32_t a, uint32_t b, float c)
+{
+    return __builtin_amdgcn_fdot2(__builtin_bit_cast(hh2, a), __builtin_bit_cast(hh2, b), c, false);
+}
+// fp16 pairs 1024 + byte of bytes (0,2) / (1,3) of a word; 1024 + nibble of bytes (0,2)
+__device__ __forceinline__ uint32_t b02(uint32_t c) { return __builtin_amdgcn_perm(0x64646464u, c, 0x04020400u); }
+__device__ __forceinline__ uint32_t b13(uint32_t c) { return __builtin_amdgcn_perm(0x64646464u, c, 0x04030401u); }
+__device__ __forceinline__ uint32_t n02(uint32_t v) { return (v & 0x000f000fu) | 0x64006400u; }
+
+template <int F, int NT>
+__device__ __forceinline__ void dot_unit_h(const UnitRaw<F> &r, const ActH<NT> &a, float (&acc)[NT])
+{
+    if constexpr (F == Q8_0) { // codes + 128 (xor 0x80): pairs 1152 + q
+        uint32_t p[32];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t c = r.w[i] ^ 0x80808080u;
+            p[2 * i] = b02(c);
+            p[2 * i + 1] = b13(c);
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                s0 = fdot2u(p[i], a.x[t][i], s0);
+                s1 = fdot2u(p[16 + i], a.x[t][16 + i], s1);
+            }
+            acc[t] += r.d0 * (s0 - 1152.f * (a.s[t][0] + a.s[t][1])) + r.d1 * (s1 - 1152.f * (a.s[t][2] + a.s[t][3]));
+        }
+    } else if constexpr (F == Q4_K) { // low nibbles: sub-block A, high: B
+        uint32_t p[32];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            p[2 * i] = n02(r.w[i]);
+            p[2 * i + 1] = n02(r.w[i] >> 8);
+            p[16 + 2 * i] = n02(r.w[i] >> 4);
+            p[16 + 2 * i + 1] = n02(r.w[i] >> 12);
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                s0 = fdot2u(p[i], a.x[t][i], s0);
+                s1 = fdot2u(p[16 + i], a.x[t][16 + i], s1);
+            }
+            const float xa = a.s[t][0] + a.s[t][1], xb = a.s[t][2] + a.s[t][3];
+            acc[t] += r.ds0 * (s0 - 1024.f * xa) - r.dm0 * xa + r.ds1 * (s1 - 1024.f * xb) - r.dm1 * xb;
+        }
+    } else { // Q6_K: codes 0..63, weight (q - 32) * d * sc per 16 elements
+        uint32_t p[32];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            p[2 * i] = b02(r.ca[i]);
+            p[2 * i + 1] = b13(r.ca[i]);
+            p[16 + 2 * i] = b02(r.cb[i]);
+            p[16 + 2 * i + 1] = b13(r.cb[i]);
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            float q[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) q[k] = fdot2u(p[8 * k + i], a.x[t][8 * k + i], q[k]);
+            acc[t] += r.fa1 * (q[0] - 1056.f * a.s[t][0]) + r.fa2 * (q[1] - 1056.f * a.s[t][1]) +
+                      r.fb1 * (q[2] - 1056.f * a.s[t][2]) + r.fb2 * (q[3] - 1056.f * a.s[t][3]);
+        }
+    }
+}
+
 template <int F, int NT>
 __device__ __forceinline__ void unit_dot(const uint8_t *__restrict__ rowp, int u, int64_t nb, const Act<F, NT> &a,
                                          float (&acc)[NT])

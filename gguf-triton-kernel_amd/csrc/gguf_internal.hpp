@@ -75,10 +75,11 @@ hipError_t launch_gemv(int fmt, const uint8_t *A, const int8_t *xq, const float 
 
 // Streaming decode (mmq_decode.hip): q8_1 quantization of the N <= 8 tokens in LDS + the
 // weight stream, one launch.  decode_fused_ok() says whether the LDS image fits (else:
-// act_quant + launch_gemv).
-bool decode_fused_ok(int fmt, int64_t N, int64_t K);
+// act_quant + launch_gemv).  fp8: the fp8 activation variant's form (e4m3-quantized x~ in LDS,
+// fp16 dot products).
+bool decode_fused_ok(int fmt, int64_t N, int64_t K, bool fp8 = false);
 hipError_t launch_decode_fused(int fmt, const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, int64_t M,
-                               int64_t N, int64_t K, int64_t ldc, hipStream_t s);
+                               int64_t N, int64_t K, int64_t ldc, hipStream_t s, bool fp8 = false);
 
 // Batched GEMM on fp16 MFMA (mmq_gemm.hip): C[t][m] from the dequantized activation x~.
 struct GemmPlan {
@@ -141,8 +142,8 @@ struct DecodeItem {
     int64_t ldc;
     int64_t M, K;
 };
-bool decode_grouped_ok(const DecodeItem *items, int n, int64_t N);
-hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipStream_t s);
+bool decode_grouped_ok(const DecodeItem *items, int n, int64_t N, bool fp8 = false);
+hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipStream_t s, bool fp8 = false);
 
 // Skinny-token MMQ (mmq_skinny.hip, 1..32 tokens, K % 256 == 0): 16*rg rows x 16*nb tokens per
 // workgroup, K split over its 8 waves (8/nb ranges x nb token tiles), weights and activations

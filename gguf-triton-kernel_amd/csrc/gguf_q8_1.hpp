@@ -140,4 +140,47 @@ __device__ __forceinline__ Q81Quad q8_1_quad(u32x4 w)
     return r;
 }
 
+// The fp8 variant's block quantization (act_quant.hip F8 / F8DEQ; include/gguf_mmq.h states the
+// rule) by an aligned group of 4 lanes, 8 elements each: X = 2^e with e the smallest integer
+// such that max|x| <= 448 * 2^e (X = 1 for an all-zero block), codes = e4m3(x / X) RNE, stored
+// per 4-group in the order (0,2,1,3); x~ = code * X, exact in fp16, as fp16 pairs (0,2), (1,3)
+// of each 4-group -- the DEQ layout.
+struct F8Quad {
+    uint32_t codes[2]; // e4m3 bytes, 4-groups (0,2,1,3)
+    uint32_t xt[4];    // x~ pairs: (x0,x2), (x1,x3), (x4,x6), (x5,x7)
+    int e;
+};
+
+__device__ __forceinline__ F8Quad f8_quad(u32x4 w)
+{
+    const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
+    float x[8], amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        x[2 * i] = h2f(wd[i] & 0xffff);
+        x[2 * i + 1] = h2f(wd[i] >> 16);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(x[i]));
+    amax = fmaxf(amax, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax), 0xb1, 0xf, 0xf, false)));
+    amax = fmaxf(amax, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax), 0x4e, 0xf, 0xf, false)));
+    // amax = m * 2^E, m in [0.5, 1): amax <= 448 * 2^e  <=>  e >= E - 9 + (m > 0.875)
+    const uint32_t ab = __builtin_bit_cast(uint32_t, amax);
+    const int E = (int)((ab >> 23) & 0xff) - 126;
+    F8Quad r;
+    r.e = amax == 0.f ? 0 : E - 9 + ((ab & 0x7fffffu) > 0x600000u ? 1 : 0);
+    const float inv = __builtin_bit_cast(float, (uint32_t)(127 - r.e) << 23); // 2^-e, exact
+    const float X = __builtin_bit_cast(float, (uint32_t)(127 + r.e) << 23);
+    typedef _Float16 h2t __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int h = 0; h < 2; ++h) { // elements 4h..4h+3 -> bytes (0,2,1,3)
+        int c = __builtin_amdgcn_cvt_pk_fp8_f32(x[4 * h] * inv, x[4 * h + 2] * inv, 0, false);
+        c = __builtin_amdgcn_cvt_pk_fp8_f32(x[4 * h + 1] * inv, x[4 * h + 3] * inv, c, true);
+        r.codes[h] = (uint32_t)c;
+        r.xt[2 * h] = __builtin_bit_cast(uint32_t, (h2t)__builtin_amdgcn_cvt_scalef32_pk_f16_fp8(c, X, false));
+        r.xt[2 * h + 1] = __builtin_bit_cast(uint32_t, (h2t)__builtin_amdgcn_cvt_scalef32_pk_f16_fp8(c, X, true));
+    }
+    return r;
+}
+
 } // namespace gq

@@ -325,6 +325,10 @@ size_t ws_bytes(int t, int act, int64_t M, int64_t N, int64_t K)
 // gq_mmq_ex takes the one-launch fused decode (no workspace) for this call
 bool fused_decode_route(int t, int act, int64_t N, int64_t K)
 {
+    // the fp8 variant's own decode form (mmq_decode.hip FP8: fp16 dot products, 3-4x the int8
+    // form's VALU) at 1-2 tokens; at 3-4 the skinny kernel / GEMM is faster (7B layer x4 83 vs
+    // 73 us; profiles/r03/s3/fp8_decode.log)
+    if (act == GQ_ACT_FP8_E4M3) return N <= 2 && gq::decode_fused_ok(t, N, K, true) && gq::tuning().fused_decode;
     return route(t, act, N, K).gemv && gq::decode_fused_ok(t, N, K) && gq::tuning().fused_decode;
 }
 // what a gq_mmq_ex call itself needs (gq_act_prepare / gq_mmq_prepared need ws_bytes)
@@ -586,7 +590,7 @@ int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int6
     if (fused_decode_route(t, act, N, K)) {
         // one launch: activation quantization in LDS + decode GEMV
         hipError_t e = gq::launch_decode_fused(t, (const uint8_t *)A, (const uint16_t *)B, ldb, (uint16_t *)C, M, N,
-                                               K, ldc, (hipStream_t)stream);
+                                               K, ldc, (hipStream_t)stream, act == GQ_ACT_FP8_E4M3);
         if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (decode): %s", hipGetErrorString(e));
         return GQ_OK;
     }
@@ -780,15 +784,22 @@ size_t gq_mmq_sharded_workspace_size(gq_type t, int64_t M, int64_t N, int64_t K,
 
 int gq_mmq_grouped(const gq_group_item *items, int n, int64_t N, void *stream)
 {
+    return gq_mmq_grouped_ex(GQ_ACT_Q8_1, items, n, N, stream);
+}
+
+int gq_mmq_grouped_ex(gq_act act, const gq_group_item *items, int n, int64_t N, void *stream)
+{
     g_err.clear();
+    const bool fp8 = act == GQ_ACT_FP8_E4M3;
     if (n < 0 || (n > 0 && !items)) return fail(GQ_EINVAL, "bad item list (n=%d, items=%p)", n, (const void *)items);
     if (N < 0) return fail(GQ_EINVAL, "negative N");
     gq::DecodeItem di[16];
     int m = 0;
     for (int i = 0; i < n; ++i) {
         const gq_group_item &it = items[i];
-        const int rc = check_common(it.type, it.M, N, it.K);
+        int rc = check_common(it.type, it.M, N, it.K);
         if (rc != GQ_OK) return rc;
+        if ((rc = check_act(act, it.K)) != GQ_OK) return rc;
         if (it.M == 0 || N == 0) continue;
         if (it.K == 0) return fail(GQ_EINVAL, "item %d: K must be positive", i);
         if (!it.A || !it.B || !it.C) return fail(GQ_EINVAL, "item %d: null pointer", i);
@@ -799,10 +810,10 @@ int gq_mmq_grouped(const gq_group_item *items, int n, int64_t N, void *stream)
                                  it.ldc, it.M, it.K};
     }
     if (m == 0) return GQ_OK;
-    if (!gq::decode_grouped_ok(di, m, N))
-        return fail(GQ_EUNSUPPORTED, "not a grouped-decode shape (N=%lld; N <= 4 and every item a one-launch decode)",
-                    (long long)N);
-    hipError_t e = gq::launch_decode_grouped(di, m, N, (hipStream_t)stream);
+    if (!gq::decode_grouped_ok(di, m, N, fp8))
+        return fail(GQ_EUNSUPPORTED, "not a grouped-decode shape (N=%lld; N <= %d and every item a one-launch decode)",
+                    (long long)N, fp8 ? 2 : 4);
+    hipError_t e = gq::launch_decode_grouped(di, m, N, (hipStream_t)stream, fp8);
     if (e == hipErrorInvalidValue) return fail(GQ_EUNSUPPORTED, "grouped decode: more than 16 parts");
     if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (grouped decode): %s", hipGetErrorString(e));
     return GQ_OK;

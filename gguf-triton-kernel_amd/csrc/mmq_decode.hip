@@ -171,7 +171,11 @@ __device__ __forceinline__ void act_from_lds(Act<F, NT> &a, const uint8_t *codes
 // (stream_decode_kernel: the grid itself; stream_decode_grouped_kernel: a slice of a grid shared
 // by several matrices).  A row's arithmetic depends on F, NT and K only -- not on bx, gx or the
 // geometry's rows per task -- so a matrix computed inside a group gives the same bits as alone.
-template <int F, int NT, int ITC, int IM = 0>
+// FP8 = 1: the fp8 activation variant -- the prologue quantizes x per 32-block to e4m3 codes
+// and widens them back (gguf_q8_1.hpp f8_quad: the bytes act_quant's F8DEQ form writes), the
+// LDS image is fp16 x~ + the x~ sums of every 16-element quarter, and the units multiply by
+// v_dot2_f32_f16 (gguf_dot.hpp dot_unit_h); no register cache of activations (ITC = 0).
+template <int F, int NT, int ITC, int IM = 0, int FP8 = 0>
 __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X, int64_t ldx,
                                             uint16_t *__restrict__ C, int M, int64_t N, int K, int64_t ldc,
                                             DecodeGeom geo, int bx, int gx, int by, uint8_t *smem)
@@ -192,8 +196,12 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
     const int cpr = upr / UPC; // lane chunks per row
     uint8_t *ring = smem + wave * (NS * SLOT);
     uint8_t *codes = smem + RING;
-    float *sd = (float *)(codes + NT * kp);
+    float *sd = (float *)(codes + NT * kp * (FP8 ? 2 : 1)); // FP8: quarter sums [NT][2*nb]
     float *sx = sd + NT * nb; // Q4_K: s [NT][nb] (float); Q6_K: code sums [NT][2*nb] (int)
+    static_assert(!FP8 || ITC == 0, "fp8 decode: activations read from LDS per unit");
+    // FP8: x~ 16-byte piece P of a token row at piece P ^ ((P >> 4) & 7) (the lanes of a unit
+    // read hit distinct banks)
+    auto xpiece = [](int P) { return P ^ ((P >> 4) & 7); };
 
     const __amdgpu_buffer_rsrc_t wrs =
         __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, (int)(((uint32_t)M * RB + 15u) & ~15u), 0x00020000);
@@ -309,14 +317,30 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
             if constexpr (F == Q4_K) sx[t * nb + j] = h2f(qq.sbits);
         }
     };
+    auto store_f = [&](int b, const F8Quad &f, float ls) { // FP8: x~ and the lane pair's quarter sum
+        int t, j;
+        tok_split(b, t, j);
+        const int P = 4 * j + (lane & 3); // 16-byte piece of the token row
+        *(u32x4 *)(codes + 2 * t * kp + 16 * xpiece(P)) = (u32x4){f.xt[0], f.xt[1], f.xt[2], f.xt[3]};
+        if ((lane & 1) == 0) sd[t * 2 * nb + 2 * j + ((lane >> 1) & 1)] = ls;
+    };
     auto quantize = [&](int r, const u32x4 (&xv)[XP]) {
         const int np = npass(r);
 #pragma unroll
         for (int q = 0; q < XP; ++q) {
             if (q < np) { // every lane of the wave computes (DPP groups); stores only real blocks
-                const Q81Quad qq = q8_1_quad(xv[q]);
                 const int b = xblock(r, q);
-                if (b < xblocks) store_q(b, qq);
+                if constexpr (FP8) {
+                    const F8Quad f = f8_quad(xv[q]);
+                    float ls = 0.f; // the lane's 8 x~ in fp32, then + the pair lane's (a quarter)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) ls += h2f(f.xt[i] & 0xffffu) + h2f(f.xt[i] >> 16);
+                    ls += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, ls), 0xb1, 0xf, 0xf, false));
+                    if (b < xblocks) store_f(b, f, ls);
+                } else {
+                    const Q81Quad qq = q8_1_quad(xv[q]);
+                    if (b < xblocks) store_q(b, qq);
+                }
             }
         }
         // consume every activation register on every path: a load the compiler sees as possibly
@@ -376,9 +400,44 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = 0.f;
 
+    // FP8: the unit's x~ (two 32-element runs: Q6_K A and B, else elements 64u..64u+63) and quarter sums
+    auto act_h = [&](ActH<NT> &a, int u) {
+        int e0, e1;
+        if constexpr (F == Q6_K) {
+            e0 = 256 * (u >> 2) + 128 * ((u >> 1) & 1) + 32 * (u & 1);
+            e1 = e0 + 64;
+        } else {
+            e0 = 64 * u;
+            e1 = e0 + 32;
+        }
+        const bool has1 = F != Q8_0 || 2 * u + 1 < nb; // (Q8_0, K % 64 == 32: no second block)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+#pragma unroll
+            for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    u32x4 v = *(const u32x4 *)(codes + 2 * t * kp + 16 * xpiece(((rr ? e1 : e0) >> 3) + i));
+                    if (rr && !has1) v = (u32x4){0, 0, 0, 0};
+                    a.x[t][16 * rr + 4 * i] = v.x;
+                    a.x[t][16 * rr + 4 * i + 1] = v.y;
+                    a.x[t][16 * rr + 4 * i + 2] = v.z;
+                    a.x[t][16 * rr + 4 * i + 3] = v.w;
+                }
+            const float *sq = sd + t * 2 * nb;
+            a.s[t][0] = sq[e0 >> 4];
+            a.s[t][1] = sq[(e0 >> 4) + 1];
+            a.s[t][2] = has1 ? sq[e1 >> 4] : 0.f;
+            a.s[t][3] = has1 ? sq[(e1 >> 4) + 1] : 0.f;
+        }
+    };
     // the contribution of unit u (activation slot i when cached) of the row at rowp
     auto unit = [&](const UnitLoad<F> &l, int u, int i, float (&acc)[NT]) {
-        if constexpr (ITC > 0) {
+        if constexpr (FP8) {
+            ActH<NT> a;
+            act_h(a, u);
+            dot_unit_h<F, NT>(UnitRaw<F>::from(l, u, nb), a, acc);
+        } else if constexpr (ITC > 0) {
             dot_unit<F, NT>(UnitRaw<F>::from(l, u, nb), ca[i], acc);
         } else {
             Act<F, NT> a;
@@ -555,28 +614,30 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
 #endif
 }
 
-template <int F, int NT, int ITC, int IM>
+template <int F, int NT, int ITC, int IM, int FP8>
 __global__ __launch_bounds__(DW * 64) void stream_decode_kernel(const uint8_t *__restrict__ A,
                                                                 const uint16_t *__restrict__ X, int64_t ldx,
                                                                 uint16_t *__restrict__ C, int M, int64_t N, int K,
                                                                 int64_t ldc, DecodeGeom geo)
 {
     extern __shared__ __attribute__((aligned(1024))) uint8_t smem[];
-    decode_body<F, NT, ITC, IM>(A, X, ldx, C, M, N, K, ldc, geo, (int)blockIdx.x, (int)gridDim.x, (int)blockIdx.y, smem);
+    decode_body<F, NT, ITC, IM, FP8>(A, X, ldx, C, M, N, K, ldc, geo, (int)blockIdx.x, (int)gridDim.x, (int)blockIdx.y, smem);
 }
 
 struct Pick {
     int nt, itc;
     bool img = false;       // Q6_K: the aligned ring image (kImgSB)
+    bool fp8 = false;       // the fp8 activation variant (decode_body FP8; set before pick())
     bool lds_split = false; // fewer tokens per workgroup than wanted: the activations do not fit LDS
     size_t lds;
     DecodeGeom geo;
     int grid;
 };
 
-size_t act_lds(int fmt, int nt, int64_t K)
+size_t act_lds(int fmt, int nt, int64_t K, bool fp8 = false)
 {
     const int64_t kp = (K + 63) / 64 * 64, nb = K / 32;
+    if (fp8) return (size_t)nt * kp * 2 + (size_t)nt * nb * 2 * 4; // x~ + quarter sums
     return (size_t)nt * kp + (size_t)nt * nb * 4 * (fmt == Q8_0 ? 1 : (fmt == Q4_K ? 2 : 3));
 }
 
@@ -603,12 +664,12 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p, int wgs = 0)
     int nt_cap = fmt == Q6_K && K >= 8192 ? 2 : 4;
     if (tuning().decode_maxnt > 0) nt_cap = tuning().decode_maxnt; // tuning override
     while (p.nt > 1 && p.nt > nt_cap) p.nt >>= 1;
-    while ((size_t)RING + act_lds(fmt, p.nt, K) > (size_t)LDS_CAP) {
+    while ((size_t)RING + act_lds(fmt, p.nt, K, p.fp8) > (size_t)LDS_CAP) {
         if (p.nt == 1) return false;
         p.nt >>= 1;
         p.lds_split = true;
     }
-    p.lds = (size_t)RING + act_lds(fmt, p.nt, K);
+    p.lds = (size_t)RING + act_lds(fmt, p.nt, K, p.fp8);
     // ring bytes per row and per task (the 16-byte aligned window of a packed task may start up
     // to 14 bytes before it; the Q6_K image starts at the slot)
     const bool img = p.img = img_of(fmt, K, p.nt);
@@ -651,24 +712,25 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p, int wgs = 0)
     // profiles/r02/decode_nt4_cache_ab.txt; GQ_DECODE_NT4_CACHE=0: off)
     if (p.nt == 4 && units == 1 && tuning().decode_nt4_cache)
         p.itc = 1;
+    if (p.fp8) p.itc = 0;
     const int64_t waves = g.ngroups < W ? g.ngroups : W;
     p.grid = (int)((waves + DW - 1) / DW);
     return true;
 }
 
-template <int F, int NT, int ITC, int IM = 0>
+template <int F, int NT, int ITC, int IM = 0, int FP8 = 0>
 hipError_t launch_t(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, int64_t M, int64_t N, int64_t K,
                     int64_t ldc, const Pick &p, hipStream_t s)
 {
     static bool attr = false; // raise the dynamic LDS limit once per instantiation
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void *)stream_decode_kernel<F, NT, ITC, IM>,
+        hipError_t e = hipFuncSetAttribute((const void *)stream_decode_kernel<F, NT, ITC, IM, FP8>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, LDS_CAP);
         if (e != hipSuccess) return e;
         attr = true;
     }
     dim3 grid((unsigned)p.grid, (unsigned)((N + NT - 1) / NT)), block(DW * 64);
-    stream_decode_kernel<F, NT, ITC, IM><<<grid, block, p.lds, s>>>(A, X, ldx, C, (int)M, N, (int)K, ldc, p.geo);
+    stream_decode_kernel<F, NT, ITC, IM, FP8><<<grid, block, p.lds, s>>>(A, X, ldx, C, (int)M, N, (int)K, ldc, p.geo);
     return hipGetLastError();
 }
 
@@ -678,6 +740,19 @@ hipError_t launch_f(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *
 {
 #define GQ_LT(nt, itc) launch_t<F, nt, itc>(A, X, ldx, C, M, N, K, ldc, p, s)
 #define GQ_LTI(nt, itc) launch_t<F, nt, itc, 1>(A, X, ldx, C, M, N, K, ldc, p, s)
+    if (p.fp8) { // (itc = 0)
+        if constexpr (F == Q6_K)
+            if (p.img) switch (p.nt) {
+                case 1: return launch_t<F, 1, 0, 1, 1>(A, X, ldx, C, M, N, K, ldc, p, s);
+                case 2: return launch_t<F, 2, 0, 1, 1>(A, X, ldx, C, M, N, K, ldc, p, s);
+                default: return launch_t<F, 4, 0, 1, 1>(A, X, ldx, C, M, N, K, ldc, p, s);
+                }
+        switch (p.nt) {
+        case 1: return launch_t<F, 1, 0, 0, 1>(A, X, ldx, C, M, N, K, ldc, p, s);
+        case 2: return launch_t<F, 2, 0, 0, 1>(A, X, ldx, C, M, N, K, ldc, p, s);
+        default: return launch_t<F, 4, 0, 0, 1>(A, X, ldx, C, M, N, K, ldc, p, s);
+        }
+    }
     if constexpr (F == Q6_K) { // pick(): at most 8 cached units (4 chunks), 2 with two tokens
         if (p.img) switch (p.nt * 8 + p.itc) {
             case 8: return GQ_LTI(1, 0);
@@ -748,7 +823,7 @@ struct GroupedArgs {
     GroupedProblem p[kMaxGroup];
 };
 
-template <int NT>
+template <int NT, int FP8 = 0>
 __global__ __launch_bounds__(DW * 64) void stream_decode_grouped_kernel(const GroupedArgs args)
 {
     extern __shared__ __attribute__((aligned(1024))) uint8_t smem[];
@@ -765,7 +840,15 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_grouped_kernel(const Gr
     case Q6_K * 16 + 8 + itc:                                                                                          \
         decode_body<Q6_K, NT, itc, 1>(q.A, q.X, q.ldx, q.C, q.M, args.N, q.K, q.ldc, q.geo, bx, q.gx, q.by, smem);   \
         return;
-    if constexpr (NT == 1) {
+    if constexpr (FP8) { // (itc = 0)
+        switch (q.code) {
+        case Q8_0 * 16: decode_body<Q8_0, NT, 0, 0, 1>(q.A, q.X, q.ldx, q.C, q.M, args.N, q.K, q.ldc, q.geo, bx, q.gx, q.by, smem); return;
+        case Q4_K * 16: decode_body<Q4_K, NT, 0, 0, 1>(q.A, q.X, q.ldx, q.C, q.M, args.N, q.K, q.ldc, q.geo, bx, q.gx, q.by, smem); return;
+        case Q6_K * 16: decode_body<Q6_K, NT, 0, 0, 1>(q.A, q.X, q.ldx, q.C, q.M, args.N, q.K, q.ldc, q.geo, bx, q.gx, q.by, smem); return;
+        case Q6_K * 16 + 8: decode_body<Q6_K, NT, 0, 1, 1>(q.A, q.X, q.ldx, q.C, q.M, args.N, q.K, q.ldc, q.geo, bx, q.gx, q.by, smem); return;
+        default: return;
+        }
+    } else if constexpr (NT == 1) {
         switch (q.code) {
             GQ_GB(Q8_0, 0) GQ_GB(Q8_0, 1) GQ_GB(Q8_0, 2) GQ_GB(Q8_0, 3) GQ_GB(Q8_0, 4) GQ_GB(Q8_0, 5) GQ_GB(Q8_0, 6)
             GQ_GB(Q8_0, 7) GQ_GB(Q4_K, 0) GQ_GB(Q4_K, 1) GQ_GB(Q4_K, 2) GQ_GB(Q4_K, 3) GQ_GB(Q4_K, 4) GQ_GB(Q4_K, 5)
@@ -789,25 +872,26 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_grouped_kernel(const Gr
 #undef GQ_GBI
 }
 
-template <int NT>
+template <int NT, int FP8 = 0>
 hipError_t launch_grouped_nt(GroupedArgs &a, int blocks, size_t lds, hipStream_t s)
 {
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void *)stream_decode_grouped_kernel<NT>,
+        hipError_t e = hipFuncSetAttribute((const void *)stream_decode_grouped_kernel<NT, FP8>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, LDS_CAP);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    stream_decode_grouped_kernel<NT><<<dim3((unsigned)blocks), dim3(DW * 64), lds, s>>>(a);
+    stream_decode_grouped_kernel<NT, FP8><<<dim3((unsigned)blocks), dim3(DW * 64), lds, s>>>(a);
     return hipGetLastError();
 }
 
 } // namespace
 
-bool decode_fused_ok(int fmt, int64_t N, int64_t K)
+bool decode_fused_ok(int fmt, int64_t N, int64_t K, bool fp8)
 {
     Pick p;
+    p.fp8 = fp8;
     // 32-bit buffer offsets: the packed tensor must stay below 2 GiB (the C ABI splits larger ones).
     // When the tokens' activations do not fit LDS beside the ring (long K: every extra token
     // group streams the weights again), the GEMV path (activations quantized once to global,
@@ -817,13 +901,14 @@ bool decode_fused_ok(int fmt, int64_t N, int64_t K)
 }
 
 hipError_t launch_decode_fused(int fmt, const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, int64_t M,
-                               int64_t N, int64_t K, int64_t ldc, hipStream_t s)
+                               int64_t N, int64_t K, int64_t ldc, hipStream_t s, bool fp8)
 {
     const int64_t RB = row_bytes(fmt, K);
     const int64_t max_rows = ((int64_t)1 << 31) / RB - 1; // rows per launch under 2 GiB
     for (int64_t m0 = 0; m0 < M; m0 += max_rows) {
         const int64_t m = M - m0 < max_rows ? M - m0 : max_rows;
         Pick p;
+        p.fp8 = fp8;
         if (!pick(fmt, m, N, K, p)) return hipErrorInvalidValue;
         hipError_t e;
         switch (fmt) {
@@ -836,25 +921,27 @@ hipError_t launch_decode_fused(int fmt, const uint8_t *A, const uint16_t *X, int
     return hipSuccess;
 }
 
-bool decode_grouped_ok(const DecodeItem *items, int n, int64_t N)
+bool decode_grouped_ok(const DecodeItem *items, int n, int64_t N, bool fp8)
 {
-    if (n < 1 || n > kMaxGroup || N < 1 || N > 4) return false;
+    if (n < 1 || n > kMaxGroup || N < 1 || N > (fp8 ? 2 : 4)) return false;
     for (int i = 0; i < n; ++i) {
         const DecodeItem &it = items[i];
-        if (it.M < 1 || !decode_fused_ok(it.fmt, N, it.K)) return false;
+        if (it.M < 1 || !decode_fused_ok(it.fmt, N, it.K, fp8)) return false;
         if (it.M * row_bytes(it.fmt, it.K) >= ((int64_t)1 << 31)) return false; // 32-bit buffer offsets
     }
     return true;
 }
 
-hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipStream_t s)
+hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipStream_t s, bool fp8)
 {
-    if (!decode_grouped_ok(items, n, N)) return hipErrorInvalidValue;
+    if (!decode_grouped_ok(items, n, N, fp8)) return hipErrorInvalidValue;
     // every item's token tile as a launch of its own would pick it (bit-identical rows); one
     // launch per distinct tile (a Q6_K long-K item caps it at 2 tokens, so 3-4 tokens can take two)
     Pick solo[kMaxGroup];
-    for (int i = 0; i < n; ++i)
+    for (int i = 0; i < n; ++i) {
+        solo[i].fp8 = fp8;
         if (!pick(items[i].fmt, items[i].M, N, items[i].K, solo[i])) return hipErrorInvalidValue;
+    }
     for (int nt : {1, 2, 4}) {
         // the launch's parts: (item, token group); its LDS is the largest part's
         int pi[kMaxGroup], py[kMaxGroup], np = 0;
@@ -869,6 +956,8 @@ hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipS
                 py[np] = y;
                 // Q6_K bytes weigh more at 1-2 tokens (their unpacking costs more per byte than
                 // Q4_K's): measured on the Q4_K_M 7B layer, profiles/r03/tails/grouped_q6k_weight_ab.log
+                // (re-swept after the Q6_K ring image: 0.9-1.75 at one and two tokens, none better,
+                // profiles/r03/s3/grouped_q6w_sweep.log)
                 const double q6w = nt == 1 ? 1.15 : (nt == 2 ? 1.5 : 1.0);
                 bytes[np] = (double)items[i].M * (double)row_bytes(items[i].fmt, items[i].K) *
                             (items[i].fmt == Q6_K ? q6w : 1.0);
@@ -916,6 +1005,7 @@ hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipS
         for (int j = 0; j < np; ++j) {
             const int i = pi[j];
             Pick p;
+            p.fp8 = fp8;
             if (!pick(items[i].fmt, items[i].M, N, items[i].K, p, wg[j]) || p.nt != nt) return hipErrorInvalidValue;
             GroupedProblem &q = a.p[j];
             q.A = items[i].A;
@@ -933,7 +1023,8 @@ hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipS
             blocks += p.grid;
         }
         a.n = np;
-        hipError_t e = nt == 1   ? launch_grouped_nt<1>(a, blocks, lds, s)
+        hipError_t e = fp8       ? (nt == 1 ? launch_grouped_nt<1, 1>(a, blocks, lds, s) : launch_grouped_nt<2, 1>(a, blocks, lds, s))
+                       : nt == 1 ? launch_grouped_nt<1>(a, blocks, lds, s)
                        : nt == 2 ? launch_grouped_nt<2>(a, blocks, lds, s)
                                  : launch_grouped_nt<4>(a, blocks, lds, s);
         if (e != hipSuccess) return e;

@@ -59,6 +59,7 @@ SIGNATURES = {
     "gq_mmq_sharded_workspace_size": ([_I, _I64, _I64, _I64, _I], _SZ),
     "gq_mmq_sharded": ([_I, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _I, _P, _P, _SZ, _P], _I),
     "gq_mmq_grouped": ([ctypes.POINTER(GroupItem), _I, _I64, _P], _I),
+    "gq_mmq_grouped_ex": ([_I, ctypes.POINTER(GroupItem), _I, _I64, _P], _I),
     "gq_act_prepare_grouped": ([_I, ctypes.POINTER(PrepItem), _I, _P], _I),
     "gq_last_error": ([], ctypes.c_char_p),
     "gq_version": ([], _I),
@@ -209,9 +210,10 @@ def mmq(gtype: int, A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int,
     return C
 
 
-def mmq_grouped(items, N: int):
-    """One grouped decode launch (gq_mmq_grouped) for several MMQs with the same token count N
-    (1..4): items = [(gtype, A, B, M, K, out or None), ...], every B an fp16 (N, K) tensor.
+def mmq_grouped(items, N: int, act: str = "q8_1"):
+    """One grouped decode launch (gq_mmq_grouped_ex) for several MMQs with the same token count N
+    (1..4; act="fp8": 1..2): items = [(gtype, A, B, M, K, out or None), ...], every B an fp16
+    (N, K) tensor.
     Returns the (N, M) outputs (bit-identical to mmq() per item), or None when the library
     reports the shapes unsupported (N > 4, or an item that is no one-launch decode shape) --
     nothing was launched then and the caller runs mmq() per item."""
@@ -230,7 +232,7 @@ def mmq_grouped(items, N: int):
         outs.append(C)
         arr[i] = GroupItem(gtype, A.data_ptr(), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, K)
     with torch.cuda.device(dev):
-        rc = lib().gq_mmq_grouped(arr, len(items), N, torch.cuda.current_stream(dev).cuda_stream)
+        rc = lib().gq_mmq_grouped_ex(ACTS[act], arr, len(items), N, torch.cuda.current_stream(dev).cuda_stream)
     if rc == GQ_EUNSUPPORTED:
         return None
     _check(rc)

@@ -114,7 +114,7 @@ class LayerMix:
         res = {}
         inputs = (x, x if attn is None else attn, x if x_ffn is None else x_ffn, h)
         done = False
-        if (self.act == "q8_1" and x.shape[0] <= self.max_grouped
+        if (x.shape[0] <= (self.max_grouped if self.act == "q8_1" else min(2, self.max_grouped))
                 and all(inp.shape[0] == x.shape[0] for inp in inputs)):
             N = x.shape[0]
             keys, items = [], []
@@ -122,14 +122,13 @@ class LayerMix:
                 for key, L in calls:
                     keys.append(key)
                     items.append((L.gtype, L.A, inp, L.M, inp.shape[1], self._out(key, L, N, inp.device, out)))
-            outs = _lib.mmq_grouped(items, N)
+            outs = _lib.mmq_grouped(items, N, act=self.act)
             if outs is not None:
                 res.update(zip(keys, outs))
                 done = True
-        if not done and all(inp.shape[0] == x.shape[0] for inp in inputs) and (x.shape[0] > 4 or self.act == "fp8"):
+        if not done and all(inp.shape[0] == x.shape[0] for inp in inputs) and x.shape[0] > (4 if self.act == "q8_1" else 2):
             # every input group's activations quantized in ONE launch (gq_act_prepare_grouped),
             # then every call prepared -- bit-identical to each call quantizing its own input
-            # (fp8: at every token count -- it has no decode kernel)
             N = x.shape[0]
             preps, wss = [], []
             for calls, inp in zip(self.calls, inputs):
@@ -146,7 +145,7 @@ class LayerMix:
         if not done:
             for calls, inp in zip(self.calls, inputs):
                 N, K = inp.shape
-                if (N <= 4 and self.act == "q8_1") or len(calls) == 1:
+                if N <= (4 if self.act == "q8_1" else 2) or len(calls) == 1:
                     # decode (each call quantizes its tokens in-kernel), or a single call
                     for key, L in calls:
                         res[key] = _lib.mmq(L.gtype, L.A, inp, L.M, N, K, out=self._out(key, L, N, inp.device, out),

@@ -192,6 +192,10 @@ typedef struct gq_group_item {
     int64_t M, K;
 } gq_group_item;
 int gq_mmq_grouped(const gq_group_item *items, int n, int64_t N, void *stream);
+/* The same with an activation format: GQ_ACT_Q8_1 is gq_mmq_grouped; GQ_ACT_FP8_E4M3 (the fp8
+ * variant, its decode form at N <= 2) gives every item gq_mmq_ex(..., GQ_ACT_FP8_E4M3, ...)'s
+ * bits and is GQ_EUNSUPPORTED (nothing launched) from N = 3. */
+int gq_mmq_grouped_ex(gq_act act, const gq_group_item *items, int n, int64_t N, void *stream);
 
 /* Text of the last error on this thread ("" if none). */
 const char *gq_last_error(void);

@@ -202,3 +202,43 @@ def test_layer_mix_prepared_matches_per_call(N, act):
         torch.cuda.synchronize()
         assert torch.equal(res[n].view(torch.int16), solo.view(torch.int16)), n
         assert O.max_rel_err(fused[n].cpu().numpy(), solo.cpu().numpy()) <= 4e-3, n
+
+
+@pytest.mark.parametrize("N", [1, 2, 3])
+@pytest.mark.parametrize("layer", [0, 5])
+def test_grouped_llama_layer_fp8(N, layer):
+    """The fp8 activation variant's grouped decode (gq_mmq_grouped_ex, GQ_ACT_FP8_E4M3: the decode
+    kernel's FP8 form, fp16 x~ and v_dot2): the seven Llama-7B projections in one launch, each
+    bit-identical to its own mmq(act="fp8") call and within the fp8 tolerance of the fp8-exact
+    product; refused (nothing launched) when an item has no one-launch fp8 decode form -- from 3
+    tokens, and at 2 for the ffn_down's K = 11008 (2 x 11008 fp16 x~ do not fit LDS beside the
+    ring)."""
+    import kernels._lib as kl
+    from gguf import LLAMA_LAYER_SHAPES, q4_k_m_layer_types
+    dev = _dev()
+    types = q4_k_m_layer_types(layer, 32)
+    raw, A = _layer(types, seed=100 * layer + 1)
+    x = random_activations(N, 4096, seed=3 + N)
+    h = random_activations(N, 11008, seed=4 + N)
+    xt, ht = torch.from_numpy(x).to(dev), torch.from_numpy(h).to(dev)
+    items, names = [], []
+    for n, (M, K) in LLAMA_LAYER_SHAPES.items():
+        names.append(n)
+        items.append((kl.TYPES[types[n]], A[n], ht if K == 11008 else xt, M, K, None))
+    outs = kl.mmq_grouped(items, N, act="fp8")
+    if N >= 2:
+        assert outs is None
+        return
+    assert outs is not None, kl.lib().gq_last_error()
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(N + 7)
+    for n, C in zip(names, outs):
+        M, K = LLAMA_LAYER_SHAPES[n]
+        solo = kl.mmq(kl.TYPES[types[n]], A[n], ht if K == 11008 else xt, M, N, K, act="fp8")
+        torch.cuda.synchronize()
+        assert torch.equal(C.view(torch.int16), solo.view(torch.int16)), n
+        rows = np.sort(rng.choice(M, size=24, replace=False))
+        rb = raw[n].size // M
+        sub = np.concatenate([raw[n][r * rb:(r + 1) * rb] for r in rows])
+        ideal = O.mmq_fp8_ideal(types[n], sub, h if K == 11008 else x, len(rows), N, K)
+        assert O.max_rel_err(C.cpu().numpy()[:, rows], ideal) <= 4e-3, n

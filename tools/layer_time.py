@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Q4_K_M Llama-7B layer (bench.bench_layer) at decode sizes, grouped vs one launch per set.
-python tools/layer_time.py [Ns] [--lib other-build.so] [--grouped-only] [--tune KEY=V,...]"""
+python tools/layer_time.py [Ns] [--lib other-build.so] [--grouped-only] [--tune KEY=V,...] [--act fp8]"""
 import json
 import os
 import sys
@@ -21,9 +21,10 @@ if "--tune" in args:  # library tuning overrides (gq_debug_set_tuning)
     for kv in filter(None, args[args.index("--tune") + 1].split(",")):
         k, v = kv.split("=")
         kl.set_tuning(k, int(v))
-pos = [a for i, a in enumerate(args) if not a.startswith("--") and (i == 0 or args[i - 1] not in ("--lib", "--tune"))]
+act = args[args.index("--act") + 1] if "--act" in args else "q8_1"
+pos = [a for i, a in enumerate(args) if not a.startswith("--") and (i == 0 or args[i - 1] not in ("--lib", "--tune", "--act"))]
 Ns = tuple(int(n) for n in (pos[0] if pos else "1,2,3,4").split(","))
 for grouped in ((True,) if "--grouped-only" in args else (True, False)):  # (True: grouped at 1..4 tokens)
-    r = bench.bench_layer(Ns, ("q8_1",), 50, 5, dev, fuse=True, grouped=grouped)
-    print(json.dumps({"grouped": grouped, "tune": args[args.index("--tune") + 1] if "--tune" in args else "", "lib": os.path.basename(lib or "libgguf_mmq.so"), "weight_bytes": r["weight_bytes"],
+    r = bench.bench_layer(Ns, (act,), 50, 5, dev, fuse=True, grouped=grouped)
+    print(json.dumps({"grouped": grouped, "act": act, "tune": args[args.index("--tune") + 1] if "--tune" in args else "", "lib": os.path.basename(lib or "libgguf_mmq.so"), "weight_bytes": r["weight_bytes"],
                       "points": [(p["M_tok"], p["us_per_step"], p["weight_GBps"]) for p in r["points"]]}), flush=True)

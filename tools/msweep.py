@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--tune", default="", help="KEY=V,... library tuning overrides (gq_debug_set_tuning)")
     ap.add_argument("--lib", default=None, help="another build of libgguf_mmq.so (diagnostic variants)")
+    ap.add_argument("--act", default="q8_1", help="activation format: q8_1 or fp8")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     import kernels._lib as kl
@@ -31,9 +32,9 @@ def main():
     for shp in a.shapes.split(","):
         fmt, M, K = shp.split(":")
         M, K = int(M), int(K)
-        row = {"shape": shp, "tune": a.tune, "lib": os.path.basename(kl.LIB_PATH), "us": {}, "hbm_frac": {}}
+        row = {"shape": shp, "act": a.act, "tune": a.tune, "lib": os.path.basename(kl.LIB_PATH), "us": {}, "hbm_frac": {}}
         for N in (int(t) for t in a.tokens.split(",")):
-            r = bench.Runner(fmt, M, K, N, dev, a.steps)
+            r = bench.Runner(fmt, M, K, N, dev, a.steps, act=a.act)
             g = r.capture(r.step, a.steps)
             g.replay()
             t = min(bench.timed_replay(g, dev) for _ in range(3)) / a.steps
