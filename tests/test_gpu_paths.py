@@ -57,6 +57,28 @@ def test_q8_0_int8_mfma_gemm(M, N, K, splits, tune):
     assert O.allclose(exact, got, 0.01)
 
 
+@pytest.mark.parametrize("M,N,K", [(4096, 128, 4096), (11008, 128, 4096), (4096, 300, 11008)])
+def test_q8_0_int8_mfma_full_size(M, N, K, tune):
+    """The int8 form at BASELINE sizes (configs[1]: 4096^2 x128; the 7B up/down shapes), every
+    token, 48 sampled rows against the oracle (IDEAL at the tight int8 gate, EXACT at the
+    reference's 1%)."""
+    from kernels._lib import TYPES, mmq
+    tune(GQ_GEMM_I8=1, GQ_WGEMM=0)
+    dev = _dev()
+    qA = random_blocks("q8_0", M, K, seed=M + K)
+    B = random_activations(N, K, seed=N + 11)
+    C = mmq(TYPES["q8_0"], torch.from_numpy(qA.view(np.int8)).to(dev), torch.from_numpy(B).to(dev), M, N, K)
+    torch.cuda.synchronize()
+    rows = np.sort(np.random.default_rng(M).choice(M, size=48, replace=False))
+    rb = qA.size // M
+    sub = np.concatenate([qA[r * rb:(r + 1) * rb] for r in rows])
+    got = C.cpu().numpy()[:, rows]
+    ideal = O.mmq_from_fp16("q8_0", sub, B, len(rows), N, K, O.IDEAL)
+    assert O.max_rel_err(got, ideal) <= TIGHT_I8
+    exact = O.mmq_from_fp16("q8_0", sub, B, len(rows), N, K, O.EXACT)
+    assert O.allclose(exact, got, 0.01)
+
+
 def test_q8_0_int8_mfma_golden(golden, tune):
     """Every golden case of the reference through the int8 form (cases with N >= 5 run it)."""
     tune(GQ_GEMM_I8=1, GQ_WGEMM=0)
