@@ -1,13 +1,20 @@
-// gguf_half.hpp -- IEEE binary16 <-> binary32 on the host (round to nearest even).
-// Host-only helpers shared by the format producers and the C-ABI argument checks;
-// device code uses the hardware conversions (v_cvt_f16_f32 / v_cvt_f32_f16).
+// gguf_half.hpp -- IEEE binary16 <-> binary32 in software (round to nearest even).
+// Shared by the format producers (host, and the device quantizers of quant_device.hip, which
+// run the host's exact code) and the C-ABI argument checks; the MMQ kernels use the hardware
+// conversions (v_cvt_f16_f32 / v_cvt_f32_f16).
 #pragma once
 #include <cstdint>
 #include <cstring>
 
+#ifdef __HIPCC__
+#define GQ_HHD __host__ __device__
+#else
+#define GQ_HHD
+#endif
+
 namespace gq {
 
-inline float h2f(uint16_t h)
+GQ_HHD inline float h2f(uint16_t h)
 {
     uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
     uint32_t exp = (h >> 10) & 0x1fu;
@@ -29,14 +36,14 @@ inline float h2f(uint16_t h)
         bits = sign | ((uint32_t)(113 - shift) << 23) | ((man & 0x3ffu) << 13);
     }
     float f;
-    std::memcpy(&f, &bits, 4);
+    __builtin_memcpy(&f, &bits, 4);
     return f;
 }
 
-inline uint16_t f2h(float f)
+GQ_HHD inline uint16_t f2h(float f)
 {
     uint32_t x;
-    std::memcpy(&x, &f, 4);
+    __builtin_memcpy(&x, &f, 4);
     const uint16_t sign = (uint16_t)((x >> 16) & 0x8000u);
     const uint32_t ax = x & 0x7fffffffu;
     if (ax >= 0x7f800000u) return (uint16_t)(sign | 0x7c00u | (ax != 0x7f800000u ? 0x200u : 0u));

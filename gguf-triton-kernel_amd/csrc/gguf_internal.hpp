@@ -56,6 +56,10 @@ enum ActForm : int { AF_F16 = 0, AF_I8 = 1 };
 // group stored (0,2,1,3); out1 = float 2^e [K/32][(rows + 3) & ~3], e the smallest integer with
 // max|x| <= 448 * 2^e over the block (2^0 for an all-zero block); code = e4m3(x / 2^e), RNE.
 // F8DEQ: out0 = fp16 code * 2^e [rows][K] in the DEQ layout (the fp8 variant's GEMM input).
+// Weight quantizers on the device (quant_device.hip): kind 0 Q8_0 (fp16 in), 1 Q4_K (fp32),
+// 2 Q6_K (fp32), 3 Q8_1 (fp16); the host producers' bytes.
+hipError_t launch_quant_blocks(int kind, const void *x, void *y, int64_t nblocks, hipStream_t s);
+
 hipError_t launch_act_quant(int mode, const uint16_t *X, int64_t ldx, int64_t rows, int64_t K, void *out0,
                             void *out1, void *out2, hipStream_t s);
 // The DEQ form of up to kMaxDeqSegs tensors in one launch (wg0 is set by the launcher),

@@ -737,6 +737,21 @@ int gq_quantize_q8_1(const void *X, void *Y, int64_t rows, int64_t K, int64_t ld
     return GQ_OK;
 }
 
+int gq_quantize_weights(gq_type t, const void *X, void *Y, int64_t n, void *stream)
+{
+    g_err.clear();
+    if (t != GQ_Q8_0 && t != GQ_Q4_K && t != GQ_Q6_K) return fail(GQ_EUNSUPPORTED, "unknown gguf type %d", (int)t);
+    if (n < 0) return fail(GQ_EINVAL, "negative size");
+    const int qk = block_elems(t);
+    if (n % qk != 0) return fail(GQ_EINVAL, "n=%lld is not a multiple of %d", (long long)n, qk);
+    if (n == 0) return GQ_OK;
+    if (!X || !Y) return fail(GQ_EINVAL, "null pointer");
+    const int kind = t == GQ_Q8_0 ? 0 : (t == GQ_Q4_K ? 1 : 2);
+    hipError_t e = gq::launch_quant_blocks(kind, X, Y, n / qk, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (weight quantizer): %s", hipGetErrorString(e));
+    return GQ_OK;
+}
+
 int gq_quantize_fp8(const void *X, void *codes, void *scales, int64_t rows, int64_t K, int64_t ldx, void *stream)
 {
     g_err.clear();

@@ -53,6 +53,7 @@ SIGNATURES = {
     "gq_act_prepare_ex": ([_I, _P, _I64, _I64, _I64, _P, _SZ, _P], _I),
     "gq_mmq_prepared_ex": ([_I, _I, _P, _P, _SZ, _P, _I64, _I64, _I64, _I64, _P], _I),
     "gq_quantize_fp8": ([_P, _P, _P, _I64, _I64, _I64, _P], _I),
+    "gq_quantize_weights": ([_I, _P, _P, _I64, _P], _I),
     "gq_shard_rows": ([_I64, _I, _I, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                        ctypes.POINTER(ctypes.c_int64)], _I),
     "gq_assemble_shards": ([_P, _P, _I, _I64, _I64, _I64, _I64, _P], _I),
@@ -315,6 +316,24 @@ def mmq_prepared(gtype: int, A: torch.Tensor, workspace: torch.Tensor, M: int, N
         _check(lib().gq_mmq_prepared_ex(gtype, ACTS[act], A.data_ptr(), workspace.data_ptr(), workspace.numel(),
                                         C.data_ptr(), M, N, K, C.stride(0), stream))
     return C
+
+
+def quantize_weights_device(fmt: str, X: torch.Tensor) -> torch.Tensor:
+    """GGUF weight quantization on the device (gq_quantize_weights): the bytes of
+    utils.quantize.quantize_to_<fmt> (int8, flat), from an fp16 (q8_0) or fp32 (q4_k, q6_k)
+    device tensor read as flat blocks."""
+    want = torch.float16 if fmt == "q8_0" else torch.float32
+    if not X.is_cuda or X.dtype != want:
+        raise RuntimeError(f"quantize_weights_device({fmt}) needs a {want} device tensor")
+    X = X.contiguous().reshape(-1)
+    qk, nbytes = (32, 34) if fmt == "q8_0" else (256, 144 if fmt == "q4_k" else 210)
+    if X.numel() % qk:
+        raise RuntimeError(f"{X.numel()} elements are not whole {fmt} blocks")
+    out = torch.empty(X.numel() // qk * nbytes, dtype=torch.int8, device=X.device)
+    with torch.cuda.device(X.device):
+        _check(lib().gq_quantize_weights(TYPES[fmt], X.data_ptr(), out.data_ptr(), X.numel(),
+                                         torch.cuda.current_stream(X.device).cuda_stream))
+    return out
 
 
 def quantize_fp8_device(X: torch.Tensor):

@@ -14,6 +14,7 @@
  *   gq_mmq(GQ_Q4_K, ...)  <- kernels/mmq_q4_k.py:240  mmq_q4_k(A, B, M, N, K)
  *   gq_mmq(GQ_Q6_K, ...)  <- kernels/mmq_q6_k.py:197  mmq_q6_k(A, B, M, N, K)
  *   gq_quantize_q8_1      <- utils/quantize/q8_1.py:18 quantize_to_q8_1 (on the device)
+ *   gq_quantize_weights   <- utils/quantize/{q8_0.py:4, q4_k.py:87, q6_k.py:97} (on the device)
  *   gq_dequantize         <- utils/quantize/q4_k.py:125, q6_k.py:117, q8_0.py:52 dequantize (device)
  * Beyond the reference (no counterpart there):
  *   gq_*_ex(..., GQ_ACT_FP8_E4M3, ...)  the fp8 activation variant (BASELINE.json configs[4])
@@ -137,6 +138,17 @@ int gq_quantize_q8_1(const void *X, void *Y, int64_t rows, int64_t K, int64_t ld
  * (0,2,1,3), and scales [K/32][(rows + 3) & ~3] float X = 2^e (block-major).
  */
 int gq_quantize_fp8(const void *X, void *codes, void *scales, int64_t rows, int64_t K, int64_t ldx, void *stream);
+
+/*
+ * GGUF weight quantization on the device (the reference quantizes on the host only), byte-
+ * identical to the reference's producers and to include/gguf_quant.h's gq_quantize_*:
+ *   GQ_Q8_0: X = n fp16 values (n % 32 == 0)  -> Y = n/32 blocks of 34 bytes (quantize_to_q8_0)
+ *   GQ_Q4_K: X = n fp32 values (n % 256 == 0) -> Y = n/256 blocks of 144 bytes (quantize_to_q4_k)
+ *   GQ_Q6_K: X = n fp32 values (n % 256 == 0) -> Y = n/256 blocks of 210 bytes (quantize_to_q6_k)
+ * X is read as flat blocks (a row-major (M, K) matrix gives the packed A of gq_mmq).  One thread
+ * per block runs the host producer's exact code; no host sync.
+ */
+int gq_quantize_weights(gq_type t, const void *X, void *Y, int64_t n, void *stream);
 
 /*
  * Row-sharded MMQ over the GPUs of one node (SURVEY.md 8(b) "gq_mmq_sharded", 8(e)).  The
