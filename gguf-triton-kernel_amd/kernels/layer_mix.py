@@ -126,6 +126,17 @@ class LayerMix:
             if outs is not None:
                 res.update(zip(keys, outs))
                 done = True
+            elif self.act == "fp8" and N == 2:
+                # the fp8 decode form holds 2 tokens' fp16 x~ in LDS: rows of K > 8192 (ffn_down's
+                # 11008) do not fit beside the ring -- group the rest, run those on their own
+                sub = [i for i, it in enumerate(items) if it[4] <= 8192]
+                o = _lib.mmq_grouped([items[i] for i in sub], N, act=self.act) if 0 < len(sub) < len(items) else None
+                if o is not None:
+                    res.update(zip([keys[i] for i in sub], o))
+                    for i, (g, A, inp, M, K, buf) in enumerate(items):
+                        if i not in sub:
+                            res[keys[i]] = _lib.mmq(g, A, inp, M, N, K, out=buf, act=self.act)
+                    done = True
         if not done and all(inp.shape[0] == x.shape[0] for inp in inputs) and x.shape[0] > (4 if self.act == "q8_1" else 2):
             # every input group's activations quantized in ONE launch (gq_act_prepare_grouped),
             # then every call prepared -- bit-identical to each call quantizing its own input

@@ -176,7 +176,7 @@ def test_act_prepare_grouped_matches_individual(act):
 
 
 @pytest.mark.parametrize("N,act", [(5, "q8_1"), (8, "q8_1"), (16, "q8_1"), (64, "q8_1"), (128, "q8_1"),
-                                   (1, "fp8"), (3, "fp8"), (8, "fp8"), (128, "fp8")])
+                                   (1, "fp8"), (2, "fp8"), (3, "fp8"), (8, "fp8"), (128, "fp8")])
 def test_layer_mix_prepared_matches_per_call(N, act):
     """LayerMix from 5 tokens (the four inputs quantized in one gq_act_prepare_grouped launch, every
     projection prepared): unfused, every projection bit-identical to its own mmq(); fused (q+k and
