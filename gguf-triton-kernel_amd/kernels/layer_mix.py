@@ -16,7 +16,11 @@ graph-replayed, profiles/r03/tails/grouped_q6k_weight_ab.log): 28.8 / 42.3 / 58.
 and True take it at 1..4 tokens (a call the grouped launch refuses -- e.g. a long-K Q6_K item
 at 3..4 tokens -- runs the sets' own launches), False never.  From 5 tokens on (q8_1) the four
 inputs' activations are quantized in one launch (gq_act_prepare_grouped) and every call reads
-them prepared: one act_quant launch per layer instead of four.
+them prepared: one act_quant launch per layer instead of four.  act="fp8" (the e4m3 variant):
+the decode kernel's fp8 form at 1..2 tokens -- one grouped launch (gq_mmq_grouped_ex) at one
+token, at two the projections whose 2-token x~ fits LDS grouped and the rest on their own
+(40 / 62 us for the 7B layer) -- and from 3 tokens the grouped prepare and prepared calls as
+q8_1 from 5 (profiles/r03/s3/fp8_decode.log).
 """
 from __future__ import annotations
 
