@@ -5,9 +5,11 @@
 Default workload = BASELINE.json configs[1]: Q8_0 weights N_out=4096 x K=4096, M_tok=128
 fp16 activations on one MI355X.  One "step" = one drop-in call: q8_1 quantization of the
 activations + the MMQ over one weight matrix (gq_mmq).  Inputs are resident in HBM before
-timing; the steps cycle through >= 1 GiB of distinct weight copies so the 256 MB
-Infinity Cache cannot serve them.  K steps are captured into one hipGraph and replayed;
-time = HIP events around the replay, bracketed by barrier + synchronize.
+timing.  K steps are captured into a hipGraph; ceil(copies / K) such graphs together cycle
+over >= 1 GiB of distinct weight copies (rotation_plan), whatever K is, and are replayed
+round robin, so every timed replay finds its weights evicted from the 256 MB Infinity Cache by
+the >= 1 GiB read since.  Time = HIP events around one replay (K steps), bracketed by barrier +
+synchronize; the MEDIAN over the replays is reported.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME] [--strong] [--quick] [--no-cpu]
 
@@ -89,6 +91,31 @@ def device_random_blocks(fmt: str, M: int, K: int, dev, seed: int) -> torch.Tens
     return raw.view(-1).view(torch.int8)
 
 
+def rotation_plan(wbytes: int, steps: int, rotate: int = ROTATE_BYTES):
+    """-> (ncopies, plans): ncopies = ceil(rotate / wbytes) (>= 2) distinct weight copies and
+    G = ceil(ncopies / steps) graphs of `steps` launches; launch i of graph g uses copy
+    (g * steps + i) % ncopies.  Replayed round robin (timed_rotation), every copy is read once
+    per round, so >= rotate bytes separate two reads of one copy whatever `steps` is."""
+    ncopies = max(2, math.ceil(rotate / max(1, wbytes)))
+    G = max(1, math.ceil(ncopies / max(1, steps)))
+    return ncopies, [[(g * steps + i) % ncopies for i in range(steps)] for g in range(G)]
+
+
+def rotated_bytes(wbytes: int, plans) -> int:
+    """Distinct weight bytes a rotation's graphs read per round."""
+    return wbytes * len({c for p in plans for c in p})
+
+
+def timed_rotation(graphs, dev, dist_on=False) -> float:
+    """Median seconds per replay: one untimed round, then round-robin replays of the graphs
+    (at least 6, at least 2 rounds), each timed alone (timed_replay)."""
+    for g in graphs:
+        g.replay()
+    torch.cuda.synchronize(dev)
+    rounds = max(2, math.ceil(6 / len(graphs)))
+    return float(np.median([timed_replay(g, dev, dist_on) for _ in range(rounds) for g in graphs]))
+
+
 def model(fmt, M, K, N):
     qk, nbytes = BLOCK[fmt]
     wbytes = M * (K // qk) * nbytes
@@ -106,8 +133,9 @@ class Runner:
         self.fmt, self.M, self.K, self.N, self.dev = fmt, M, K, N, dev
         self.act = kl.ACTS[act]
         self.gtype = GTYPE[fmt]
-        wbytes, _, _ = model(fmt, M, K, N)
-        self.ncopies = max(2, math.ceil(ROTATE_BYTES / wbytes))
+        self.wbytes, _, _ = model(fmt, M, K, N)
+        self.ncopies, self.plans = rotation_plan(self.wbytes, steps)
+        self.rotated = rotated_bytes(self.wbytes, self.plans)
         base = device_random_blocks(fmt, M, K, dev, seed)
         self.weights = [base] + [base.clone() for _ in range(self.ncopies - 1)]
         g = torch.Generator(device=dev).manual_seed(seed + 1)
@@ -120,8 +148,8 @@ class Runner:
     def _stream(self):
         return torch.cuda.current_stream(self.dev).cuda_stream
 
-    def step(self, i, c=None):
-        A = self.weights[i % self.ncopies]
+    def step(self, i, copy, c=None):
+        A = self.weights[copy]
         C = self.C[i & 1] if c is None else c
         rc = self.L.gq_mmq_ex(self.gtype, self.act, A.data_ptr(), self.B.data_ptr(), C.data_ptr(), self.M, self.N,
                               self.K, self.K, self.M, self.ws.data_ptr(), self.ws_bytes, self._stream())
@@ -134,25 +162,37 @@ class Runner:
         if rc:
             raise RuntimeError(self.L.gq_last_error().decode())
 
-    def kernel(self, i):
-        A = self.weights[i % self.ncopies]
+    def kernel(self, i, copy):
+        A = self.weights[copy]
         rc = self.L.gq_mmq_prepared_ex(self.gtype, self.act, A.data_ptr(), self.ws.data_ptr(), self.ws_bytes,
                                        self.C[i & 1].data_ptr(), self.M, self.N, self.K, self.M, self._stream())
         if rc:
             raise RuntimeError(self.L.gq_last_error().decode())
 
-    def capture(self, fn, n):
+    def capture(self, fn, copies):
+        """One graph of fn(i, copies[i]) for every i."""
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(s):
-            fn(0)  # warm the launch path outside capture
+            fn(0, copies[0])  # warm the launch path outside capture
         torch.cuda.current_stream(self.dev).wait_stream(s)
         torch.cuda.synchronize(self.dev)
         with torch.cuda.graph(g):
-            for i in range(n):
-                fn(i)
+            for i, c in enumerate(copies):
+                fn(i, c)
         return g
+
+    def graphs(self, fn):
+        """The rotation's graphs (rotation_plan) of fn."""
+        return [self.capture(fn, p) for p in self.plans]
+
+    def timed(self, fn):
+        """Median seconds per step of fn over the rotation (timed_rotation)."""
+        gs = self.graphs(fn)
+        t = timed_rotation(gs, self.dev) / len(self.plans[0])
+        del gs
+        return t
 
 
 def timed_replay(graph, dev, dist_on=False) -> float:
@@ -329,7 +369,7 @@ class ShardStep:
 
     CHUNKS = (1, 2, 4)
 
-    def __init__(self, fmt, M_global, K, N, dev, world, rank, seed=0, cpu=False, A_shard=None, B=None):
+    def __init__(self, fmt, M_global, K, N, dev, world, rank, seed=0, cpu=False, A_shard=None, B=None, steps=1):
         """A_shard / B (tests): this rank's packed rows (dist.row_shard.shard_bytes, align 256) and
         the fp16 activations, instead of random ones."""
         from dist.row_shard import shard_rows
@@ -343,7 +383,7 @@ class ShardStep:
         if cpu:
             from utils.quantize.q8_1 import quantize_to_q8_1
             from utils.synth import random_blocks
-            self.ncopies = 1
+            self.ncopies, self.plans = 1, [[0] * steps]
             base = torch.from_numpy(random_blocks(fmt, nrows, K, seed=seed + rank).view(np.int8))
             g = torch.Generator().manual_seed(seed + 1)
             self.B = torch.randn(N, K, generator=g).to(torch.float16) if B is None else B
@@ -351,7 +391,7 @@ class ShardStep:
         else:
             import kernels._lib as kl
             self.kl, self.L = kl, kl.lib()
-            self.ncopies = max(2, math.ceil(ROTATE_BYTES / max(1, self.rows * self.rb)))
+            self.ncopies, self.plans = rotation_plan(max(1, self.rows * self.rb), steps)
             base = device_random_blocks(fmt, nrows, K, dev, seed + rank)
             g = torch.Generator(device=dev).manual_seed(seed + 1)
             self.B = torch.randn(N, K, device=dev, generator=g).to(torch.float16) if B is None else B
@@ -377,14 +417,14 @@ class ShardStep:
         if rc:
             raise RuntimeError(self.L.gq_last_error().decode())
 
-    def compute(self, i, C, c, j):
-        """Local MMQ of chunk c (of C) of step i's weight copy into slab set j."""
+    def compute(self, copy, C, c, j):
+        """Local MMQ of chunk c (of C) of weight copy `copy` into slab set j."""
         Rc = self.R // C
         r0 = c * Rc
         n = max(0, min(self.rows - r0, Rc))
         if n == 0 or self.N == 0:
             return
-        A = self.weights[i % self.ncopies]
+        A = self.weights[copy]
         out = self.slab[C][j][c]
         if self.cpu:
             from kernels.cpu_impls._cpu import cpu_mmq
@@ -416,40 +456,43 @@ class ShardStep:
         return self.out[j][:, :self.Mg]
 
     # -- GPU: three graphs ----------------------------------------------------------------
-    def _graph(self, body, n):
+    def _graph(self, body, copies):
+        """One graph of body(i, copies[i], warm=False) for every i (two warm steps first, eager)."""
+        n = len(copies)
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(s):  # warm every op outside capture (RCCL communicator included)
-            body(0, True)
-            body(1, True)
+            body(0, copies[0], True)
+            body(1, copies[1 % n], True)
         torch.cuda.current_stream(self.dev).wait_stream(s)
         torch.cuda.synchronize(self.dev)
         g = torch.cuda.CUDAGraph()
         # thread_local: the process group's watchdog thread polls its work events during capture
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
-            for i in range(n):
-                body(i, False)
+            for i, cp in enumerate(copies):
+                body(i, cp, False)
         return g
 
-    def graph_compute(self, n):
-        def body(i, warm):
+    def graph_compute(self, copies):
+        def body(i, cp, warm):
             self.prepare()
-            self.compute(i, 1, 0, i & 1)
-        return self._graph(body, n)
+            self.compute(cp, 1, 0, i & 1)
+        return self._graph(body, copies)
 
-    def graph_overlap(self, n):
+    def graph_overlap(self, copies):
         """Independent steps: step i's exchange (one all_gather) runs on a side stream under step
         i+1's compute; slab set j is rewritten only after the exchange that read it."""
         side = torch.cuda.Stream(self.dev)
         done = [torch.cuda.Event() for _ in range(2)]
+        n = len(copies)
 
-        def body(i, warm):
+        def body(i, cp, warm):
             j = i & 1
             cur = torch.cuda.current_stream(self.dev)
             if i >= 2 and not warm:  # (only events recorded inside this capture)
                 cur.wait_event(done[j])
             self.prepare()
-            self.compute(i, 1, 0, j)
+            self.compute(cp, 1, 0, j)
             side.wait_stream(cur)
             with torch.cuda.stream(side):
                 self.gather(1, 0, j)
@@ -457,37 +500,44 @@ class ShardStep:
                 done[j].record(side)
             if warm or i == n - 1:
                 cur.wait_stream(side)
-        return self._graph(body, n)
+        return self._graph(body, copies)
 
-    def graph_chain(self, n, C):
+    def graph_chain(self, copies, C):
         """Dependent steps: step i+1's matmul waits for step i's assembled output; inside a step
         the C chunks pipeline compute against the exchange."""
         side = torch.cuda.Stream(self.dev)
         ev = [torch.cuda.Event() for _ in range(C)]
 
-        def body(i, warm):
+        def body(i, cp, warm):
             cur = torch.cuda.current_stream(self.dev)
             self.prepare()
             for c in range(C):
-                self.compute(i, C, c, 0)
+                self.compute(cp, C, c, 0)
                 ev[c].record(cur)
                 side.wait_event(ev[c])
                 with torch.cuda.stream(side):
                     self.gather(C, c, 0)
                     self.assemble(C, c, 0)
             cur.wait_stream(side)  # the next step starts from this step's output
-        return self._graph(body, n)
+        return self._graph(body, copies)
 
-    # -- CPU rehearsal: the same three, eager -------------------------------------------
+    # -- eager: the same three, launched one by one (the CPU rehearsal, and the GPU when a
+    # capture failed on any rank); the GPU forms quantize the activations per step as the graphs do
+    def copy_of(self, i):
+        p = self.plans[(i // len(self.plans[0])) % len(self.plans)]
+        return p[i % len(p)]
+
     def cpu_compute(self, n):
         for i in range(n):
-            self.compute(i, 1, 0, i & 1)
+            self.prepare()
+            self.compute(self.copy_of(i), 1, 0, i & 1)
 
     def cpu_overlap(self, n):
         pending = []
         for i in range(n):
             j = i & 1
-            self.compute(i, 1, 0, j)
+            self.prepare()
+            self.compute(self.copy_of(i), 1, 0, j)
             pending.append((self.gather(1, 0, j, async_op=True), j))
             if len(pending) > 1:
                 w, jj = pending.pop(0)
@@ -500,8 +550,9 @@ class ShardStep:
     def cpu_chain(self, n, C):
         for i in range(n):
             works = []
+            self.prepare()
             for c in range(C):
-                self.compute(i, C, c, 0)
+                self.compute(self.copy_of(i), C, c, 0)
                 works.append(self.gather(C, c, 0, async_op=True))
             for c, w in enumerate(works):
                 w.wait()
@@ -515,73 +566,97 @@ def _max_over_ranks(t, dev):
     return float(tt.item())
 
 
-def time_sharded(ss: ShardStep, steps, warmup):
-    """{compute, overlap, chain_C...}: seconds per step, max over ranks (barrier on both sides)."""
+def agree_all(ok: bool, dev) -> bool:
+    """True on every rank iff `ok` on every rank (one all_reduce MIN): a decision every rank
+    must take the same way -- e.g. graphs holding captured all_gathers on some ranks and eager
+    collectives on others would pair mismatched collectives and hang the group."""
     import torch.distributed as dist
-    res = {}
-    if ss.cpu:
-        runs = [("compute", ss.cpu_compute), ("overlap", ss.cpu_overlap)] + \
-               [(f"chain{C}", (lambda n, C=C: ss.cpu_chain(n, C))) for C in ss.CHUNKS]
-        for key, run in runs:
-            run(max(1, warmup))
-            dist.barrier()
-            t0 = time.perf_counter()
-            run(steps)
-            t = time.perf_counter() - t0
-            dist.barrier()
-            res[key] = _max_over_ranks(t, ss.dev) / steps
-        return res
-    graphs = [("compute", lambda n: ss.graph_compute(n)), ("overlap", lambda n: ss.graph_overlap(n))] + \
-             [(f"chain{C}", (lambda n, C=C: ss.graph_chain(n, C))) for C in ss.CHUNKS]
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def capture_fault_injected() -> bool:
+    """BENCH_INJECT_CAPTURE_FAIL=<rank>: that rank's capture step fails (tests of the agreement)."""
+    r = os.environ.get("BENCH_INJECT_CAPTURE_FAIL")
+    return r is not None and r != "" and int(r) == int(os.environ.get("RANK", "0"))
+
+
+def time_eager(run, steps, warmup, dev, cpu):
+    import torch.distributed as dist
+    run(max(1, warmup))
+    if not cpu:
+        torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    run(steps)
+    if not cpu:
+        torch.cuda.synchronize(dev)
+    t = time.perf_counter() - t0
+    dist.barrier()
+    return _max_over_ranks(t, dev) / steps
+
+
+def time_sharded(ss: ShardStep, steps, warmup):
+    """{compute, overlap, chain_C..., graph}: seconds per step, max over ranks (barrier on both
+    sides).  GPU: every key's graphs (one per rotation plan) are captured first, then the ranks
+    agree (agree_all) -- all replay graphs, or, if a capture failed on ANY rank, all time every
+    key eagerly (the same ops, the per-step activation quantization included).  A failed capture
+    (hipErrorStreamCaptureUnjoined once in four world-1 runs in round 3, its log not kept) then
+    changes the timing mode of the whole line, never of one rank or one key."""
     eager = {"compute": ss.cpu_compute, "overlap": ss.cpu_overlap}
     eager.update({f"chain{C}": (lambda n, C=C: ss.cpu_chain(n, C)) for C in ss.CHUNKS})
-    use_graph = True
-    for key, make in graphs:
-        if use_graph:
-            try:
-                g = make(steps)
-            except Exception as e:  # (every rank runs the same capture)
-                # seen once on one MI355X at world 1 (hipErrorStreamCaptureUnjoined from a capture
-                # holding the process group's all_gather; the next run of the same command was clean)
-                print(f"bench: graph capture of the sharded step ({key}) failed ({e!r}); timing it eagerly",
-                      file=sys.stderr, flush=True)
-                use_graph = False
-                res["graph"] = False
-                torch.cuda.synchronize(ss.dev)
-        if use_graph:
-            g.replay()
+    built, ok = {}, True
+    if not ss.cpu:
+        makers = [("compute", ss.graph_compute), ("overlap", ss.graph_overlap)] + \
+                 [(f"chain{C}", (lambda cp, C=C: ss.graph_chain(cp, C))) for C in ss.CHUNKS]
+        try:
+            if capture_fault_injected():
+                raise RuntimeError("injected capture failure (BENCH_INJECT_CAPTURE_FAIL)")
+            for key, make in makers:
+                built[key] = [make(p) for p in ss.plans]
+        except Exception as e:
+            print(f"bench: graph capture of the sharded step failed on rank {os.environ.get('RANK', '0')} ({e!r})",
+                  file=sys.stderr, flush=True)
+            ok = False
+            built = {}
             torch.cuda.synchronize(ss.dev)
-            res[key] = min(timed_replay(g, ss.dev, True) for _ in range(3)) / steps
-            del g
-            continue
-        # eager fallback: the same ops launched one by one, synchronized and timed as the graphs
-        run = eager[key]
-        run(max(1, warmup))
-        torch.cuda.synchronize(ss.dev)
-        dist.barrier()
-        t0 = time.perf_counter()
-        run(steps)
-        torch.cuda.synchronize(ss.dev)
-        t = time.perf_counter() - t0
-        dist.barrier()
-        res[key] = _max_over_ranks(t, ss.dev) / steps
+    elif capture_fault_injected():  # (the CPU rehearsal captures nothing: the agreement alone)
+        print(f"bench: injected capture failure (BENCH_INJECT_CAPTURE_FAIL) on rank {os.environ.get('RANK', '0')}",
+              file=sys.stderr, flush=True)
+        ok = False
+    ok = agree_all(ok, ss.dev)
+    res = {"graph": ok and not ss.cpu, "capture_agreed": ok}
+    for key in eager:
+        if res["graph"]:
+            res[key] = timed_rotation(built[key], ss.dev, True) / steps
+        else:
+            res[key] = time_eager(eager[key], steps, warmup, ss.dev, ss.cpu)
+    del built
     return res
 
 
-def time_unsharded(fmt, M, K, N, steps, warmup, dev, cpu):
+def time_unsharded(fmt, M, K, N, steps, warmup, dev, cpu, graph=True):
     """The whole matrix on this one device (rank 0's 1-GPU reference for speedup_vs_1gpu): the same
-    ShardStep compute as the ranks run, with world 1 (no process-group calls)."""
-    ss = ShardStep(fmt, M, K, N, dev, 1, 0, cpu=cpu)
-    if cpu:
+    ShardStep compute as the ranks run, with world 1 (no process-group calls), timed the way the
+    ranks' keys were (graph: the rotation's graphs; else eager)."""
+    ss = ShardStep(fmt, M, K, N, dev, 1, 0, cpu=cpu, steps=steps)
+    if cpu or not graph:
         ss.cpu_compute(max(1, warmup))
+        if not cpu:
+            torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         ss.cpu_compute(steps)
-        return (time.perf_counter() - t0) / steps
-    g = ss.graph_compute(steps)
-    g.replay()
-    t = min(timed_replay(g, dev) for _ in range(3)) / steps
-    del ss, g
-    torch.cuda.empty_cache()
+        if not cpu:
+            torch.cuda.synchronize(dev)
+        t = (time.perf_counter() - t0) / steps
+    else:
+        gs = [ss.graph_compute(p) for p in ss.plans]
+        t = timed_rotation(gs, dev) / steps
+        del gs
+    del ss
+    if not cpu:
+        torch.cuda.empty_cache()
     return t
 
 
@@ -590,9 +665,10 @@ def bench_sharded(fmt, Mg, K, N, steps, warmup, dev, world, rank, cpu, unsharded
     dependent chain (per chunk count; the best is `e2e_chain`), and -- rank 0, the other ranks
     waiting -- the unsharded matrix on one device for speedup_vs_1gpu."""
     import torch.distributed as dist
-    ss = ShardStep(fmt, Mg, K, N, dev, world, rank, cpu=cpu)
+    ss = ShardStep(fmt, Mg, K, N, dev, world, rank, cpu=cpu, steps=steps)
     t = time_sharded(ss, steps, warmup)
     rows_per_rank, ncopies = ss.R, ss.ncopies
+    rotated = rotated_bytes(max(1, ss.rows * ss.rb), ss.plans)
     del ss
     if not cpu:
         torch.cuda.empty_cache()
@@ -600,7 +676,7 @@ def bench_sharded(fmt, Mg, K, N, steps, warmup, dev, world, rank, cpu, unsharded
     if unsharded:
         dist.barrier()
         if rank == 0:
-            t1 = time_unsharded(fmt, Mg, K, N, steps, warmup, dev, cpu)
+            t1 = time_unsharded(fmt, Mg, K, N, steps, warmup, dev, cpu, graph=t["graph"])
         dist.barrier()
     chains = {C: t[f"chain{C}"] for C in ShardStep.CHUNKS}
     best = min(chains, key=chains.get)
@@ -609,7 +685,7 @@ def bench_sharded(fmt, Mg, K, N, steps, warmup, dev, world, rank, cpu, unsharded
     wbytes = Mg * (K // qk) * nbytes
     ms = lambda x: round(x * 1e3, 6)  # noqa: E731
     out = {"config": f"{fmt}_{Mg}x{K}_m{N}", "fmt": fmt, "N_out_global": Mg, "K": K, "M_tok": N, "ranks": world,
-           "rows_per_rank": rows_per_rank, "weight_copies": ncopies,
+           "rows_per_rank": rows_per_rank, "weight_copies": ncopies, "weight_bytes_rotated_per_rank": rotated,
            "compute_ms_per_step": ms(t["compute"]), "e2e_overlap_ms_per_step": ms(t["overlap"]),
            "e2e_chain_ms_per_step": ms(chains[best]), "e2e_chain_chunks": best,
            "e2e_chain_ms_by_chunks": {str(C): ms(v) for C, v in chains.items()},
@@ -618,7 +694,9 @@ def bench_sharded(fmt, Mg, K, N, steps, warmup, dev, world, rank, cpu, unsharded
            "e2e_chain_tflops": round(flops / chains[best] / 1e12, 3),
            "e2e_chain_weight_GBps": round(wbytes / chains[best] / 1e9, 1),
            "collective": f"all_gather_into_tensor per row chunk (backend {dist_backend()}) + assemble copy",
-           "timing": "eager" if cpu or t.get("graph") is False else "hipGraph replay"}
+           "timing": ("hipGraph replay (median of the rotation's graphs)" if t["graph"] else
+                      "eager" + ("" if t["capture_agreed"] else " (a graph capture failed on some rank; every rank "
+                                                                    "and the 1-GPU reference timed eagerly)"))}
     if t1 is not None:
         out["unsharded_1dev_ms_per_step"] = ms(t1)
         out["speedup_vs_1gpu"] = {"compute": round(t1 / t["compute"], 3), "e2e_overlap": round(t1 / t["overlap"], 3),
@@ -637,29 +715,25 @@ def bench_config(name, steps, warmup, dev):
     and the dominant kernel for the roofline."""
     fmt, M, K, N = CONFIGS[name]
     r = Runner(fmt, M, K, N, dev, steps)
-    gw = r.capture(r.step, max(1, warmup))
+    gw = r.capture(r.step, [i % r.ncopies for i in range(max(1, warmup))])
     gw.replay()
     torch.cuda.synchronize(dev)
-    g = r.capture(r.step, steps)
-    g.replay()  # first replay pays lazy init
-    t = min(timed_replay(g, dev) for _ in range(3))
+    del gw
+    per_step = r.timed(r.step)
     # dominant kernel: decode (N <= 4) -- the step IS one launch (fused quantizer + weight
     # stream), so its time is the step's; GEMM -- the MMQ call alone (gemm_kernel [+ split-K
-    # reduce]) with the activations prepared once, K launches in a graph
+    # reduce]) with the activations prepared once, K launches per graph, the same rotation
     if N <= 4:
-        t_k = t / steps
+        t_k = per_step
         kname = "stream_decode_kernel (fused q8_1 + decode)"
     else:
         r.prepare()
-        gk = r.capture(r.kernel, steps)
-        gk.replay()
-        t_k = min(timed_replay(gk, dev) for _ in range(3)) / steps
+        t_k = r.timed(r.kernel)
         # (the library's routing, csrc/gq_capi.hip use_wgemm: Q4_K from 33 tokens on takes the
         # weight-register GEMM)
         kname = ("wgemm_kernel (+ wreduce_kernel when split-K)" if fmt == "q4_k" and N >= 33
                  else "gemm_kernel (+ gemm_reduce_kernel when split-K)")
     wbytes, alg_bytes, flops = model(fmt, M, K, N)
-    per_step = t / steps
     out = {
         "config": name, "fmt": fmt, "N_out": M, "K": K, "M_tok": N,
         "ms_per_step": per_step * 1e3,
@@ -667,6 +741,8 @@ def bench_config(name, steps, warmup, dev):
         "weight_GBps": wbytes / per_step / 1e9,
         "roofline": dict(roofline(fmt, M, K, N, t_k, load_traffic(name)), kernel=kname),
         "weight_copies": r.ncopies,
+        "weight_bytes_rotated": r.rotated,
+        "graphs_rotated": len(r.plans),
     }
     del r
     torch.cuda.empty_cache()
@@ -685,7 +761,7 @@ def bench_layer(Ns, acts, steps, warmup, dev, fuse=True, grouped="auto"):
     types = q4_k_m_layer_types(0, 32)
     one = {n: device_random_blocks(types[n], M, K, dev, seed=i) for i, (n, (M, K)) in enumerate(LLAMA_LAYER_SHAPES.items())}
     layer_bytes = sum(t.numel() for t in one.values())
-    ncopies = max(2, math.ceil(ROTATE_BYTES / layer_bytes))
+    ncopies, plans = rotation_plan(layer_bytes, steps)
     lins = [{n: GGUFLinear(types[n], one[n] if c == 0 else one[n].clone(), *LLAMA_LAYER_SHAPES[n])
              for n in LLAMA_LAYER_SHAPES} for c in range(ncopies)]
     res = []
@@ -710,21 +786,24 @@ def bench_layer(Ns, acts, steps, warmup, dev, fuse=True, grouped="auto"):
                 layers[0].forward(x, h, out=outs)
             torch.cuda.current_stream(dev).wait_stream(s)
             torch.cuda.synchronize(dev)
-            with torch.cuda.graph(gr):
-                for i in range(steps):
-                    layers[i % ncopies].forward(x, h, out=outs)
-            gr.replay()
-            t = min(timed_replay(gr, dev) for _ in range(3)) / steps
+            grs = []
+            for p in plans:
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr):
+                    for c in p:
+                        layers[c].forward(x, h, out=outs)
+                grs.append(gr)
+            t = timed_rotation(grs, dev) / steps
             res.append({"config": f"q4_k_m_llama7b_layer_m{N}", "act": act, "fused": fuse,
                         "grouped": act == "q8_1" and N <= GROUPED_MAX_TOKENS[grouped],
                         "fmt": "q4_k+q6_k", "M_tok": N,
                         "us_per_step": round(t * 1e6, 2), "tflops": round(flops / t / 1e12, 3),
                         "weight_GBps": round(layer_bytes / t / 1e9, 1)})
-            del gr
+            del grs
     del lins, layers
     torch.cuda.empty_cache()
     return {"config": "q4_k_m_llama7b_layer_msweep", "types": types, "weight_bytes": layer_bytes,
-            "weight_copies": ncopies, "points": res}
+            "weight_copies": ncopies, "weight_bytes_rotated": rotated_bytes(layer_bytes, plans), "points": res}
 
 
 def bench_fp8(names, steps, warmup, dev):
@@ -733,15 +812,14 @@ def bench_fp8(names, steps, warmup, dev):
     for name in names:
         fmt, M, K, N = CONFIGS[name]
         r = Runner(fmt, M, K, N, dev, steps, act="fp8")
-        gw = r.capture(r.step, max(1, warmup))
+        gw = r.capture(r.step, [i % r.ncopies for i in range(max(1, warmup))])
         gw.replay()
-        g = r.capture(r.step, steps)
-        g.replay()
-        t = min(timed_replay(g, dev) for _ in range(3)) / steps
+        t = r.timed(r.step)
         wbytes, _, flops = model(fmt, M, K, N)
         out.append({"config": name + "_fp8act", "act": "fp8", "us_per_step": round(t * 1e6, 2),
-                    "tflops": round(flops / t / 1e12, 3), "weight_GBps": round(wbytes / t / 1e9, 1)})
-        del r, g, gw
+                    "tflops": round(flops / t / 1e12, 3), "weight_GBps": round(wbytes / t / 1e9, 1),
+                    "weight_bytes_rotated": r.rotated})
+        del r, gw
         torch.cuda.empty_cache()
     return out
 
@@ -751,15 +829,14 @@ def bench_msweep(steps, warmup, dev, fmt="q4_k", M=4096, K=4096):
     res = []
     for N in (1, 2, 4, 8, 16, 32, 64, 128, 256, 512):
         r = Runner(fmt, M, K, N, dev, steps)
-        gw = r.capture(r.step, max(1, warmup))
+        gw = r.capture(r.step, [i % r.ncopies for i in range(max(1, warmup))])
         gw.replay()
-        gs = r.capture(r.step, steps)
-        gs.replay()
-        t = min(timed_replay(gs, dev) for _ in range(3)) / steps
+        t = r.timed(r.step)
         wbytes, alg_bytes, flops = model(fmt, M, K, N)
         res.append({"M_tok": N, "us_per_step": round(t * 1e6, 2), "tflops": round(flops / t / 1e12, 3),
-                    "weight_GBps": round(wbytes / t / 1e9, 1), "alg_GBps": round(alg_bytes / t / 1e9, 1)})
-        del r, gw, gs
+                    "weight_GBps": round(wbytes / t / 1e9, 1), "alg_GBps": round(alg_bytes / t / 1e9, 1),
+                    "weight_bytes_rotated": r.rotated})
+        del r, gw
         torch.cuda.empty_cache()
     return {"config": f"{fmt}_{M}x{K}_msweep", "points": res}
 
@@ -922,7 +999,9 @@ def main():
                  "q8_1 int8 activations x GGUF int codes on v_dot4_i32_i8, fp32 block scaling",
         "data": "synthetic (random packed blocks, N(0,1) fp16 activations)",
         "config": {"workload": name, "gguf_type": fmt, "N_out": M, "K": K, "M_tok": N, "parallelism": "single",
-                   "weight_copies_rotated": head["weight_copies"]},
+                   "weight_copies": head["weight_copies"], "weight_bytes_rotated": head["weight_bytes_rotated"],
+                   "graphs_rotated": head["graphs_rotated"],
+                   "timing": "median of round-robin replays of the rotation's graphs, K steps each"},
         "weight_GBps": round(head["weight_GBps"], 1),
         "roofline": head["roofline"],
         "cpu_baseline": cpu_b,

@@ -35,6 +35,7 @@ struct Tuning {
     int skinny = -1;                          // GQ_SKINNY: 5..32-token kernel (-1 auto, 0 off, 1 every 1..32)
     int skinny_rg = 0;                        // GQ_SKINNY_RG: fragments per workgroup, 1..4 (0: auto)
     int skinny_d = 0;                         // GQ_SKINNY_D: super-blocks in the register ring, 2..4 (0: auto)
+    int cus = 0;                              // GQ_CUS: compute units to plan for (0: the device's count)
     int ablate = 0;                           // GQ_ABLATE (GQ_ABLATION diagnostic builds only)
 };
 const Tuning &tuning();
@@ -43,6 +44,9 @@ const Tuning &tuning();
 // value out of range.  reset: back to the environment's values.
 int set_tuning(const char *key, long long value);
 void reset_tuning();
+// compute units of the current device (hipDeviceAttributeMultiprocessorCount, queried once per
+// device), or the GQ_CUS override: every "one round of the chip" plan sizes its grid by it
+int num_cus();
 
 enum ActMode : int { ACT_AOS = 0, ACT_SOA = 1, ACT_DEQ = 2, ACT_I8 = 3, ACT_F8 = 4, ACT_F8DEQ = 5 };
 // Activation form the MFMA GEMM reads (mmq_gemm.hip): fp16 x~ (q8_1's, or the fp8 variant's

@@ -88,6 +88,9 @@ bool parse_key(Tuning &t, const char *key, long long v)
     } else if (k == "GQ_SKINNY_D") {
         if (!in({0, 2, 3, 4})) return false;
         t.skinny_d = (int)v;
+    } else if (k == "GQ_CUS") {
+        if (v < 0 || v > 1024) return false;
+        t.cus = (int)v;
     } else if (k == "GQ_ABLATE") t.ablate = (int)v;
     else return false;
     return true;
@@ -101,7 +104,7 @@ void tuning_from_env(Tuning &t)
                                        "GQ_GEMM_NB", "GQ_GEMM_RG", "GQ_GEMM_LOADERS", "GQ_GEMM_SPLITS",
                                        "GQ_GEMM_PARTIAL", "GQ_GEMM_FUSED_REDUCE", "GQ_GEMV_CAP", "GQ_GEMV_R",
                                        "GQ_WGEMM", "GQ_WGEMM_RG", "GQ_WGEMM_NB", "GQ_WGEMM_SPLITS", "GQ_WGEMM_WD",
-                                       "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D", "GQ_ABLATE"};
+                                       "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D", "GQ_CUS", "GQ_ABLATE"};
     for (const char *k : keys) {
         const char *e = getenv(k); // the only getenv of the library: once per process
         if (!e || !*e) continue;
@@ -132,7 +135,23 @@ int set_tuning(const char *key, long long value)
 void reset_tuning()
 {
     tuning();
-    tuning_from_env(g_tuning);
+    Tuning t;
+    tuning_from_env(t); // built aside and published by one assignment, as set_tuning does
+    g_tuning = t;
+}
+
+int num_cus()
+{
+    if (tuning().cus > 0) return tuning().cus; // test override (GQ_CUS)
+    static int cached[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (cached[dev] <= 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cached[dev] = n;
+    }
+    return cached[dev];
 }
 
 } // namespace gq

@@ -641,6 +641,14 @@ size_t act_lds(int fmt, int nt, int64_t K, bool fp8 = false)
     return (size_t)nt * kp + (size_t)nt * nb * 4 * (fmt == Q8_0 ? 1 : (fmt == Q4_K ? 2 : 3));
 }
 
+// the largest cached-chunk count ITC instantiated for (format, token tile)
+int itc_max(int fmt, int nt)
+{
+    if (nt == 1) return fmt == Q6_K ? 4 : 7;
+    if (nt == 2) return fmt == Q6_K ? 1 : 4;
+    return 1;
+}
+
 int64_t row_bytes(int fmt, int64_t K)
 {
     return fmt == Q8_0 ? K / 32 * 34 : (fmt == Q4_K ? K / 256 * 144 : K / 256 * 210);
@@ -678,7 +686,7 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p, int wgs = 0)
     const int64_t cpr = upr / upc_of(fmt, p.nt); // lane chunks per row
     const int64_t cap = img ? NI * 1024 : NI * 1024 - 16;
     const int per_cu = (int)(LDS_CAP / p.lds) > 0 ? (int)(LDS_CAP / p.lds) : 1;
-    int64_t W = (int64_t)256 * per_cu * DW; // waves the chip holds (or the granted workgroups')
+    int64_t W = (int64_t)num_cus() * per_cu * DW; // waves the chip holds (or the granted workgroups')
     if (wgs > 0) W = (int64_t)wgs * DW;
     DecodeGeom &g = p.geo;
     if (RB <= cap) {
@@ -708,6 +716,9 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p, int wgs = 0)
     // units and 1 token (K <= 28672: the 70B ffn_down rows) -- no spills (kernel-resource-usage)
     const int64_t itc = (cpr + (1 << g.lp2) - 1) >> g.lp2, units = itc * (upr / cpr);
     p.itc = ((p.nt <= 2 && units <= (fmt == Q6_K ? 2 : 4)) || (p.nt == 1 && units <= 8)) ? (int)itc : 0;
+    // only the instantiated chunk counts (launch_f, stream_decode_grouped_kernel): one token
+    // 0..7 (Q6_K 0..4), two 0..4 (Q6_K 0..1), four 0..1 -- e.g. K = 29568 at one token gives 8
+    if (p.itc > itc_max(fmt, p.nt)) p.itc = 0;
     // four tokens, one unit per lane (K <= 4096): cached too (Q6_K 14336x4096 x4 27.7 -> 20.7 us,
     // profiles/r02/decode_nt4_cache_ab.txt; GQ_DECODE_NT4_CACHE=0: off)
     if (p.nt == 4 && units == 1 && tuning().decode_nt4_cache)
@@ -794,8 +805,9 @@ hipError_t launch_f(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *
         case 18: return GQ_LT(2, 2);
         case 19: return GQ_LT(2, 3);
         case 20: return GQ_LT(2, 4);
+        case 32: return GQ_LT(4, 0);
         case 33: return GQ_LT(4, 1);
-        default: return GQ_LT(4, 0);
+        default: return hipErrorInvalidValue; // (pick() caps itc at itc_max)
         }
     }
 #undef GQ_LT
@@ -973,7 +985,7 @@ hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipS
         // 258 of 256), doubling the launch (44.5 -> 30.1 us at one token).  Weighting the bytes by
         // each format's large-matrix streaming rate measured 1-5% slower (grouped_alloc_ab.log).
         const int per_cu = (int)(LDS_CAP / lds) > 0 ? (int)(LDS_CAP / lds) : 1;
-        const int budget = 256 * per_cu;
+        const int budget = num_cus() * per_cu;
         int wg[kMaxGroup], used = 0;
         double frac[kMaxGroup];
         for (int j = 0; j < np; ++j) {
@@ -1016,6 +1028,7 @@ hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipS
             q.M = (int)items[i].M;
             q.K = (int)items[i].K;
             q.geo = p.geo;
+            if (p.itc > itc_max(items[i].fmt, nt) || (fp8 && p.itc != 0)) return hipErrorInvalidValue; // no kernel case
             q.code = items[i].fmt * 16 + p.itc + (p.img ? 8 : 0);
             q.block0 = blocks;
             q.gx = p.grid;

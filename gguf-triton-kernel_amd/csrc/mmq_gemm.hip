@@ -1175,7 +1175,7 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, int act)
     const int64_t tiles = ((M + bm - 1) / bm) * ((N + 16 * p.nb - 1) / (16 * p.nb));
     // one workgroup per CU (LDS-bound): the largest split that keeps tiles * S <= 256 CUs, so no
     // second wave of workgroups (258 workgroups ran 25% slower than 172 at 11008 x 4096 x 128)
-    const int64_t cus = 256;
+    const int64_t cus = num_cus();
     int64_t S = tiles >= cus ? 1 : cus / tiles;
     if (tuning().gemm_splits > 0) S = tuning().gemm_splits; // tuning / test override
     const int64_t max_split = nws / 2 > 0 ? nws / 2 : 1;            // >= 2 super-blocks per split

@@ -48,7 +48,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 constexpr int SABL = GQ_SKINNY_ABL;
 
 constexpr int SW = 8;     // waves per workgroup, each a contiguous K range of the workgroup's rows
-constexpr int kCUs = 256; // MI355X: 256 CUs
+// compute units: num_cus() (the device attribute, queried once per device)
 
 template <int F> constexpr int w_loads() { return F == Q4_K ? 3 : (F == Q6_K ? 10 : 5); } // per fragment
 
@@ -193,7 +193,7 @@ hipError_t launch_cfg(const uint8_t *A, const uint16_t *X, uint16_t *C, int64_t 
     // persistent: one workgroup per CU (the 128 KiB activation ring fills its LDS), each a
     // contiguous range of units
     const int64_t nunits = (M + 16 * RG - 1) / (16 * RG);
-    const unsigned grid = (unsigned)(nunits < kCUs ? nunits : kCUs);
+    const unsigned grid = (unsigned)(nunits < num_cus() ? nunits : num_cus());
     skinny_kernel<F, NT, RG, D><<<dim3(grid), dim3(64 * SW), 0, s>>>(A, X, C, (int)M, (int)N, (int)K, (int)ldc,
                                                                      (int)nunits);
     return hipGetLastError();
@@ -247,7 +247,7 @@ SkinnyPlan plan_skinny(int fmt, int64_t M, int64_t N, int64_t K, int rg, int d)
     double best = 1e300;
     for (int r = 1; r <= rmax; ++r) {
         const int64_t units = (frags + r - 1) / r;
-        const double cost = (double)((units + kCUs - 1) / kCUs) * (r + xr);
+        const double cost = (double)((units + num_cus() - 1) / num_cus()) * (r + xr);
         if (cost < best - 1e-9) {
             best = cost;
             p.rg = r;

@@ -435,7 +435,8 @@ WGemmPlan plan_wgemm(int fmt, int64_t M, int64_t N, int64_t K, int rg, int nb, i
     p.tiles_m = (int)((M + bm - 1) / bm);
     p.tiles_n = (int)((N + bn - 1) / bn);
     const int64_t nsb = K / 256, tiles = (int64_t)p.tiles_m * p.tiles_n;
-    int64_t S = splits > 0 ? splits : (tiles >= 256 ? 1 : 256 / tiles);
+    const int64_t cus = num_cus();
+    int64_t S = splits > 0 ? splits : (tiles >= cus ? 1 : cus / tiles);
     if (S > nsb) S = nsb;
     if (S < 1) S = 1;
     const int64_t sps = (nsb + S - 1) / S;

@@ -182,3 +182,46 @@ def test_bench_world_size_mismatch_fails():
     r = _run_bench(["--gpus", "2", "--steps", "2"], {"WORLD_SIZE": "1", "BENCH_REHEARSAL": "1"}, timeout=120)
     assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
     assert "world size 1 != --gpus 2" in r.stderr
+
+
+def test_bench_capture_failure_is_agreed_by_every_rank():
+    """A graph capture that fails on ONE rank (injected on rank 1: BENCH_INJECT_CAPTURE_FAIL=1)
+    switches EVERY rank, and the 1-GPU reference, to eager timing: rank 0 never failed itself,
+    yet its line says the capture failed on some rank; both ranks exit 0 (no rank replays graphs
+    holding collectives while another runs them eagerly)."""
+    r = _run_bench(["--gpus", "2", "--steps", "2", "--warmup", "1"],
+                   {"BENCH_REHEARSAL": "1", "BENCH_INJECT_CAPTURE_FAIL": "1"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    for p in d["strong"] + [d["weak"]]:
+        assert "capture failed on some rank" in p["timing"], p["timing"]
+    assert "injected capture failure" in r.stderr
+
+
+def test_bench_rotation_touches_a_gib_at_driver_steps():
+    """The driver runs `bench.py --steps 20`: every single-GPU config, the Q4_K_M layer and the
+    row-sharded shards still cycle over >= 1 GiB of distinct weights (bench.rotation_plan: several
+    20-step graphs replayed round robin), each graph exactly `steps` launches."""
+    sys.path.insert(0, ROOT)
+    import bench
+    steps = 20
+    for name, (fmt, M, K, N) in bench.CONFIGS.items():
+        wbytes, _, _ = bench.model(fmt, M, K, N)
+        ncopies, plans = bench.rotation_plan(wbytes, steps)
+        assert all(len(p) == steps for p in plans), name
+        assert bench.rotated_bytes(wbytes, plans) >= 1 << 30, name
+        assert len({c for p in plans for c in p}) == ncopies, name
+    layer_bytes = 129785856
+    _, plans = bench.rotation_plan(layer_bytes, steps)
+    assert bench.rotated_bytes(layer_bytes, plans) >= 1 << 30
+    for world in (1, 2, 4, 8):  # the strong-scaling shard per rank
+        rb = 8192 // 256 * 210
+        rows = -(-28672 // world)
+        _, plans = bench.rotation_plan(rows * rb, steps)
+        assert bench.rotated_bytes(rows * rb, plans) >= 1 << 30
+    # and the Runner really takes its copies from the plan
+    import inspect
+    src = inspect.getsource(bench.Runner.__init__)
+    assert "rotation_plan(self.wbytes, steps)" in src

@@ -242,3 +242,28 @@ def test_grouped_llama_layer_fp8(N, layer):
         sub = np.concatenate([raw[n][r * rb:(r + 1) * rb] for r in rows])
         ideal = O.mmq_fp8_ideal(types[n], sub, h if K == 11008 else x, len(rows), N, K)
         assert O.max_rel_err(C.cpu().numpy()[:, rows], ideal) <= 4e-3, n
+
+
+def test_q8_0_long_k_one_token_grouped_and_solo():
+    """Q8_0 at one token with 28672 < K <= 32768 (K = 29568, Qwen2-72B's ffn_down): the decode
+    pick() once chose a cached-chunk count (8) that no kernel instantiates -- the grouped launch
+    wrote nothing and returned success, the single launch ran the 2-token kernel.  Both forms
+    now match the oracle on sampled rows, and each other bit for bit."""
+    import kernels._lib as kl
+    dev = _dev()
+    M, K, N = 512, 29568, 1
+    raw = random_blocks("q8_0", M, K, seed=11)
+    qA = torch.from_numpy(raw.view(np.int8)).to(dev)
+    x = random_activations(N, K, seed=12)
+    xt = torch.from_numpy(x).to(dev)
+    solo = kl.mmq(kl.GQ_Q8_0, qA, xt, M, N, K)
+    out = torch.full((N, M), float("nan"), dtype=torch.float16, device=dev)
+    res = kl.mmq_grouped([(kl.GQ_Q8_0, qA, xt, M, K, out)], N)
+    torch.cuda.synchronize()
+    rows = np.arange(0, M, 37)
+    rb = raw.size // M
+    sub = np.concatenate([raw[r * rb:(r + 1) * rb] for r in rows])
+    ideal = O.mmq_from_fp16("q8_0", sub, x, len(rows), N, K, O.IDEAL)
+    assert O.max_rel_err(solo.cpu().numpy()[:, rows], ideal) <= TIGHT_DEC
+    if res is not None:  # grouped form taken: it must have written every output
+        assert torch.equal(out.view(torch.int16), solo.view(torch.int16))
