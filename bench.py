@@ -852,9 +852,10 @@ def compact(e):
 
 
 def eager_call_us(dev, n=1000):
-    """Median wall time of n eager drop-in calls kernels.mmq_q4_k.mmq_q4_k(A, B, 4096, 1, 4096)
-    (the reference's callers' form, /root/reference/test/test_mmq_q4_k.py:34): Python + ctypes
-    + output allocation + launch, each call synchronized."""
+    """The drop-in called eagerly, kernels.mmq_q4_k.mmq_q4_k(A, B, 4096, 1, 4096) (the reference's
+    callers' form, /root/reference/test/test_mmq_q4_k.py:34): Python + ctypes + output allocation
+    + launch.  -> (median wall time of n calls each synchronized, host time per call of n
+    back-to-back calls with one synchronize at the end)."""
     from kernels.mmq_q4_k import mmq_q4_k
     A = device_random_blocks("q4_k", 4096, 4096, dev, seed=11)
     B = torch.randn(1, 4096, device=dev).to(torch.float16)
@@ -867,7 +868,12 @@ def eager_call_us(dev, n=1000):
         mmq_q4_k(A, B, 4096, 1, 4096)
         torch.cuda.synchronize(dev)
         ts.append(time.perf_counter() - t0)
-    return round(float(np.median(ts)) * 1e6, 2)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        mmq_q4_k(A, B, 4096, 1, 4096)
+    torch.cuda.synchronize(dev)
+    host = (time.perf_counter() - t0) / n
+    return round(float(np.median(ts)) * 1e6, 2), round(host * 1e6, 2)
 
 
 def strong_line(args, world, rank, dev, cpu):
@@ -981,7 +987,7 @@ def main():
         sweep.append(bench_msweep(sweep_steps, args.warmup, dev))
         sweep.extend(bench_fp8(("q8_0_4096x4096_m128", "q4_k_11008x4096_m128", "q6_k_28672x8192_m128",
                                 "q4_k_4096x4096_m1"), sweep_steps, args.warmup, dev))
-    eager = eager_call_us(dev)
+    eager, eager_host = eager_call_us(dev)
     cpu_b, cpu_var = (None, None) if args.no_cpu else cpu_baseline(fmt, M, K, N)
     line = {
         "metric": "effective fp16 TFLOPS (+ quant-weight GB/s) per GGUF type",
@@ -1007,6 +1013,9 @@ def main():
         "cpu_baseline": cpu_b,
         "eager_us": eager,
         "eager_us_is": "median of 1000 eager kernels.mmq_q4_k.mmq_q4_k(A, B, 4096, 1, 4096) calls, each synchronized",
+        "eager_host_us": eager_host,
+        "eager_host_us_is": "the same call 1000 times back to back, one synchronize at the end, / 1000 (the "
+                            "per-call host cost when the kernel is shorter)",
     }
     if cpu_var:
         line["cpu_baseline_variants"] = cpu_var

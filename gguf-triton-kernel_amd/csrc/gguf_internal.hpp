@@ -35,6 +35,8 @@ struct Tuning {
     int skinny = -1;                          // GQ_SKINNY: 5..32-token kernel (-1 auto, 0 off, 1 every 1..32)
     int skinny_rg = 0;                        // GQ_SKINNY_RG: fragments per workgroup, 1..4 (0: auto)
     int skinny_d = 0;                         // GQ_SKINNY_D: super-blocks in the register ring, 2..4 (0: auto)
+    int rgemm = -1;                           // GQ_RGEMM: resident-split GEMM -1 auto / 0 off / 1 wherever it applies
+    int rgemm_spol = 0;                       // GQ_RGEMM_SPOL: its partial stores' cache policy 0 / 2 (nt) / 16 (sc1)
     int cus = 0;                              // GQ_CUS: compute units to plan for (0: the device's count)
     int ablate = 0;                           // GQ_ABLATE (GQ_ABLATION diagnostic builds only)
 };
@@ -121,6 +123,24 @@ bool gemm_supported(int fmt, int64_t K);
 GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, int act = AF_F16);
 hipError_t launch_gemm(int fmt, const uint8_t *A, const GemmAct &x, uint16_t *C, float *partials,
                        const GemmPlan &plan, int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
+
+// The split-K sum of the fp16 partials gemm_kernel (and rgemm_kernel) write: tiles of 16*8*rg
+// rows x 16*nb tokens, S splits (mmq_gemm.hip gemm_reduce_f16_kernel).
+hipError_t launch_gemm_reduce_f16(int nb, int rg, const uint16_t *P, uint16_t *C, int64_t M, int64_t N, int64_t ldc,
+                                  int S, int tiles_x, int tiles_y, hipStream_t s = nullptr);
+
+// Resident-split GEMM (mmq_rgemm.hip): 256 rows x 16*nb tokens x one super-block per workgroup,
+// the split's weights and activations loaded once into LDS; split-K over every super-block
+// (fp16 partials + launch_gemm_reduce_f16).  aq: 0 prepared x~ (X = [N][K] DEQ / F8DEQ form),
+// 1 raw fp16 activations (X rows ldx apart) q8_1-quantized in-kernel, 2 raw, fp8-quantized.
+struct RGemmPlan {
+    bool ok = false;
+    int nb = 8, tiles_m = 0, tiles_n = 0, splits = 1;
+    size_t partial_bytes = 0;
+};
+RGemmPlan plan_rgemm(int64_t M, int64_t N, int64_t K);
+hipError_t launch_rgemm(int fmt, int aq, const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, void *partials,
+                        const RGemmPlan &p, int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
 
 // Weight-register GEMM (mmq_wgemm.hip): weights streamed into VGPRs a super-block ahead,
 // activations (fp16 x~, act_quant DEQ form) register-staged into a two-slot LDS ring; 128*rg

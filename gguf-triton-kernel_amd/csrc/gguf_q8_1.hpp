@@ -140,6 +140,46 @@ __device__ __forceinline__ Q81Quad q8_1_quad(u32x4 w)
     return r;
 }
 
+// The DEQ form's x~ = fp16(d * q) of one 32-element block held by an aligned group of 4 lanes
+// (8 elements each), bit-identical to q8_1_quad + the fp32 product act_quant.hip rounds (the
+// same amax, d, fp16-exact quotient and clamp), with the per-element tail on packed fp16: the
+// quotient rounded to fp16 by one pack, rint as (q + 1536) - 1536 (|q| < 512: the sum's ulp is
+// 1, IEEE round-to-nearest-even = rintf), the clamp by packed min/max, and fp16(d * q) by one
+// packed multiply (the exact product rounded once, as the fp32 product rounded to fp16).
+// Returns the pairs (x0,x2), (x1,x3), (x4,x6), (x5,x7): the (0,2,1,3) 4-group order.
+__device__ __forceinline__ u32x4 deq_quad(u32x4 w)
+{
+    typedef _Float16 h2t __attribute__((ext_vector_type(2)));
+    const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
+    float x[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        x[2 * i] = h2f(wd[i] & 0xffff);
+        x[2 * i + 1] = h2f(wd[i] >> 16);
+    }
+    float amax = fmaxf(fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))),
+                       fmaxf(fmaxf(fabsf(x[4]), fabsf(x[5])), fmaxf(fabsf(x[6]), fabsf(x[7]))));
+    amax = fmaxf(amax, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax), 0xb1, 0xf, 0xf, false)));
+    amax = fmaxf(amax, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax), 0x4e, 0xf, 0xf, false)));
+    const uint16_t dbits = amax != 0.f ? f2h_bits(q81_div(amax, 127.0f, 1.0f / 127.0f)) : (uint16_t)0;
+    const float d = h2f(dbits);
+    const float div = d == 0.f ? 1.0f : d;
+    const float rdiv = __builtin_amdgcn_rcpf(div);
+    const _Float16 dh = __builtin_bit_cast(_Float16, dbits);
+    const h2t dd = {dh, dh}, magic = {(_Float16)1536.f, (_Float16)1536.f};
+    const h2t lo = {(_Float16)-127.f, (_Float16)-127.f}, hi = {(_Float16)127.f, (_Float16)127.f};
+    const int ord[8] = {0, 2, 1, 3, 4, 6, 5, 7};
+    uint32_t o[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        h2t q = {(_Float16)q81_div(x[ord[2 * p]], div, rdiv), (_Float16)q81_div(x[ord[2 * p + 1]], div, rdiv)};
+        q = (q + magic) - magic;
+        q = __builtin_elementwise_min(__builtin_elementwise_max(q, lo), hi);
+        o[p] = __builtin_bit_cast(uint32_t, q * dd);
+    }
+    return (u32x4){o[0], o[1], o[2], o[3]};
+}
+
 // The fp8 variant's block quantization (act_quant.hip F8 / F8DEQ; include/gguf_mmq.h states the
 // rule) by an aligned group of 4 lanes, 8 elements each: X = 2^e with e the smallest integer
 // such that max|x| <= 448 * 2^e (X = 1 for an all-zero block), codes = e4m3(x / X) RNE, stored

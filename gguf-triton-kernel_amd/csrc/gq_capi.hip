@@ -88,6 +88,12 @@ bool parse_key(Tuning &t, const char *key, long long v)
     } else if (k == "GQ_SKINNY_D") {
         if (!in({0, 2, 3, 4})) return false;
         t.skinny_d = (int)v;
+    } else if (k == "GQ_RGEMM") {
+        if (!in({-1, 0, 1})) return false;
+        t.rgemm = (int)v;
+    } else if (k == "GQ_RGEMM_SPOL") {
+        if (!in({0, 2, 16})) return false;
+        t.rgemm_spol = (int)v;
     } else if (k == "GQ_CUS") {
         if (v < 0 || v > 1024) return false;
         t.cus = (int)v;
@@ -104,7 +110,7 @@ void tuning_from_env(Tuning &t)
                                        "GQ_GEMM_NB", "GQ_GEMM_RG", "GQ_GEMM_LOADERS", "GQ_GEMM_SPLITS",
                                        "GQ_GEMM_PARTIAL", "GQ_GEMM_FUSED_REDUCE", "GQ_GEMV_CAP", "GQ_GEMV_R",
                                        "GQ_WGEMM", "GQ_WGEMM_RG", "GQ_WGEMM_NB", "GQ_WGEMM_SPLITS", "GQ_WGEMM_WD",
-                                       "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D", "GQ_CUS", "GQ_ABLATE"};
+                                       "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D", "GQ_RGEMM", "GQ_RGEMM_SPOL", "GQ_CUS", "GQ_ABLATE"};
     for (const char *k : keys) {
         const char *e = getenv(k); // the only getenv of the library: once per process
         if (!e || !*e) continue;
@@ -226,6 +232,7 @@ int64_t gemm_toks_per_launch(int64_t N, int64_t K)
 // Q6_K stay on the LDS-DMA GEMM (4096^2 x128 Q8_0 20.8 vs 17.3; Q6_K 28672x8192 x128 115.6 vs
 // 111.9).
 constexpr int64_t kWgemmMinTokens = 33;
+constexpr int64_t kRgemmMinTokens = 17;
 bool use_wgemm(int t, int form, int64_t N)
 {
     const int w = gq::tuning().wgemm;
@@ -267,6 +274,26 @@ gq::WGemmPlan wgemm_plan(int t, int64_t M, int64_t N, int64_t K)
     // the two-fragment waves, 3 to 2 where it would spill
     p.wd = tu.wgemm_wd ? tu.wgemm_wd : (nb <= 4 ? 4 : 3);
     return p;
+}
+
+// Resident-split GEMM (mmq_rgemm.hip: 256 rows x <= 128 tokens x one super-block per workgroup,
+// the split's operands loaded once; profiles/r04/).  By default where its grid is one round of
+// the chip and at least half of it (a 4096-row matrix at K = 4096: 16 x 16 workgroups) and the
+// call needs no 2 GiB chunking; the q8_1 activations are quantized inside it (gq_mmq_ex) or read
+// prepared (gq_mmq_prepared).  With split-K over every super-block its partial sums differ from
+// gemm_kernel's (other splits), so a forced split factor (GQ_GEMM_SPLITS) keeps gemm_kernel.
+// GQ_RGEMM=1: wherever it applies (tests), 0: off.
+bool use_rgemm(int t, int form, int64_t M, int64_t N, int64_t K)
+{
+    const int rg = gq::tuning().rgemm;
+    if (rg == 0 || form != gq::AF_F16 || use_gemv(N, K) || use_blas(N, K) || K % 256 != 0) return false;
+    if (gemm_rows_per_launch(t, M, K) < M || gemm_toks_per_launch(N, K) < N) return false;
+    const gq::RGemmPlan p = gq::plan_rgemm(M, N, K);
+    if (!p.ok) return false;
+    if (rg == 1) return true;
+    if (gq::tuning().gemm_splits > 0 || N < kRgemmMinTokens) return false;
+    const int64_t grid = (int64_t)p.tiles_m * p.tiles_n * p.splits, cus = gq::num_cus();
+    return grid <= cus && 2 * grid >= cus;
 }
 
 bool use_i8(int t, int64_t N, int64_t K)
@@ -327,7 +354,7 @@ size_t ws_bytes(int t, int act, int64_t M, int64_t N, int64_t K)
         // (the kernel is chosen by the call's token count, so every chunk runs the same arithmetic)
         const bool sk = use_skinny(t, r.form, N, act), wg = use_wgemm(t, r.form, N);
         const int64_t mr = gemm_rows_per_launch(t, M, K), nt = sk ? N : gemm_toks_per_launch(N, K);
-        size_t p = 0;
+        size_t p = use_rgemm(t, r.form, M, N, K) ? gq::plan_rgemm(M, N, K).partial_bytes : 0;
         for (int64_t mc : {mr, M % mr})
             for (int64_t nc : {nt, N % nt})
                 if (mc > 0 && nc > 0) {
@@ -560,6 +587,12 @@ static int compute(gq_type t, int act, const void *A, void *workspace, size_t wo
         // (the kernel is chosen by the call's token count: every chunk runs the same arithmetic)
         // (<= 32 skinny tokens are never cut: their x~ is far below the guard, and the token
         // count sets the kernel's K split)
+        if (!use_skinny(t, r.form, N, act) && use_rgemm(t, r.form, M, N, K)) {
+            e = gq::launch_rgemm(t, 0, (const uint8_t *)A, c.xdeq, K, (uint16_t *)C, c.partials, gq::plan_rgemm(M, N, K),
+                                 M, N, K, ldc, s);
+            if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (rgemm): %s", hipGetErrorString(e));
+            return GQ_OK;
+        }
         const bool sk = use_skinny(t, r.form, N, act), wg = use_wgemm(t, r.form, N);
         const int64_t mr = gemm_rows_per_launch(t, M, K), nt = sk ? N : gemm_toks_per_launch(N, K);
         e = hipSuccess;
@@ -611,6 +644,17 @@ int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int6
         hipError_t e = gq::launch_decode_fused(t, (const uint8_t *)A, (const uint16_t *)B, ldb, (uint16_t *)C, M, N,
                                                K, ldc, (hipStream_t)stream, act == GQ_ACT_FP8_E4M3);
         if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (decode): %s", hipGetErrorString(e));
+        return GQ_OK;
+    }
+    if (!use_skinny(t, r.form, N, act) && use_rgemm(t, r.form, M, N, K) && ldb % 8 == 0 &&
+        ((uintptr_t)B & 15) == 0) {
+        // one launch (+ the split-K reduce): the activations quantized inside the GEMM (q8_1, or
+        // the fp8 variant's e4m3), bit-identical to the act_quant forms it would read
+        Carved c = carve(act, workspace, N, K);
+        hipError_t e = gq::launch_rgemm(t, act == GQ_ACT_FP8_E4M3 ? 2 : 1, (const uint8_t *)A, (const uint16_t *)B, ldb,
+                                        (uint16_t *)C, c.partials, gq::plan_rgemm(M, N, K), M, N, K, ldc,
+                                        (hipStream_t)stream);
+        if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (rgemm): %s", hipGetErrorString(e));
         return GQ_OK;
     }
     if (!r.gemv && !r.blas && act == GQ_ACT_Q8_1 && r.form == gq::AF_F16 && !use_wgemm(t, r.form, N) && !use_skinny(t, r.form, N) &&

@@ -1,0 +1,377 @@
+// mmq_rgemm.hip -- the resident-split MMQ GEMM: one workgroup per (256 weight rows, 16*NB tokens,
+// one super-block of K), every operand of the split in LDS at once.
+//
+// Why this shape (profiles/r04/probe_gemm_ingest.txt): with 16 weight rows per wave the activation
+// fragment reads of 8 waves are 128 KiB of LDS per 64-element sub-stage -- 512 LDS cycles, the same
+// as the sub-stage's 512 cycles of MFMA per SIMD -- and the waves, in lockstep behind each
+// sub-stage barrier, ran the two one after the other (reads + MFMA 0.585 us per sub-stage against
+// 0.266 for the MFMAs alone).  Here every wave multiplies 32 rows (two 16-row groups share each
+// activation fragment: half the LDS bytes per MFMA), and there is no ring and no barrier in the
+// multiply: the split's weights (one super-block per row: 256 x 272 / 144 / 240 B) and its
+// activations (16*NB tokens x 256 K as fp16 x~, 64 KiB at 128 tokens) are loaded once, then each
+// wave runs its 8 k-steps on its own.  A 4096-row matrix at K = 4096 is 16 row tiles x 16 splits
+// = 256 workgroups, one per CU.
+//
+// Loads: the weights by LDS-DMA first (HBM: the long pole), then the activations -- either the
+// prepared x~ (act_quant DEQ / F8DEQ form) by LDS-DMA, or (AQ) the raw fp16 activations into
+// registers, q8_1-quantized in-kernel (gguf_q8_1.hpp q8_1_quad: x~ = fp16(d*q), bit-identical to
+// act_quant's DEQ form; F8: the fp8 variant's f8_quad) and written to LDS while the weights are
+// in flight: no act_quant launch.
+//
+// Arithmetic = gemm_kernel's (mmq_gemm.hip) for the same rows: stage_frags dequantization, the
+// same x~, v_mfma_f32_16x16x32_f16 in the same (sub-stage, k-step) order into fp32 accumulators;
+// with one split per super-block the split-K partials are written in gemm_kernel's fp16 form and
+// summed by its reduce kernel (launch_gemm_reduce_f16).
+#include "gguf_blocks.hpp"
+#include "gguf_internal.hpp"
+#include "gguf_mfma.hpp"
+#include "gguf_q8_1.hpp"
+
+namespace gq {
+namespace {
+
+// diagnostic ablation builds only (make rabl RABL=n; never the product): 1 = no weight DMA,
+// 2 = no activation load, 4 = no multiply (fragments + MFMA), 8 = no epilogue stores
+#ifndef GQ_RGEMM_ABL
+#define GQ_RGEMM_ABL 0
+#endif
+constexpr int ABL = GQ_RGEMM_ABL;
+
+constexpr int RW = 8;                 // waves per workgroup (two per SIMD)
+constexpr int RRG = 2;                // 16-row groups per wave
+constexpr int RBM = 16 * RW * RRG;    // 256 rows per tile
+constexpr int LDS_CAP = 160 * 1024;
+
+// The split's weights as two half-super-block images (K elements 0..127 and 128..255 of every
+// row), so that the multiply of the first half runs while the second half is still in flight.
+// Per format: NPH 16-byte pieces per row and half (HRB bytes, a row stride that puts the 16 rows
+// of a fragment read on distinct banks), piece pc of half h read from super-block byte
+// hsrc<F>(h, pc):
+//   Q8_0  9 pieces from byte 128h (blocks 4h..4h+3 at image byte 8h..; 8 bytes of overlap)
+//   Q4_K  5 pieces: the 16-byte header, then qs bytes 64h..64h+63
+//   Q6_K  9 pieces: ql 64h.. (4), qh 128+32h.. (2), bytes 192..207 (scales), 194..209 (d at image
+//         byte 126), the last again (padding to 144 B: a 128-B stride is 2 bank sets)
+template <int F> struct HImg;
+template <> struct HImg<Q8_0> { static constexpr int NPH = 9; };
+template <> struct HImg<Q4_K> { static constexpr int NPH = 5; };
+template <> struct HImg<Q6_K> { static constexpr int NPH = 9; };
+template <int F> __device__ __forceinline__ uint32_t hsrc(int h, int pc)
+{
+    if constexpr (F == Q8_0) return 128u * h + 16u * pc;
+    if constexpr (F == Q4_K) return pc == 0 ? 0u : 16u + 64u * h + 16u * (pc - 1);
+    return pc < 4 ? 64u * h + 16u * pc : (pc < 6 ? 128u + 32u * h + 16u * (pc - 4) : (pc == 6 ? 192u : 194u));
+}
+
+template <int F, int NB> struct RCfg {
+    static constexpr int BN = 16 * NB;
+    static constexpr int NPH = HImg<F>::NPH, HRB = 16 * NPH, SB = Layout<F>::BYTES * (256 / Layout<F>::QK);
+    static constexpr int WH_INSTR = (RBM * NPH + 63) / 64; // DMA instructions per half image
+    static constexpr int NWH = (WH_INSTR + RW - 1) / RW;   // per wave and half
+    static constexpr int W1_OFF = RBM * HRB;                // the second half image
+    static constexpr int X_OFF = 2 * RBM * HRB;             // then the activation image
+    static constexpr int X_BYTES = BN * 512;                // 4 sub-stages x BN tokens x 128 B
+    static constexpr int X_INSTR = X_BYTES / 1024;          // prepared form: DMA instructions
+    static constexpr int NX = (X_INSTR + RW - 1) / RW;
+    static constexpr bool PAD = WH_INSTR % RW != 0 || X_INSTR % RW != 0 || RBM * NPH % 64 != 0;
+    static constexpr int SCRATCH = X_OFF + X_BYTES;         // padding DMAs land here
+    static constexpr int LDS = SCRATCH + (PAD ? 1024 : 0);
+    static_assert(LDS <= LDS_CAP, "LDS budget");
+};
+
+// element offset (in the super-block) of piece q (8 elements) of activation sub-stage u: the
+// K elements k-steps 2u, 2u+1 multiply (Q6_K: two 32-element runs, as act_soff / act_voff)
+template <int F> __device__ __forceinline__ int sub_elem(int u, int q)
+{
+    if constexpr (F == Q6_K) return 128 * (u >> 1) + 32 * (u & 1) + 64 * (q >> 2) + 8 * (q & 3);
+    return 64 * u + 8 * q;
+}
+
+// AQ: token r's 32-element block kb of the super-block, lane j of its quad (elements 32kb + 8j..)
+// -> the (sub-stage, piece) holding those elements
+template <int F> __device__ __forceinline__ void block_piece(int kb, int j, int &u, int &q)
+{
+    if constexpr (F == Q6_K) {
+        const int b4 = kb & 3;
+        u = 2 * (kb >> 2) + (b4 & 1);
+        q = 4 * (b4 >> 1) + j;
+    } else {
+        u = kb >> 1;
+        q = 4 * (kb & 1) + j;
+    }
+}
+
+// A fragments of sub-stage u (half h = u >> 1) for the row whose half image starts at img
+template <int F> __device__ __forceinline__ void half_frags(const uint8_t *img, int g, int u, f16x8 (&frag)[2])
+{
+    const int h = u >> 1;
+    if constexpr (F == Q8_0) stage_frags<Q8_0>(img - 128 * h, g, u, frag, 0); // (16-byte aligned: HRB = 144)
+    else if constexpr (F == Q4_K) q4k_frags(img, img + 16 + 32 * (u & 1), g, u, frag);
+    else q6k_half_frags(img, g, h, u & 1, frag);
+}
+
+// AQ: 0 = prepared x~ (X = fp16 [N][K], DEQ layout); 1 = raw fp16 [N][ldx], q8_1 in-kernel;
+// 2 = raw fp16, the fp8 variant's e4m3 quantization in-kernel (F8DEQ x~).
+// spol: cache policy of the split-K partial stores (0 plain, 2 nt, 16 sc1: A/B knob GQ_RGEMM_SPOL).
+template <int F, int NB, int AQ>
+__global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
+                                                       int64_t ldx, uint16_t *__restrict__ C, uint16_t *__restrict__ P,
+                                                       int64_t M, int64_t N, int64_t K, int64_t ldc, int spol)
+{
+    using G = RCfg<F, NB>;
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[G::LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, l16 = lane & 15;
+    const int64_t m0 = (int64_t)blockIdx.x * RBM, n0 = (int64_t)blockIdx.y * G::BN, sb = blockIdx.z;
+    const int64_t row_bytes = (K / Layout<F>::QK) * Layout<F>::BYTES;
+    uint8_t *const ximg = lds + G::X_OFF;
+
+    // 1. (AQ) the raw activations into registers first: their loads return ahead of the weight
+    //    DMAs in this wave's in-order memory queue, so the quantization overlaps the weights' flight
+    //    (BN tokens x 8 blocks of 32, four lanes -- 8 elements, one 16-byte load -- per block)
+    u32x4 xv[AQ ? NB : 1];
+    if constexpr (AQ != 0 && !(ABL & 2)) {
+        const __amdgpu_buffer_rsrc_t xrs =
+            __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, (int)(uint32_t)(((N - 1) * ldx + K) * 2), 0x00020000);
+#pragma unroll
+        for (int ps = 0; ps < NB; ++ps) {
+            const int b = 128 * ps + (tid >> 2), r = b >> 3, kb = b & 7;
+            const int64_t tok = n0 + r < N ? n0 + r : N - 1;
+            xv[ps] = __builtin_amdgcn_raw_buffer_load_b128(
+                xrs, (uint32_t)(tok * ldx * 2) + 2u * (uint32_t)(256 * sb + 32 * kb + 8 * (lane & 3)), 0, 0);
+        }
+    }
+
+    // 2. the weights: half image h, instruction k = wave + 8i moves pieces p = 64k + lane (row p / NPH)
+    const __amdgpu_buffer_rsrc_t wrs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, (int)(uint32_t)((M * row_bytes + 15) & ~(int64_t)15), 0x00020000);
+    auto issue_half = [&](int h) __attribute__((always_inline)) {
+        if constexpr (ABL & 1) return;
+#pragma unroll
+        for (int i = 0; i < G::NWH; ++i) {
+            const int k = wave + RW * i, p = 64 * k + lane, r = p / G::NPH, pc = p - r * G::NPH;
+            const bool real = k < G::WH_INSTR && r < RBM;
+            const int64_t row = m0 + r < M ? m0 + r : M - 1;
+            const uint32_t vo = real ? (uint32_t)(row * row_bytes) + hsrc<F>(h, pc) : 0u;
+            dma16(wrs, real ? lds + h * G::W1_OFF + 1024 * k : lds + G::SCRATCH, vo, (uint32_t)(G::SB * sb)); // (+16 lane)
+        }
+    };
+    // 3. (prepared) the activation image by LDS-DMA between the halves: image piece P = 64k + lane:
+    //    sub-stage u = P / (BN*8), token r, slot qd (source-swizzled)
+    auto issue_x = [&]() __attribute__((always_inline)) {
+        if constexpr (AQ != 0 || (ABL & 2)) return;
+        const __amdgpu_buffer_rsrc_t xrs =
+            __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, (int)(uint32_t)(N * K * 2), 0x00020000);
+#pragma unroll
+        for (int i = 0; i < G::NX; ++i) {
+            const int k = wave + RW * i, pp = 64 * k + lane;
+            const int u = pp / (G::BN * 8), r = (pp / 8) % G::BN, qd = pp & 7, q = qd ^ act_swz(r);
+            const int64_t tok = n0 + r < N ? n0 + r : N - 1;
+            const uint32_t vo = (uint32_t)(tok * K * 2) + 2u * (uint32_t)sub_elem<F>(u, q);
+            dma16(xrs, k < G::X_INSTR ? lds + G::X_OFF + 1024 * k : lds + G::SCRATCH, vo, (uint32_t)(512 * sb));
+        }
+    };
+    issue_half(0);
+    issue_x();
+    issue_half(1);
+
+    // 4. (AQ) quantize into the image: x~ = fp16(d*q) in act_quant's DEQ order (deq_quad), or the
+    //    fp8 variant's F8DEQ x~ (f8_quad) -- the compiler's vmcnt for xv leaves the DMAs in flight
+    if constexpr (AQ != 0 && !(ABL & 2)) {
+#pragma unroll
+        for (int ps = 0; ps < NB; ++ps) {
+            const int b = 128 * ps + (tid >> 2), r = b >> 3, kb = b & 7;
+            u32x4 o;
+            if constexpr (AQ == 2) {
+                const F8Quad fq = f8_quad(xv[ps]);
+                o = (u32x4){fq.xt[0], fq.xt[1], fq.xt[2], fq.xt[3]};
+            } else {
+                o = deq_quad(xv[ps]);
+            }
+            int u, q;
+            block_piece<F>(kb, lane & 3, u, q);
+            *(u32x4 *)(ximg + u * (G::BN * 128) + 128 * r + 16 * (q ^ act_swz(r))) = o;
+        }
+    }
+    // first half (+ the prepared activations) landed: all but this wave's second-half DMAs
+    constexpr int W1N = (ABL & 1) ? 0 : G::NWH;
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(W1N) : "memory");
+    __builtin_amdgcn_s_barrier();
+
+    // 5. the multiply: rows 16*(2*wave + rg) + [0, 16), every token, 4 sub-stages x 2 k-steps
+    f32x4 acc[RRG][NB];
+#pragma unroll
+    for (int rg = 0; rg < RRG; ++rg)
+#pragma unroll
+        for (int t = 0; t < NB; ++t) acc[rg][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 4 && !(ABL & 4); ++u) {
+        if (u == 2) { // the second half
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
+        f16x8 af[RRG][2];
+#pragma unroll
+        for (int rg = 0; rg < RRG; ++rg)
+            half_frags<F>(lds + (u >> 1) * G::W1_OFF + G::HRB * (16 * (RRG * wave + rg) + l16), g, u, af[rg]);
+        const uint8_t *xs = ximg + u * (G::BN * 128);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            f16x8 bk[NB];
+#pragma unroll
+            for (int t = 0; t < NB; ++t) {
+                const int r = 16 * t + l16;
+                bk[t] = *(const f16x8 *)(xs + 128 * r + 16 * ((4 * s + g) ^ act_swz(r)));
+            }
+#pragma unroll
+            for (int rg = 0; rg < RRG; ++rg)
+#pragma unroll
+                for (int t = 0; t < NB; ++t)
+                    acc[rg][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[rg][s], bk[t], acc[rg][t], 0, 0, 0);
+        }
+    }
+    if constexpr ((ABL & 4) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    // 6. epilogue: acc[rg][t][i] = D[row 16*(2*wave + rg) + 4g + i][token 16t + l16]
+    if constexpr ((ABL & 8) != 0) {
+        if (acc[0][0][0] == 1234.5f) C[0] = 0;
+        return;
+    }
+    if (gridDim.z > 1) {
+        // split-K partial, gemm_kernel's fp16 form (its reduce kernel sums it): per (tile, split)
+        // a block of 256 x BN halves in accumulator order, each wave's values scaled by 2^-e
+        const int64_t tile = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+        const int64_t bidx = tile * gridDim.z + blockIdx.z;
+        float mx = 0.f;
+#pragma unroll
+        for (int rg = 0; rg < RRG; ++rg)
+#pragma unroll
+            for (int t = 0; t < NB; ++t)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) mx = fmaxf(mx, fabsf(acc[rg][t][i]));
+        int m = __builtin_bit_cast(int, mx);
+        m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x111, 0xf, 0xf, true))));
+        m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x112, 0xf, 0xf, true))));
+        m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x114, 0xf, 0xf, true))));
+        m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x118, 0xf, 0xf, true))));
+        m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x142, 0xa, 0xf, true))));
+        m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x143, 0xc, 0xf, true))));
+        const uint32_t mb = (uint32_t)__builtin_amdgcn_readlane(m, 63);
+        const int E = (int)((mb >> 23) & 0xff) - 127;
+        const int e = E - 14 > 0 ? (E - 14 < 127 ? E - 14 : 126) : 0;
+        const float down = __builtin_bit_cast(float, (uint32_t)(127 - e) << 23);
+        const int64_t nblk = (int64_t)gridDim.x * gridDim.y * gridDim.z;
+        const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)P, 0, (int)(uint32_t)(nblk * (RBM * G::BN * 2 + RW * 4)), 0x00020000);
+        const uint32_t bo = (uint32_t)(bidx * (RBM * G::BN * 2));
+        if (lane == 0) {
+            const uint32_t eo = (uint32_t)(nblk * (RBM * G::BN * 2) + (bidx * RW + wave) * 4);
+            if (spol == 2) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)e, prs, eo, 0, 2);
+            else if (spol == 16) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)e, prs, eo, 0, 16);
+            else __builtin_amdgcn_raw_buffer_store_b32((uint32_t)e, prs, eo, 0, 0);
+        }
+        auto pk = [down](const f32x4 &v) {
+            return (u32x2){(uint32_t)f2h_bits(v[0] * down) | ((uint32_t)f2h_bits(v[1] * down) << 16),
+                           (uint32_t)f2h_bits(v[2] * down) | ((uint32_t)f2h_bits(v[3] * down) << 16)};
+        };
+#pragma unroll
+        for (int rg = 0; rg < RRG; ++rg) {
+            if constexpr (NB == 1) {
+                const uint32_t vo = bo + 8u * (uint32_t)((RRG * wave + rg) * 64 + lane);
+                if (spol == 2) __builtin_amdgcn_raw_buffer_store_b64(pk(acc[rg][0]), prs, vo, 0, 2);
+                else if (spol == 16) __builtin_amdgcn_raw_buffer_store_b64(pk(acc[rg][0]), prs, vo, 0, 16);
+                else __builtin_amdgcn_raw_buffer_store_b64(pk(acc[rg][0]), prs, vo, 0, 0);
+            } else {
+#pragma unroll
+                for (int uu = 0; uu < NB / 2; ++uu) {
+                    const u32x2 lo = pk(acc[rg][2 * uu]), hi = pk(acc[rg][2 * uu + 1]);
+                    const u32x4 w = {lo.x, lo.y, hi.x, hi.y};
+                    const uint32_t vo = bo + 16u * (uint32_t)(((RRG * wave + rg) * (NB / 2) + uu) * 64 + lane);
+                    if (spol == 2) __builtin_amdgcn_raw_buffer_store_b128(w, prs, vo, 0, 2);
+                    else if (spol == 16) __builtin_amdgcn_raw_buffer_store_b128(w, prs, vo, 0, 16);
+                    else __builtin_amdgcn_raw_buffer_store_b128(w, prs, vo, 0, 0);
+                }
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int rg = 0; rg < RRG; ++rg) {
+        const int64_t row = m0 + 16 * (RRG * wave + rg) + 4 * g;
+        if (row >= M) continue;
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+            const int64_t tok = n0 + 16 * t + l16;
+            if (tok >= N) continue;
+            const f32x4 v = acc[rg][t];
+            uint16_t *dst = C + tok * ldc + row;
+            if (row + 4 <= M) {
+                *(u32x2 *)dst = (u32x2){(uint32_t)f2h_bits(v[0]) | ((uint32_t)f2h_bits(v[1]) << 16),
+                                        (uint32_t)f2h_bits(v[2]) | ((uint32_t)f2h_bits(v[3]) << 16)};
+            } else {
+                for (int i = 0; i < 4 && row + i < M; ++i) dst[i] = f2h_bits(v[i]);
+            }
+        }
+    }
+}
+
+template <int F, int NB, int AQ>
+hipError_t launch_nb(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, void *P, const RGemmPlan &p,
+                     int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s)
+{
+    const dim3 grid((unsigned)p.tiles_m, (unsigned)p.tiles_n, (unsigned)p.splits);
+    rgemm_kernel<F, NB, AQ><<<grid, dim3(64 * RW), 0, s>>>(A, X, ldx, C, (uint16_t *)P, M, N, K, ldc, tuning().rgemm_spol);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || p.splits == 1) return e;
+    return launch_gemm_reduce_f16(NB, RRG, (const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n);
+}
+
+template <int F, int AQ>
+hipError_t launch_f(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, void *P, const RGemmPlan &p,
+                    int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s)
+{
+    switch (p.nb) {
+    case 1: return launch_nb<F, 1, AQ>(A, X, ldx, C, P, p, M, N, K, ldc, s);
+    case 2: return launch_nb<F, 2, AQ>(A, X, ldx, C, P, p, M, N, K, ldc, s);
+    case 4: return launch_nb<F, 4, AQ>(A, X, ldx, C, P, p, M, N, K, ldc, s);
+    case 8: return launch_nb<F, 8, AQ>(A, X, ldx, C, P, p, M, N, K, ldc, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+} // namespace
+
+RGemmPlan plan_rgemm(int64_t M, int64_t N, int64_t K)
+{
+    RGemmPlan p;
+    if (M < 1 || N < 1 || K < 256 || K % 256 != 0) return p;
+    p.nb = N > 64 ? 8 : (N > 32 ? 4 : (N > 16 ? 2 : 1));
+    p.tiles_m = (int)((M + RBM - 1) / RBM);
+    p.tiles_n = (int)((N + 16 * p.nb - 1) / (16 * p.nb));
+    p.splits = (int)(K / 256);
+    const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
+    p.partial_bytes = p.splits > 1 ? (size_t)p.splits * tiles * RBM * 16 * p.nb * 2 + (size_t)p.splits * tiles * RW * 4 : 0;
+    p.ok = true;
+    return p;
+}
+
+hipError_t launch_rgemm(int fmt, int aq, const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, void *partials,
+                        const RGemmPlan &p, int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s)
+{
+    if (!p.ok) return hipErrorInvalidValue;
+    if (aq != 0 && ldx % 8 != 0) return hipErrorInvalidValue; // 16-byte activation loads
+#define GQ_RG_AQ(F)                                                                                                   \
+    switch (aq) {                                                                                                     \
+    case 0: return launch_f<F, 0>(A, X, ldx, C, partials, p, M, N, K, ldc, s);                                        \
+    case 1: return launch_f<F, 1>(A, X, ldx, C, partials, p, M, N, K, ldc, s);                                        \
+    default: return launch_f<F, 2>(A, X, ldx, C, partials, p, M, N, K, ldc, s);                                       \
+    }
+    switch (fmt) {
+    case Q8_0: GQ_RG_AQ(Q8_0)
+    case Q4_K: GQ_RG_AQ(Q4_K)
+    default: GQ_RG_AQ(Q6_K)
+    }
+#undef GQ_RG_AQ
+}
+
+} // namespace gq

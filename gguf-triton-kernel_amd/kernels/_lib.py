@@ -180,10 +180,42 @@ def _stream(dev) -> int:
     return torch._C._cuda_getCurrentRawStream(dev.index if dev.index is not None else torch.cuda.current_device())
 
 
+_F16, _I8, _U8 = torch.float16, torch.int8, torch.uint8
+_mmq_ex = None  # the bound gq_mmq_ex (set on first use)
+
+
 def mmq(gtype: int, A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int,
         out: torch.Tensor | None = None, workspace: torch.Tensor | None = None, act: str = "q8_1") -> torch.Tensor:
     """C = (A @ B^T)^T as fp16 (N, M) on A's device; the common body of mmq_q8_0/q4_k/q6_k.
-    act="fp8": the fp8 activation variant (gq_mmq_ex, GQ_ACT_FP8_E4M3) instead of q8_1."""
+    act="fp8": the fp8 activation variant (gq_mmq_ex, GQ_ACT_FP8_E4M3) instead of q8_1.
+    The common eager form (contiguous device A, fp16 (N, K) B with unit column stride on A's
+    device, no out/workspace given) takes a short path: the same checks, fewer Python calls."""
+    global _mmq_ex
+    if (out is None and workspace is None and A.is_cuda and B.dtype is _F16 and B.dim() == 2 and
+            (A.dtype is _I8 or A.dtype is _U8)):
+        ns, ks = B.shape
+        if ns == N and ks == K and B.stride(1) == 1 and A.is_contiguous() and \
+                A.numel() == M * (K // BLOCK_ELEMS[gtype]) * BLOCK_BYTES[gtype]:
+            dev = A.device
+            if B.device != dev:
+                raise RuntimeError(f"A on {dev} but B on {B.device}")
+            if M == 0 or N == 0:
+                return torch.empty((N, M), dtype=_F16, device=dev)
+            key = (gtype, act, M, N, K)
+            need = _call_ws.get(key)
+            if need is None:
+                need = _call_ws[key] = int(lib().gq_mmq_call_workspace_size(gtype, ACTS[act], M, N, K))
+            if _mmq_ex is None:
+                _mmq_ex = lib().gq_mmq_ex
+            idx = dev.index
+            if idx == torch._C._cuda_getDevice():
+                C = torch.empty((N, M), dtype=_F16, device=dev)
+                ws = torch.empty(need, dtype=_U8, device=dev) if need else None
+                rc = _mmq_ex(gtype, ACTS[act], A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, B.stride(0), M,
+                             ws.data_ptr() if need else None, need, torch._C._cuda_getCurrentRawStream(idx))
+                if rc:
+                    _check(rc)
+                return C
     _check_weights(gtype, A, M, K)
     _require_device(B, "B")
     dev = A.device

@@ -49,3 +49,26 @@ print("workspace_size ctypes (no sync)  ", med(lambda: kl.workspace_size(kl.GQ_Q
 print("current_stream (no sync)         ", med(lambda: torch.cuda.current_stream(dev).cuda_stream, sync=False))
 print("mmq_q4_k (no sync)               ", med(lambda: mmq_q4_k(A, B, 4096, 1, 4096), sync=False))
 print("raw gq_mmq (no sync)             ", med(lambda: L.gq_mmq(1, A.data_ptr(), B.data_ptr(), C.data_ptr(), 4096, 1, 4096, 4096, 4096, ws.data_ptr(), need, st), sync=False))
+
+
+def b2b(fn, n=1000):
+    """Back-to-back: n calls, one synchronize at the end, divided by n (host-bound when the
+    kernel is shorter than the call's host time)."""
+    for _ in range(50):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        fn()
+    torch.cuda.synchronize()
+    return round((time.perf_counter() - t0) / n * 1e6, 2)
+
+
+print("b2b mmq_q4_k                     ", b2b(lambda: mmq_q4_k(A, B, 4096, 1, 4096)))
+print("b2b raw gq_mmq                   ", b2b(lambda: L.gq_mmq(1, A.data_ptr(), B.data_ptr(), C.data_ptr(), 4096, 1, 4096, 4096, 4096, ws.data_ptr(), need, st)))
+print("_check_weights                   ", med(lambda: kl._check_weights(kl.GQ_Q4_K, A, 4096, 4096), sync=False))
+print("_check_acts                      ", med(lambda: kl._check_acts(B, 1, 4096), sync=False))
+print("_check_out                       ", med(lambda: kl._check_out(None, 1, 4096, dev), sync=False))
+print("_stream                          ", med(lambda: kl._stream(dev), sync=False))
+print("current_device                   ", med(lambda: torch.cuda.current_device(), sync=False))
+print("data_ptr x3                      ", med(lambda: (A.data_ptr(), B.data_ptr(), C.data_ptr()), sync=False))
