@@ -36,6 +36,8 @@ struct Tuning {
     int skinny_rg = 0;                        // GQ_SKINNY_RG: fragments per workgroup, 1..4 (0: auto)
     int skinny_d = 0;                         // GQ_SKINNY_D: super-blocks in the register ring, 2..4 (0: auto)
     int rgemm = -1;                           // GQ_RGEMM: resident-split GEMM -1 auto / 0 off / 1 wherever it applies
+    int sgemm = -1;                           // GQ_SGEMM: streaming 256-row GEMM -1 auto / 0 off / 1 wherever it applies
+    int sgemm_splits = 0;                     // GQ_SGEMM_SPLITS (0: auto)
     int rgemm_spol = 0;                       // GQ_RGEMM_SPOL: its partial stores' cache policy 0 / 2 (nt) / 16 (sc1)
     int cus = 0;                              // GQ_CUS: compute units to plan for (0: the device's count)
     int ablate = 0;                           // GQ_ABLATE (GQ_ABLATION diagnostic builds only)
@@ -141,6 +143,34 @@ struct RGemmPlan {
 RGemmPlan plan_rgemm(int64_t M, int64_t N, int64_t K);
 hipError_t launch_rgemm(int fmt, int aq, const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, void *partials,
                         const RGemmPlan &p, int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
+// Streaming form (mmq_rgemm.hip sgemm_kernel): the same tile over K splits of several
+// super-blocks, half-super-block stages through an LDS ring; prepared x~ only (X = [N][K]).
+// splits <= 0: as many as keep the grid within one round of the chip.
+RGemmPlan plan_sgemm(int64_t M, int64_t N, int64_t K, int splits);
+hipError_t launch_sgemm(int fmt, const uint8_t *A, const uint16_t *X, uint16_t *C, void *partials, const RGemmPlan &p,
+                        int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
+
+// Several streaming GEMMs in one launch (+ one grouped split-K reduce), at most 16 items sharing
+// the token count N; X = each item's prepared x~ ([N][K]).  The plan spreads the super-blocks
+// over one round of the chip: the fewest per workgroup that fit, every item split accordingly
+// (splits > 0: that split factor for every item, as plan_sgemm's).
+struct SGroupItem {
+    int fmt;
+    const uint8_t *A;
+    const uint16_t *X;
+    uint16_t *C;
+    int64_t ldc, M, K;
+};
+struct SGroupPlan {
+    bool ok = false;
+    int nb = 8, tiles_n = 1, blocks = 0;
+    int tiles_m[16] = {}, splits[16] = {}, wg0[16] = {};
+    size_t poff[16] = {};
+    size_t partial_bytes = 0;
+};
+SGroupPlan plan_sgemm_grouped(const SGroupItem *items, int n, int64_t N, int splits);
+hipError_t launch_sgemm_grouped(const SGroupItem *items, int n, int64_t N, const SGroupPlan &g, void *partials,
+                                hipStream_t s);
 
 // Weight-register GEMM (mmq_wgemm.hip): weights streamed into VGPRs a super-block ahead,
 // activations (fp16 x~, act_quant DEQ form) register-staged into a two-slot LDS ring; 128*rg

@@ -91,6 +91,12 @@ bool parse_key(Tuning &t, const char *key, long long v)
     } else if (k == "GQ_RGEMM") {
         if (!in({-1, 0, 1})) return false;
         t.rgemm = (int)v;
+    } else if (k == "GQ_SGEMM") {
+        if (!in({-1, 0, 1})) return false;
+        t.sgemm = (int)v;
+    } else if (k == "GQ_SGEMM_SPLITS") {
+        if (v < 0 || v > 4096) return false;
+        t.sgemm_splits = (int)v;
     } else if (k == "GQ_RGEMM_SPOL") {
         if (!in({0, 2, 16})) return false;
         t.rgemm_spol = (int)v;
@@ -110,7 +116,7 @@ void tuning_from_env(Tuning &t)
                                        "GQ_GEMM_NB", "GQ_GEMM_RG", "GQ_GEMM_LOADERS", "GQ_GEMM_SPLITS",
                                        "GQ_GEMM_PARTIAL", "GQ_GEMM_FUSED_REDUCE", "GQ_GEMV_CAP", "GQ_GEMV_R",
                                        "GQ_WGEMM", "GQ_WGEMM_RG", "GQ_WGEMM_NB", "GQ_WGEMM_SPLITS", "GQ_WGEMM_WD",
-                                       "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D", "GQ_RGEMM", "GQ_RGEMM_SPOL", "GQ_CUS", "GQ_ABLATE"};
+                                       "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D", "GQ_RGEMM", "GQ_SGEMM", "GQ_SGEMM_SPLITS", "GQ_RGEMM_SPOL", "GQ_CUS", "GQ_ABLATE"};
     for (const char *k : keys) {
         const char *e = getenv(k); // the only getenv of the library: once per process
         if (!e || !*e) continue;
@@ -296,6 +302,17 @@ bool use_rgemm(int t, int form, int64_t M, int64_t N, int64_t K)
     return grid <= cus && 2 * grid >= cus;
 }
 
+// Streaming 256-row GEMM (mmq_rgemm.hip sgemm_kernel) on the prepared x~: GQ_SGEMM=1 wherever
+// the resident form does not apply (tests, A/B), 0 off; auto: not yet the default anywhere.
+bool use_sgemm(int t, int form, int64_t M, int64_t N, int64_t K)
+{
+    const int sg = gq::tuning().sgemm;
+    if (sg <= 0 || form != gq::AF_F16 || use_gemv(N, K) || use_blas(N, K) || K % 256 != 0) return false;
+    if (gemm_rows_per_launch(t, M, K) < M || gemm_toks_per_launch(N, K) < N) return false;
+    return gq::plan_sgemm(M, N, K, gq::tuning().sgemm_splits).ok;
+}
+gq::RGemmPlan sgemm_plan(int64_t M, int64_t N, int64_t K) { return gq::plan_sgemm(M, N, K, gq::tuning().sgemm_splits); }
+
 bool use_i8(int t, int64_t N, int64_t K)
 {
     if (t != GQ_Q8_0 || use_gemv(N, K) || use_blas(N, K)) return false;
@@ -354,7 +371,8 @@ size_t ws_bytes(int t, int act, int64_t M, int64_t N, int64_t K)
         // (the kernel is chosen by the call's token count, so every chunk runs the same arithmetic)
         const bool sk = use_skinny(t, r.form, N, act), wg = use_wgemm(t, r.form, N);
         const int64_t mr = gemm_rows_per_launch(t, M, K), nt = sk ? N : gemm_toks_per_launch(N, K);
-        size_t p = use_rgemm(t, r.form, M, N, K) ? gq::plan_rgemm(M, N, K).partial_bytes : 0;
+        size_t p = use_rgemm(t, r.form, M, N, K) ? gq::plan_rgemm(M, N, K).partial_bytes
+                   : use_sgemm(t, r.form, M, N, K) ? sgemm_plan(M, N, K).partial_bytes : 0;
         for (int64_t mc : {mr, M % mr})
             for (int64_t nc : {nt, N % nt})
                 if (mc > 0 && nc > 0) {
@@ -591,6 +609,12 @@ static int compute(gq_type t, int act, const void *A, void *workspace, size_t wo
             e = gq::launch_rgemm(t, 0, (const uint8_t *)A, c.xdeq, K, (uint16_t *)C, c.partials, gq::plan_rgemm(M, N, K),
                                  M, N, K, ldc, s);
             if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (rgemm): %s", hipGetErrorString(e));
+            return GQ_OK;
+        }
+        if (!use_skinny(t, r.form, N, act) && use_sgemm(t, r.form, M, N, K)) {
+            e = gq::launch_sgemm(t, (const uint8_t *)A, c.xdeq, (uint16_t *)C, c.partials, sgemm_plan(M, N, K), M, N, K,
+                                 ldc, s);
+            if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (sgemm): %s", hipGetErrorString(e));
             return GQ_OK;
         }
         const bool sk = use_skinny(t, r.form, N, act), wg = use_wgemm(t, r.form, N);
@@ -894,6 +918,60 @@ int gq_mmq_grouped_ex(gq_act act, const gq_group_item *items, int n, int64_t N, 
     hipError_t e = gq::launch_decode_grouped(di, m, N, (hipStream_t)stream, fp8);
     if (e == hipErrorInvalidValue) return fail(GQ_EUNSUPPORTED, "grouped decode: more than 16 parts");
     if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (grouped decode): %s", hipGetErrorString(e));
+    return GQ_OK;
+}
+
+// gq_mmq_grouped_prepared: the items as the grouped streaming GEMM takes them, or a GQ_* error
+static int grouped_gemm_items(gq_act act, const gq_gemm_item *items, int n, int64_t N, gq::SGroupItem *out)
+{
+    if (n < 0 || (n > 0 && !items)) return fail(GQ_EINVAL, "bad item list (n=%d, items=%p)", n, (const void *)items);
+    if (n > 16) return fail(GQ_EUNSUPPORTED, "more than 16 items");
+    if (N < 5) return fail(GQ_EUNSUPPORTED, "grouped GEMM needs N >= 5 (N=%lld): gq_mmq_grouped for decode", (long long)N);
+    for (int i = 0; i < n; ++i) {
+        const gq_gemm_item &it = items[i];
+        int rc = check_common(it.type, it.M, N, it.K);
+        if (rc != GQ_OK) return rc;
+        if ((rc = check_act(act, it.K)) != GQ_OK) return rc;
+        if (it.K % 256 != 0 || it.K == 0) return fail(GQ_EUNSUPPORTED, "item %d: K=%lld is not a multiple of 256", i, (long long)it.K);
+        if (it.M > 0 && (!it.A || !it.ws || !it.C)) return fail(GQ_EINVAL, "item %d: null pointer", i);
+        if (it.ldc < it.M) return fail(GQ_EINVAL, "item %d: ldc=%lld < M=%lld", i, (long long)it.ldc, (long long)it.M);
+        if (gemm_rows_per_launch(it.type, it.M, it.K) < it.M || gemm_toks_per_launch(N, it.K) < N)
+            return fail(GQ_EUNSUPPORTED, "item %d: 2 GiB or more in one operand", i);
+        out[i] = gq::SGroupItem{it.type, (const uint8_t *)it.A, carve(act, const_cast<void *>(it.ws), N, it.K).xdeq,
+                                (uint16_t *)it.C, it.ldc, it.M, it.K};
+    }
+    return GQ_OK;
+}
+
+size_t gq_mmq_grouped_prepared_workspace_size(gq_act act, const gq_gemm_item *items, int n, int64_t N)
+{
+    gq::SGroupItem g[16];
+    if (n < 1 || grouped_gemm_items(act, items, n, N, g) != GQ_OK) return 0;
+    int m = 0; // items with rows (as gq_mmq_grouped_prepared plans them)
+    for (int i = 0; i < n; ++i)
+        if (g[i].M > 0) g[m++] = g[i];
+    if (m == 0) return 0;
+    const gq::SGroupPlan p = gq::plan_sgemm_grouped(g, m, N, gq::tuning().sgemm_splits);
+    return p.ok ? p.partial_bytes : 0;
+}
+
+int gq_mmq_grouped_prepared(gq_act act, const gq_gemm_item *items, int n, int64_t N, void *workspace,
+                            size_t workspace_bytes, void *stream)
+{
+    g_err.clear();
+    gq::SGroupItem g[16];
+    int rc = grouped_gemm_items(act, items, n, N, g);
+    if (rc != GQ_OK) return rc;
+    int m = 0; // items with rows
+    for (int i = 0; i < n; ++i)
+        if (g[i].M > 0) g[m++] = g[i];
+    if (m == 0) return GQ_OK;
+    const gq::SGroupPlan p = gq::plan_sgemm_grouped(g, m, N, gq::tuning().sgemm_splits);
+    if (!p.ok) return fail(GQ_EUNSUPPORTED, "not a grouped GEMM shape");
+    if (p.partial_bytes && (!workspace || workspace_bytes < p.partial_bytes))
+        return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace ? workspace_bytes : (size_t)0, p.partial_bytes);
+    const hipError_t e = gq::launch_sgemm_grouped(g, m, N, p, workspace, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (grouped GEMM): %s", hipGetErrorString(e));
     return GQ_OK;
 }
 

@@ -109,6 +109,132 @@ template <int F> __device__ __forceinline__ void half_frags(const uint8_t *img, 
     else q6k_half_frags(img, g, h, u & 1, frag);
 }
 
+// The tile's fp32 accumulators out: acc[rg][t][i] = D[row 16*(2*wave + rg) + 4g + i][token
+// 16t + l16].  One split: fp16 C.  Split-K (gridDim.z > 1): the partial in gemm_kernel's fp16
+// form (its reduce kernel sums it): per (tile, split) a block of 256 x BN halves in accumulator
+// order, each wave's values scaled by 2^-e, the e's after all blocks; spol = store cache policy.
+// One sub-stage u (64 K elements) of this wave's 32 rows x every token: the A fragments from the
+// half image wimg (half u >> 1), the B fragments from the sub-stage's activation image xs
+template <int F, int NB>
+__device__ __forceinline__ void mul_substage(const uint8_t *wimg, const uint8_t *xs, int u, f32x4 (&acc)[RRG][NB])
+{
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4, l16 = lane & 15;
+    f16x8 af[RRG][2];
+#pragma unroll
+    for (int rg = 0; rg < RRG; ++rg)
+        half_frags<F>(wimg + (16 * HImg<F>::NPH) * (16 * (RRG * wave + rg) + l16), g, u, af[rg]);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        f16x8 bk[NB];
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+            const int r = 16 * t + l16;
+            bk[t] = *(const f16x8 *)(xs + 128 * r + 16 * ((4 * s + g) ^ act_swz(r)));
+        }
+#pragma unroll
+        for (int rg = 0; rg < RRG; ++rg)
+#pragma unroll
+            for (int t = 0; t < NB; ++t)
+                acc[rg][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[rg][s], bk[t], acc[rg][t], 0, 0, 0);
+    }
+}
+
+struct TileId { // a workgroup's tile: (x, y, z) of a (gx, gy, gz) grid (z = the K split)
+    int x, y, z, gx, gy, gz;
+};
+__device__ __forceinline__ TileId grid_tile()
+{
+    return TileId{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y, (int)gridDim.z};
+}
+
+template <int NB>
+__device__ __forceinline__ void store_tile(const f32x4 (&acc)[RRG][NB], uint16_t *__restrict__ C,
+                                           uint16_t *__restrict__ P, int64_t M, int64_t N, int64_t ldc, int spol,
+                                           const TileId &id)
+{
+    constexpr int BN = 16 * NB;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4, l16 = lane & 15;
+    const int64_t m0 = (int64_t)id.x * RBM, n0 = (int64_t)id.y * BN;
+    if (id.gz > 1) {
+        // split-K partial, gemm_kernel's fp16 form (its reduce kernel sums it): per (tile, split)
+        // a block of 256 x BN halves in accumulator order, each wave's values scaled by 2^-e
+        const int64_t tile = (int64_t)id.y * id.gx + id.x;
+        const int64_t bidx = tile * id.gz + id.z;
+        float mx = 0.f;
+#pragma unroll
+        for (int rg = 0; rg < RRG; ++rg)
+#pragma unroll
+            for (int t = 0; t < NB; ++t)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) mx = fmaxf(mx, fabsf(acc[rg][t][i]));
+        int m = __builtin_bit_cast(int, mx);
+        m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x111, 0xf, 0xf, true))));
+        m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x112, 0xf, 0xf, true))));
+        m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x114, 0xf, 0xf, true))));
+        m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x118, 0xf, 0xf, true))));
+        m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x142, 0xa, 0xf, true))));
+        m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x143, 0xc, 0xf, true))));
+        const uint32_t mb = (uint32_t)__builtin_amdgcn_readlane(m, 63);
+        const int E = (int)((mb >> 23) & 0xff) - 127;
+        const int e = E - 14 > 0 ? (E - 14 < 127 ? E - 14 : 126) : 0;
+        const float down = __builtin_bit_cast(float, (uint32_t)(127 - e) << 23);
+        const int64_t nblk = (int64_t)id.gx * id.gy * id.gz;
+        const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)P, 0, (int)(uint32_t)(nblk * (RBM * BN * 2 + RW * 4)), 0x00020000);
+        const uint32_t bo = (uint32_t)(bidx * (RBM * BN * 2));
+        if (lane == 0) {
+            const uint32_t eo = (uint32_t)(nblk * (RBM * BN * 2) + (bidx * RW + wave) * 4);
+            if (spol == 2) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)e, prs, eo, 0, 2);
+            else if (spol == 16) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)e, prs, eo, 0, 16);
+            else __builtin_amdgcn_raw_buffer_store_b32((uint32_t)e, prs, eo, 0, 0);
+        }
+        auto pk = [down](const f32x4 &v) {
+            return (u32x2){(uint32_t)f2h_bits(v[0] * down) | ((uint32_t)f2h_bits(v[1] * down) << 16),
+                           (uint32_t)f2h_bits(v[2] * down) | ((uint32_t)f2h_bits(v[3] * down) << 16)};
+        };
+#pragma unroll
+        for (int rg = 0; rg < RRG; ++rg) {
+            if constexpr (NB == 1) {
+                const uint32_t vo = bo + 8u * (uint32_t)((RRG * wave + rg) * 64 + lane);
+                if (spol == 2) __builtin_amdgcn_raw_buffer_store_b64(pk(acc[rg][0]), prs, vo, 0, 2);
+                else if (spol == 16) __builtin_amdgcn_raw_buffer_store_b64(pk(acc[rg][0]), prs, vo, 0, 16);
+                else __builtin_amdgcn_raw_buffer_store_b64(pk(acc[rg][0]), prs, vo, 0, 0);
+            } else {
+#pragma unroll
+                for (int uu = 0; uu < NB / 2; ++uu) {
+                    const u32x2 lo = pk(acc[rg][2 * uu]), hi = pk(acc[rg][2 * uu + 1]);
+                    const u32x4 w = {lo.x, lo.y, hi.x, hi.y};
+                    const uint32_t vo = bo + 16u * (uint32_t)(((RRG * wave + rg) * (NB / 2) + uu) * 64 + lane);
+                    if (spol == 2) __builtin_amdgcn_raw_buffer_store_b128(w, prs, vo, 0, 2);
+                    else if (spol == 16) __builtin_amdgcn_raw_buffer_store_b128(w, prs, vo, 0, 16);
+                    else __builtin_amdgcn_raw_buffer_store_b128(w, prs, vo, 0, 0);
+                }
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int rg = 0; rg < RRG; ++rg) {
+        const int64_t row = m0 + 16 * (RRG * wave + rg) + 4 * g;
+        if (row >= M) continue;
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+            const int64_t tok = n0 + 16 * t + l16;
+            if (tok >= N) continue;
+            const f32x4 v = acc[rg][t];
+            uint16_t *dst = C + tok * ldc + row;
+            if (row + 4 <= M) {
+                *(u32x2 *)dst = (u32x2){(uint32_t)f2h_bits(v[0]) | ((uint32_t)f2h_bits(v[1]) << 16),
+                                        (uint32_t)f2h_bits(v[2]) | ((uint32_t)f2h_bits(v[3]) << 16)};
+            } else {
+                for (int i = 0; i < 4 && row + i < M; ++i) dst[i] = f2h_bits(v[i]);
+            }
+        }
+    }
+}
+
 // AQ: 0 = prepared x~ (X = fp16 [N][K], DEQ layout); 1 = raw fp16 [N][ldx], q8_1 in-kernel;
 // 2 = raw fp16, the fp8 variant's e4m3 quantization in-kernel (F8DEQ x~).
 // spol: cache policy of the split-K partial stores (0 plain, 2 nt, 16 sc1: A/B knob GQ_RGEMM_SPOL).
@@ -210,109 +336,247 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
         }
-        f16x8 af[RRG][2];
-#pragma unroll
-        for (int rg = 0; rg < RRG; ++rg)
-            half_frags<F>(lds + (u >> 1) * G::W1_OFF + G::HRB * (16 * (RRG * wave + rg) + l16), g, u, af[rg]);
-        const uint8_t *xs = ximg + u * (G::BN * 128);
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            f16x8 bk[NB];
-#pragma unroll
-            for (int t = 0; t < NB; ++t) {
-                const int r = 16 * t + l16;
-                bk[t] = *(const f16x8 *)(xs + 128 * r + 16 * ((4 * s + g) ^ act_swz(r)));
-            }
-#pragma unroll
-            for (int rg = 0; rg < RRG; ++rg)
-#pragma unroll
-                for (int t = 0; t < NB; ++t)
-                    acc[rg][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[rg][s], bk[t], acc[rg][t], 0, 0, 0);
-        }
+        mul_substage<F, NB>(lds + (u >> 1) * G::W1_OFF, ximg + u * (G::BN * 128), u, acc);
     }
     if constexpr ((ABL & 4) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-    // 6. epilogue: acc[rg][t][i] = D[row 16*(2*wave + rg) + 4g + i][token 16t + l16]
+    // 6. epilogue
     if constexpr ((ABL & 8) != 0) {
         if (acc[0][0][0] == 1234.5f) C[0] = 0;
         return;
     }
-    if (gridDim.z > 1) {
-        // split-K partial, gemm_kernel's fp16 form (its reduce kernel sums it): per (tile, split)
-        // a block of 256 x BN halves in accumulator order, each wave's values scaled by 2^-e
-        const int64_t tile = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-        const int64_t bidx = tile * gridDim.z + blockIdx.z;
-        float mx = 0.f;
+    store_tile<NB>(acc, C, P, M, N, ldc, spol, grid_tile());
+}
+
+// ---------------------------------------------------------------------------------------
+// The streaming form (sgemm_kernel): the same 256-row x 16*NB-token tile and multiply over a
+// K split of several super-blocks, the split's half-super-block stages (the W half image + the
+// activations' half x~ image, prepared by act_quant) through a ring of NS slots in LDS: stage j
+// lands -> barrier -> stage j+NS-1 is issued into the slot stage j-1 left -> stage j is multiplied.
+// For the matrices whose row tiles x super-blocks exceed one round of the chip (the 70B Q6_K
+// matrices, 11008-row Q4_K); split-K partials as rgemm_kernel's.
+template <int F, int NB> struct SCfg {
+    static constexpr int BN = 16 * NB;
+    static constexpr int NPH = HImg<F>::NPH, HRB = 16 * NPH, SB = Layout<F>::BYTES * (256 / Layout<F>::QK);
+    static constexpr int W_BYTES = RBM * HRB, X_BYTES = BN * 256; // one half stage
+    static constexpr int SLOT = W_BYTES + X_BYTES;
+    static constexpr int WH_INSTR = (RBM * NPH + 63) / 64, NWH = (WH_INSTR + RW - 1) / RW;
+    static constexpr int XH_INSTR = X_BYTES / 1024, NXH = (XH_INSTR + RW - 1) / RW;
+    static constexpr int NPS = NWH + NXH; // DMA instructions per wave and stage
+    static constexpr bool PAD = WH_INSTR % RW != 0 || XH_INSTR % RW != 0 || XH_INSTR < RW;
+    static constexpr int NS = (LDS_CAP - 1024) / SLOT > 4 ? 4 : (LDS_CAP - 1024) / SLOT; // ring slots
+    static constexpr int SCRATCH = NS * SLOT;
+    static constexpr int LDS = SCRATCH + (PAD ? 1024 : 0);
+    static_assert(NS >= 2, "two ring slots");
+    static_assert(LDS <= LDS_CAP, "LDS budget");
+    static_assert((NS - 2) * NPS <= 63, "vmcnt range");
+};
+
+constexpr int kMaxSParts = 16;
+struct SPart {
+    int fmt;
+    const uint8_t *A;
+    const uint16_t *X;
+    uint16_t *C, *P;
+    int64_t M, K, ldc;
+    int tiles_m, tiles_n, splits, wg0;
+};
+struct SParts {
+    int n;
+    int64_t N;
+    int spol;
+    SPart p[kMaxSParts];
+};
+struct RPart {
+    const uint16_t *P;
+    uint16_t *C;
+    int64_t M, ldc;
+    int tiles_m, tiles_n, splits, wg0;
+};
+struct RParts {
+    int n;
+    int64_t N;
+    RPart p[kMaxSParts];
+};
+
+template <int F, int NB>
+__device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
+                                           uint16_t *__restrict__ C, uint16_t *__restrict__ P, int64_t M, int64_t N,
+                                           int64_t K, int64_t ldc, int spol, const TileId &id, uint8_t *lds)
+{
+    using G = SCfg<F, NB>;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t m0 = (int64_t)id.x * RBM, n0 = (int64_t)id.y * G::BN;
+    const int64_t row_bytes = (K / Layout<F>::QK) * Layout<F>::BYTES, nsb = K / 256;
+    // split z: super-blocks [z*nsb/S, (z+1)*nsb/S) (split lengths differ by one when S does not divide)
+    const int64_t S = id.gz, z = id.z;
+    const int64_t sb0 = z * nsb / S, sb1 = (z + 1) * nsb / S;
+    const int nst = (int)(2 * (sb1 - sb0)); // half stages
+    const __amdgpu_buffer_rsrc_t wrs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, (int)(uint32_t)((M * row_bytes + 15) & ~(int64_t)15), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, (int)(uint32_t)(N * K * 2), 0x00020000);
+
+    auto issue = [&](int j) __attribute__((always_inline)) {
+        uint8_t *slot = lds + (j % G::NS) * G::SLOT;
+        const int64_t sb = sb0 + (j >> 1);
+        const int h = j & 1;
 #pragma unroll
-        for (int rg = 0; rg < RRG; ++rg)
-#pragma unroll
-            for (int t = 0; t < NB; ++t)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) mx = fmaxf(mx, fabsf(acc[rg][t][i]));
-        int m = __builtin_bit_cast(int, mx);
-        m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x111, 0xf, 0xf, true))));
-        m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x112, 0xf, 0xf, true))));
-        m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x114, 0xf, 0xf, true))));
-        m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x118, 0xf, 0xf, true))));
-        m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x142, 0xa, 0xf, true))));
-        m = __builtin_bit_cast(int, fmaxf(__builtin_bit_cast(float, m), __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, m, 0x143, 0xc, 0xf, true))));
-        const uint32_t mb = (uint32_t)__builtin_amdgcn_readlane(m, 63);
-        const int E = (int)((mb >> 23) & 0xff) - 127;
-        const int e = E - 14 > 0 ? (E - 14 < 127 ? E - 14 : 126) : 0;
-        const float down = __builtin_bit_cast(float, (uint32_t)(127 - e) << 23);
-        const int64_t nblk = (int64_t)gridDim.x * gridDim.y * gridDim.z;
-        const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)P, 0, (int)(uint32_t)(nblk * (RBM * G::BN * 2 + RW * 4)), 0x00020000);
-        const uint32_t bo = (uint32_t)(bidx * (RBM * G::BN * 2));
-        if (lane == 0) {
-            const uint32_t eo = (uint32_t)(nblk * (RBM * G::BN * 2) + (bidx * RW + wave) * 4);
-            if (spol == 2) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)e, prs, eo, 0, 2);
-            else if (spol == 16) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)e, prs, eo, 0, 16);
-            else __builtin_amdgcn_raw_buffer_store_b32((uint32_t)e, prs, eo, 0, 0);
+        for (int i = 0; i < G::NWH; ++i) {
+            const int k = wave + RW * i, p = 64 * k + lane, r = p / G::NPH, pc = p - r * G::NPH;
+            const bool real = k < G::WH_INSTR;
+            const int64_t row = m0 + r < M ? m0 + r : M - 1;
+            const uint32_t vo = real ? (uint32_t)(row * row_bytes) + hsrc<F>(h, pc) : 0u;
+            dma16(wrs, real ? slot + 1024 * k : lds + G::SCRATCH, vo, (uint32_t)(G::SB * sb)); // (+16 lane)
         }
-        auto pk = [down](const f32x4 &v) {
-            return (u32x2){(uint32_t)f2h_bits(v[0] * down) | ((uint32_t)f2h_bits(v[1] * down) << 16),
-                           (uint32_t)f2h_bits(v[2] * down) | ((uint32_t)f2h_bits(v[3] * down) << 16)};
-        };
+        // activation half image: piece P = 64k + lane: sub-stage ul = P / (BN*8), token r, slot qd
 #pragma unroll
-        for (int rg = 0; rg < RRG; ++rg) {
-            if constexpr (NB == 1) {
-                const uint32_t vo = bo + 8u * (uint32_t)((RRG * wave + rg) * 64 + lane);
-                if (spol == 2) __builtin_amdgcn_raw_buffer_store_b64(pk(acc[rg][0]), prs, vo, 0, 2);
-                else if (spol == 16) __builtin_amdgcn_raw_buffer_store_b64(pk(acc[rg][0]), prs, vo, 0, 16);
-                else __builtin_amdgcn_raw_buffer_store_b64(pk(acc[rg][0]), prs, vo, 0, 0);
+        for (int i = 0; i < G::NXH; ++i) {
+            const int k = wave + RW * i, pp = 64 * k + lane;
+            const bool real = k < G::XH_INSTR;
+            const int ul = pp / (G::BN * 8), r = (pp / 8) % G::BN, qd = pp & 7, q = qd ^ act_swz(r);
+            const int64_t tok = n0 + r < N ? n0 + r : N - 1;
+            const uint32_t vo = real ? (uint32_t)(tok * K * 2) + 2u * (uint32_t)sub_elem<F>(2 * h + ul, q) : 0u;
+            dma16(xrs, real ? slot + G::W_BYTES + 1024 * k : lds + G::SCRATCH, vo, (uint32_t)(512 * sb));
+        }
+    };
+
+    f32x4 acc[RRG][NB];
+#pragma unroll
+    for (int rg = 0; rg < RRG; ++rg)
+#pragma unroll
+        for (int t = 0; t < NB; ++t) acc[rg][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < G::NS - 1; ++i)
+        if (i < nst) issue(i);
+    for (int j = 0; j < nst; ++j) {
+        // stage j landed: all but the (<= NS-2) younger stages this wave issued
+        const int younger = G::NS - 2 < nst - 1 - j ? G::NS - 2 : nst - 1 - j;
+        vm_wait<(G::NS - 2) * G::NPS>(younger * G::NPS);
+        __builtin_amdgcn_s_barrier();
+        if (j + G::NS - 1 < nst) issue(j + G::NS - 1); // into the slot stage j-1 left (barrier passed)
+        const uint8_t *slot = lds + (j % G::NS) * G::SLOT;
+        const int h = j & 1;
+#pragma unroll
+        for (int ul = 0; ul < 2; ++ul)
+            mul_substage<F, NB>(slot, slot + G::W_BYTES + ul * (G::BN * 128), 2 * h + ul, acc);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // (nothing is in flight here; no DMA outlives the workgroup)
+    store_tile<NB>(acc, C, P, M, N, ldc, spol, id);
+}
+
+template <int F, int NB>
+__global__ __launch_bounds__(64 * RW) void sgemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
+                                                       uint16_t *__restrict__ C, uint16_t *__restrict__ P, int64_t M,
+                                                       int64_t N, int64_t K, int64_t ldc, int spol)
+{
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[SCfg<F, NB>::LDS];
+    sgemm_body<F, NB>(A, X, C, P, M, N, K, ldc, spol, grid_tile(), lds);
+}
+
+// ---- several matrices in one launch (gq_mmq_grouped_prepared): part i = one matrix's
+// (row tile, token tile, split) grid, its workgroups [wg0, wg0 + tiles_m * tiles_n * splits)
+template <int NB> constexpr int max_slds()
+{
+    constexpr int a = SCfg<Q8_0, NB>::LDS, b = SCfg<Q4_K, NB>::LDS, c = SCfg<Q6_K, NB>::LDS;
+    return a > b ? (a > c ? a : c) : (b > c ? b : c);
+}
+
+template <int NB>
+__global__ __launch_bounds__(64 * RW) void sgemm_grouped_kernel(const SParts a)
+{
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[max_slds<NB>()];
+    const int b = (int)blockIdx.x;
+    int i = 0;
+    while (i + 1 < a.n && b >= a.p[i + 1].wg0) ++i;
+    const SPart &q = a.p[i];
+    const int l = b - q.wg0, txy = q.tiles_m * q.tiles_n;
+    const TileId id{l % q.tiles_m, (l % txy) / q.tiles_m, l / txy, q.tiles_m, q.tiles_n, q.splits};
+    switch (q.fmt) {
+    case Q8_0: sgemm_body<Q8_0, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, lds); return;
+    case Q4_K: sgemm_body<Q4_K, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, lds); return;
+    default: sgemm_body<Q6_K, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, lds); return;
+    }
+}
+
+// The split-K sum of several parts' fp16 partials (store_tile's form): one thread per 16-byte
+// unit of a tile block (two token tiles x 4 rows; NB = 1: 8 bytes, one token tile); a part's S
+// splits summed in split order in fp32 after each wave's 2^e -- gemm_reduce_f16_kernel's
+// arithmetic (the same order, the same trailing +0 for S % 8 != 0), so every part's bits equal
+// its own launch's.
+template <int NB>
+__global__ __launch_bounds__(256) void reduce_grouped_kernel(const RParts a)
+{
+    constexpr int TPU = NB == 1 ? 1 : 2, UPT = RW * RRG * (NB / TPU) * 64; // units per tile
+    constexpr int BPT = (UPT + 255) / 256;
+    const int b = (int)blockIdx.x;
+    int i = 0;
+    while (i + 1 < a.n && b >= a.p[i + 1].wg0) ++i;
+    const RPart &q = a.p[i];
+    const int l = b - q.wg0, tile = l / BPT, it = (l % BPT) * 256 + (int)threadIdx.x;
+    const int ntiles = q.tiles_m * q.tiles_n;
+    if (tile >= ntiles || it >= UPT) return;
+    const int lane = it & 63, u = (it >> 6) % (NB / TPU), wr = (it >> 6) / (NB / TPU);
+    const int wv = __builtin_amdgcn_readfirstlane(wr / RRG);
+    const int64_t m0 = (int64_t)(tile % q.tiles_m) * RBM, n0 = (int64_t)(tile / q.tiles_m) * (16 * NB);
+    const int64_t blk = (int64_t)RBM * 16 * NB; // halves per (tile, split) block
+    const int S = q.splits;
+    const int *es = (const int *)(q.P + (int64_t)ntiles * S * blk);
+    f32x4 acc[TPU];
+#pragma unroll
+    for (int j = 0; j < TPU; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int s0 = 0; s0 < S; s0 += 8) {
+        u32x4 v[8];
+        float up[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { // unconditional (clamped) loads, the surplus zeroed after
+            const int64_t sp = (int64_t)tile * S + (s0 + k < S ? s0 + k : S - 1);
+            up[k] = __builtin_bit_cast(float, (uint32_t)(127 + es[sp * RW + wv]) << 23);
+            if constexpr (TPU == 2) {
+                v[k] = ((const u32x4 *)(q.P + sp * blk))[it];
             } else {
-#pragma unroll
-                for (int uu = 0; uu < NB / 2; ++uu) {
-                    const u32x2 lo = pk(acc[rg][2 * uu]), hi = pk(acc[rg][2 * uu + 1]);
-                    const u32x4 w = {lo.x, lo.y, hi.x, hi.y};
-                    const uint32_t vo = bo + 16u * (uint32_t)(((RRG * wave + rg) * (NB / 2) + uu) * 64 + lane);
-                    if (spol == 2) __builtin_amdgcn_raw_buffer_store_b128(w, prs, vo, 0, 2);
-                    else if (spol == 16) __builtin_amdgcn_raw_buffer_store_b128(w, prs, vo, 0, 16);
-                    else __builtin_amdgcn_raw_buffer_store_b128(w, prs, vo, 0, 0);
-                }
+                const u32x2 w = ((const u32x2 *)(q.P + sp * blk))[it];
+                v[k] = (u32x4){w.x, w.y, 0u, 0u};
             }
         }
-        return;
-    }
 #pragma unroll
-    for (int rg = 0; rg < RRG; ++rg) {
-        const int64_t row = m0 + 16 * (RRG * wave + rg) + 4 * g;
-        if (row >= M) continue;
+        for (int k = 0; k < 8; ++k) {
+            if (s0 + k >= S) v[k] = (u32x4){0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int t = 0; t < NB; ++t) {
-            const int64_t tok = n0 + 16 * t + l16;
-            if (tok >= N) continue;
-            const f32x4 v = acc[rg][t];
-            uint16_t *dst = C + tok * ldc + row;
-            if (row + 4 <= M) {
-                *(u32x2 *)dst = (u32x2){(uint32_t)f2h_bits(v[0]) | ((uint32_t)f2h_bits(v[1]) << 16),
-                                        (uint32_t)f2h_bits(v[2]) | ((uint32_t)f2h_bits(v[3]) << 16)};
-            } else {
-                for (int i = 0; i < 4 && row + i < M; ++i) dst[i] = f2h_bits(v[i]);
+            for (int j = 0; j < TPU; ++j) {
+                const uint32_t x0 = j == 0 ? v[k].x : v[k].z, x1 = j == 0 ? v[k].y : v[k].w;
+                acc[j][0] += h2f(x0 & 0xffffu) * up[k];
+                acc[j][1] += h2f(x0 >> 16) * up[k];
+                acc[j][2] += h2f(x1 & 0xffffu) * up[k];
+                acc[j][3] += h2f(x1 >> 16) * up[k];
             }
         }
     }
+    const int64_t row = m0 + 16 * wr + 4 * (lane >> 4);
+    if (row >= q.M) return;
+#pragma unroll
+    for (int j = 0; j < TPU; ++j) {
+        const int64_t tok = n0 + 16 * (TPU * u + j) + (lane & 15);
+        if (tok >= a.N) continue;
+        uint16_t *dst = q.C + tok * q.ldc + row;
+        if (row + 4 <= q.M) {
+            *(u32x2 *)dst = (u32x2){(uint32_t)f2h_bits(acc[j][0]) | ((uint32_t)f2h_bits(acc[j][1]) << 16),
+                                    (uint32_t)f2h_bits(acc[j][2]) | ((uint32_t)f2h_bits(acc[j][3]) << 16)};
+        } else {
+            for (int e = 0; e < 4 && row + e < q.M; ++e) dst[e] = f2h_bits(acc[j][e]);
+        }
+    }
+}
+
+template <int F, int NB>
+hipError_t launch_snb(const uint8_t *A, const uint16_t *X, uint16_t *C, void *P, const RGemmPlan &p, int64_t M,
+                      int64_t N, int64_t K, int64_t ldc, hipStream_t s)
+{
+    const dim3 grid((unsigned)p.tiles_m, (unsigned)p.tiles_n, (unsigned)p.splits);
+    sgemm_kernel<F, NB><<<grid, dim3(64 * RW), 0, s>>>(A, X, C, (uint16_t *)P, M, N, K, ldc, tuning().rgemm_spol);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || p.splits == 1) return e;
+    return launch_gemm_reduce_f16(NB, RRG, (const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n);
 }
 
 template <int F, int NB, int AQ>
@@ -353,6 +617,110 @@ RGemmPlan plan_rgemm(int64_t M, int64_t N, int64_t K)
     p.partial_bytes = p.splits > 1 ? (size_t)p.splits * tiles * RBM * 16 * p.nb * 2 + (size_t)p.splits * tiles * RW * 4 : 0;
     p.ok = true;
     return p;
+}
+
+RGemmPlan plan_sgemm(int64_t M, int64_t N, int64_t K, int splits)
+{
+    RGemmPlan p;
+    if (M < 1 || N < 1 || K < 256 || K % 256 != 0) return p;
+    p.nb = N > 64 ? 8 : (N > 32 ? 4 : (N > 16 ? 2 : 1));
+    p.tiles_m = (int)((M + RBM - 1) / RBM);
+    p.tiles_n = (int)((N + 16 * p.nb - 1) / (16 * p.nb));
+    const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n, nsb = K / 256, cus = num_cus();
+    // as many splits as keep the grid within one round of the chip (each at least one super-block)
+    int64_t S = splits > 0 ? splits : (tiles >= cus ? 1 : cus / tiles);
+    if (S > nsb) S = nsb;
+    p.splits = (int)(S < 1 ? 1 : S);
+    p.partial_bytes = p.splits > 1 ? (size_t)p.splits * tiles * RBM * 16 * p.nb * 2 + (size_t)p.splits * tiles * RW * 4 : 0;
+    p.ok = true;
+    return p;
+}
+
+hipError_t launch_sgemm(int fmt, const uint8_t *A, const uint16_t *X, uint16_t *C, void *partials, const RGemmPlan &p,
+                        int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s)
+{
+    if (!p.ok) return hipErrorInvalidValue;
+#define GQ_SG_NB(F)                                                                                                       switch (p.nb) {                                                                                                       case 1: return launch_snb<F, 1>(A, X, C, partials, p, M, N, K, ldc, s);                                               case 2: return launch_snb<F, 2>(A, X, C, partials, p, M, N, K, ldc, s);                                               case 4: return launch_snb<F, 4>(A, X, C, partials, p, M, N, K, ldc, s);                                               case 8: return launch_snb<F, 8>(A, X, C, partials, p, M, N, K, ldc, s);                                               default: return hipErrorInvalidValue;                                                                                 }
+    switch (fmt) {
+    case Q8_0: GQ_SG_NB(Q8_0)
+    case Q4_K: GQ_SG_NB(Q4_K)
+    default: GQ_SG_NB(Q6_K)
+    }
+#undef GQ_SG_NB
+}
+
+SGroupPlan plan_sgemm_grouped(const SGroupItem *items, int n, int64_t N, int splits)
+{
+    SGroupPlan g;
+    if (n < 1 || n > kMaxSParts || N < 1) return g;
+    g.nb = N > 64 ? 8 : (N > 32 ? 4 : (N > 16 ? 2 : 1));
+    const int tn = (int)((N + 16 * g.nb - 1) / (16 * g.nb));
+    int64_t units = 0, tiles = 0, Lmax = 1;
+    for (int i = 0; i < n; ++i) {
+        if (items[i].M < 1 || items[i].K < 256 || items[i].K % 256 != 0) return g;
+        g.tiles_m[i] = (int)((items[i].M + RBM - 1) / RBM);
+        const int64_t t = (int64_t)g.tiles_m[i] * tn, nsb = items[i].K / 256;
+        units += t * nsb;
+        tiles += t;
+        Lmax = nsb > Lmax ? nsb : Lmax;
+    }
+    // the fewest super-blocks per workgroup L that keeps every part's (tiles x ceil(nsb / L))
+    // grid within one round of the chip: the work spread evenly, the splits (partials) fewest
+    const int64_t cus = num_cus();
+    int64_t L = (units + cus - 1) / cus;
+    if (L < 1) L = 1;
+    for (;; ++L) {
+        int64_t wg = 0;
+        for (int i = 0; i < n; ++i) wg += (int64_t)g.tiles_m[i] * tn * ((items[i].K / 256 + L - 1) / L);
+        if (wg <= cus || L >= Lmax) break;
+    }
+    int64_t wg0 = 0;
+    size_t pb = 0;
+    for (int i = 0; i < n; ++i) {
+        const int64_t nsb = items[i].K / 256;
+        int64_t S = splits > 0 ? splits : (nsb + L - 1) / L;
+        if (S > nsb) S = nsb;
+        g.splits[i] = (int)S;
+        g.wg0[i] = (int)wg0;
+        wg0 += (int64_t)g.tiles_m[i] * tn * S;
+        g.poff[i] = pb;
+        if (S > 1) pb += ((size_t)S * g.tiles_m[i] * tn * (RBM * 16 * g.nb * 2 + RW * 4) + 255) & ~(size_t)255;
+    }
+    g.tiles_n = tn;
+    g.blocks = (int)wg0;
+    g.partial_bytes = pb;
+    g.ok = true;
+    return g;
+}
+
+hipError_t launch_sgemm_grouped(const SGroupItem *items, int n, int64_t N, const SGroupPlan &g, void *partials,
+                                hipStream_t s)
+{
+    if (!g.ok) return hipErrorInvalidValue;
+    SParts a{};
+    RParts r{};
+    a.n = n;
+    a.N = N;
+    a.spol = tuning().rgemm_spol;
+    r.N = N;
+    int rb = 0;
+    constexpr int UPB = 256; // reduce: threads per workgroup
+    for (int i = 0; i < n; ++i) {
+        uint16_t *P = (uint16_t *)((uint8_t *)partials + g.poff[i]);
+        a.p[i] = SPart{items[i].fmt, items[i].A, items[i].X, items[i].C, P, items[i].M, items[i].K, items[i].ldc,
+                       g.tiles_m[i], g.tiles_n, g.splits[i], g.wg0[i]};
+        if (g.splits[i] > 1) {
+            const int tpu = g.nb == 1 ? 1 : 2, upt = RW * RRG * (g.nb / tpu) * 64, bpt = (upt + UPB - 1) / UPB;
+            r.p[r.n++] = RPart{P, items[i].C, items[i].M, items[i].ldc, g.tiles_m[i], g.tiles_n, g.splits[i], rb};
+            rb += g.tiles_m[i] * g.tiles_n * bpt;
+        }
+    }
+#define GQ_SGG(NB_)                                                                                                       case NB_:                                                                                                                 sgemm_grouped_kernel<NB_><<<dim3((unsigned)g.blocks), dim3(64 * RW), 0, s>>>(a);                                        if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;                                                    if (r.n > 0) reduce_grouped_kernel<NB_><<<dim3((unsigned)rb), dim3(UPB), 0, s>>>(r);                                   return hipGetLastError();
+    switch (g.nb) {
+        GQ_SGG(1) GQ_SGG(2) GQ_SGG(4) GQ_SGG(8)
+    default: return hipErrorInvalidValue;
+    }
+#undef GQ_SGG
 }
 
 hipError_t launch_rgemm(int fmt, int aq, const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, void *partials,

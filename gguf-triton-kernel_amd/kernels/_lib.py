@@ -38,6 +38,11 @@ class PrepItem(ctypes.Structure):
     _fields_ = [("B", _P), ("N", _I64), ("K", _I64), ("ldb", _I64), ("workspace", _P), ("workspace_bytes", _SZ)]
 
 
+class GemmItem(ctypes.Structure):
+    """gq_gemm_item (include/gguf_mmq.h)."""
+    _fields_ = [("type", ctypes.c_int), ("A", _P), ("ws", _P), ("C", _P), ("ldc", _I64), ("M", _I64), ("K", _I64)]
+
+
 SIGNATURES = {
     "gq_block_elems": ([_I], _I),
     "gq_block_bytes": ([_I], _I),
@@ -62,6 +67,8 @@ SIGNATURES = {
     "gq_mmq_grouped": ([ctypes.POINTER(GroupItem), _I, _I64, _P], _I),
     "gq_mmq_grouped_ex": ([_I, ctypes.POINTER(GroupItem), _I, _I64, _P], _I),
     "gq_act_prepare_grouped": ([_I, ctypes.POINTER(PrepItem), _I, _P], _I),
+    "gq_mmq_grouped_prepared_workspace_size": ([_I, ctypes.POINTER(GemmItem), _I, _I64], _SZ),
+    "gq_mmq_grouped_prepared": ([_I, ctypes.POINTER(GemmItem), _I, _I64, _P, _SZ, _P], _I),
     "gq_last_error": ([], ctypes.c_char_p),
     "gq_version": ([], _I),
     "gq_debug_set_tuning": ([ctypes.c_char_p, ctypes.c_longlong], _I),
@@ -266,6 +273,35 @@ def mmq_grouped(items, N: int, act: str = "q8_1"):
         arr[i] = GroupItem(gtype, A.data_ptr(), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, K)
     with torch.cuda.device(dev):
         rc = lib().gq_mmq_grouped_ex(ACTS[act], arr, len(items), N, torch.cuda.current_stream(dev).cuda_stream)
+    if rc == GQ_EUNSUPPORTED:
+        return None
+    _check(rc)
+    return outs
+
+
+def mmq_grouped_prepared(items, N: int, act: str = "q8_1"):
+    """One grouped streaming-GEMM launch (gq_mmq_grouped_prepared) for several prepared MMQs with
+    the same token count N: items = [(gtype, A, ws, M, K, out or None), ...], ws the workspace the
+    item's input was prepared into (act_prepare / act_prepare_grouped with this N, K, act).
+    Returns the (N, M) outputs, or None when the library reports the shapes unsupported (N < 5,
+    K % 256 != 0, > 16 items): nothing was launched then, call mmq_prepared per item."""
+    if not items:
+        return []
+    dev = items[0][1].device
+    arr = (GemmItem * len(items))()
+    outs = []
+    for i, (gtype, A, ws, M, K, out) in enumerate(items):
+        _check_weights(gtype, A, M, K)
+        if A.device != dev or ws.device != dev:
+            raise RuntimeError("grouped items must share one device")
+        C = _check_out(out, N, M, dev)
+        outs.append(C)
+        arr[i] = GemmItem(gtype, A.data_ptr(), ws.data_ptr(), C.data_ptr(), C.stride(0), M, K)
+    need = int(lib().gq_mmq_grouped_prepared_workspace_size(ACTS[act], arr, len(items), N))
+    part = torch.empty(need, dtype=torch.uint8, device=dev) if need else None
+    with torch.cuda.device(dev):
+        rc = lib().gq_mmq_grouped_prepared(ACTS[act], arr, len(items), N, part.data_ptr() if need else None, need,
+                                           torch.cuda.current_stream(dev).cuda_stream)
     if rc == GQ_EUNSUPPORTED:
         return None
     _check(rc)

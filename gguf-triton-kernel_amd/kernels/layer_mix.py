@@ -31,6 +31,8 @@ from . import _lib
 
 # grouped= setting -> the most tokens LayerMix runs as one grouped decode launch
 GROUPED_MAX_TOKENS = {"auto": 4, True: 4, False: 0}
+# grouped= setting -> the fewest tokens LayerMix runs as one grouped streaming-GEMM launch
+GEMM_GROUPED_MIN_TOKENS = {"auto": 17, True: 17, False: 1 << 62}
 
 
 class GGUFLinear:
@@ -60,6 +62,9 @@ class LayerMix:
         self.act = act  # "q8_1" (the reference's activation quantization) or "fp8" (e4m3 variant)
         # one gq_mmq_grouped launch for the whole layer: "auto" / True at 1..4 tokens, False never
         self.max_grouped = GROUPED_MAX_TOKENS[grouped]
+        # one gq_mmq_grouped_prepared launch (the streaming GEMM) for the whole layer from this
+        # many tokens ("auto" / True; False never)
+        self.min_gemm_grouped = GEMM_GROUPED_MIN_TOKENS[grouped]
         self.lin = {}     # name -> GGUFLinear (unfused projections)
         self.parts = {}   # name -> (fused key, first column, rows)
         # per input group: the calls to make, each (key, GGUFLinear); fused keys join names by "+"
@@ -152,10 +157,22 @@ class LayerMix:
                 preps.append((inp, N, inp.shape[1], ws))
                 wss.append(ws)
             _lib.act_prepare_grouped(preps, act=self.act)
-            for calls, inp, ws in zip(self.calls, inputs, wss):
-                for key, L in calls:
-                    res[key] = _lib.mmq_prepared(L.gtype, L.A, ws, L.M, N, inp.shape[1],
-                                                 self._out(key, L, N, inp.device, out), act=self.act)
+            outs = None
+            if N >= self.min_gemm_grouped:
+                # every call in ONE grouped streaming-GEMM launch (+ one split-K reduce launch)
+                keys, items = [], []
+                for calls, inp, ws in zip(self.calls, inputs, wss):
+                    for key, L in calls:
+                        keys.append(key)
+                        items.append((L.gtype, L.A, ws, L.M, inp.shape[1], self._out(key, L, N, inp.device, out)))
+                outs = _lib.mmq_grouped_prepared(items, N, act=self.act)
+                if outs is not None:
+                    res.update(zip(keys, outs))
+            if outs is None:
+                for calls, inp, ws in zip(self.calls, inputs, wss):
+                    for key, L in calls:
+                        res[key] = _lib.mmq_prepared(L.gtype, L.A, ws, L.M, N, inp.shape[1],
+                                                     self._out(key, L, N, inp.device, out), act=self.act)
             done = True
         if not done:
             for calls, inp in zip(self.calls, inputs):

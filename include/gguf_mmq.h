@@ -209,6 +209,32 @@ int gq_mmq_grouped(const gq_group_item *items, int n, int64_t N, void *stream);
  * bits and is GQ_EUNSUPPORTED (nothing launched) from N = 3. */
 int gq_mmq_grouped_ex(gq_act act, const gq_group_item *items, int n, int64_t N, void *stream);
 
+/*
+ * Grouped GEMM: several gq_mmq_prepared_ex calls with the same token count N (5 <= N) in ONE
+ * launch of the streaming 256-row MFMA GEMM (+ one launch summing the split-K partials), e.g.
+ * the seven projections of a transformer block at prefill (BASELINE.json configs[4]; no
+ * reference counterpart).  Item i: weights A (M x K of `type`, K % 256 == 0), ws = the
+ * workspace its input was prepared into by gq_act_prepare[_ex|_grouped](act, ..., N, K, ...)
+ * (items may share one), output C (N x M, row stride ldc).  The chip's workgroups are spread
+ * over the items' row tiles x super-blocks (each item split along K so that the whole launch is
+ * one round of the chip); with the split factor pinned (GQ_SGEMM_SPLITS) every item's output is
+ * bit-identical to its own gq_mmq_prepared_ex call on that kernel (GQ_SGEMM=1).  workspace: the
+ * split-K partials, >= gq_mmq_grouped_prepared_workspace_size() bytes (0 when nothing splits:
+ * NULL allowed).  GQ_EUNSUPPORTED (nothing launched) for N < 5, more than 16 items, K % 256 != 0
+ * or >= 2 GiB in one item: call gq_mmq_prepared_ex per item then.  No host sync.
+ */
+typedef struct gq_gemm_item {
+    gq_type type;
+    const void *A;
+    const void *ws;
+    void *C;
+    int64_t ldc;
+    int64_t M, K;
+} gq_gemm_item;
+size_t gq_mmq_grouped_prepared_workspace_size(gq_act act, const gq_gemm_item *items, int n, int64_t N);
+int gq_mmq_grouped_prepared(gq_act act, const gq_gemm_item *items, int n, int64_t N, void *workspace,
+                            size_t workspace_bytes, void *stream);
+
 /* Text of the last error on this thread ("" if none). */
 const char *gq_last_error(void);
 

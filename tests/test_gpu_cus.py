@@ -39,7 +39,7 @@ def test_smaller_cu_count_bit_identical(cus, tune):
     cases.append(("skinny", lambda: kl.mmq(kl.GQ_Q4_K, qs[0], x16, 4096, 16, 4096)))
     x128 = torch.from_numpy(random_activations(128, 4096, seed=128)).to(dev)
     cases.append(("gemm", lambda: kl.mmq(kl.GQ_Q8_0, qs[2], x128, 2048, 128, 4096)))
-    tune(GQ_GEMM_SPLITS=8, GQ_SKINNY_RG=1)  # the plans the count could change, pinned
+    tune(GQ_GEMM_SPLITS=8, GQ_SKINNY_RG=1, GQ_RGEMM=0)  # the plans the count could change, pinned
     ref = {name: _bits(fn()) for name, fn in cases}
     tune(GQ_CUS=cus)
     for name, fn in cases:

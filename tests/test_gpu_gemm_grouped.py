@@ -1,0 +1,165 @@
+"""GPU tests of the grouped streaming GEMM (gq_mmq_grouped_prepared, csrc/mmq_rgemm.hip
+sgemm_grouped_kernel + reduce_grouped_kernel): the projections of a layer, each of its own type,
+prepared activations and output, in ONE launch (plus one split-K reduce launch) at 5..767
+tokens.  Each projection bit for bit against its own per-matrix call at the same split (one split:
+gemm_kernel's MFMA sequence; four: the streaming kernel's own partials and reduce), the full
+Llama-7B Q4_K_M layer against the oracle at 16/128/512 tokens (sampled rows; TIGHT vs IDEAL,
+the reference's 1% gate vs EXACT), LayerMix's grouped route against its per-call route within
+the GEMM tolerance, and what the grouped form cannot take refused without launching."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from utils.synth import random_activations, random_blocks
+
+pytestmark = pytest.mark.gpu
+
+TIGHT = 4e-3
+
+
+def _dev():
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    return torch.device("cuda:0")
+
+
+def _layer(types, seed=0):
+    from gguf import LLAMA_LAYER_SHAPES
+    dev = _dev()
+    raw = {n: random_blocks(types[n], M, K, seed=seed + i) for i, (n, (M, K)) in enumerate(LLAMA_LAYER_SHAPES.items())}
+    return raw, {n: torch.from_numpy(raw[n].view(np.int8)).to(dev) for n in raw}
+
+
+def _prepare(kl, B, N, K, act="q8_1"):
+    ws = torch.empty(kl.workspace_size(kl.GQ_Q4_K, 256, N, K, act), dtype=torch.uint8, device=_dev())
+    kl.act_prepare(B, N, K, ws, act=act)
+    return ws
+
+
+def _layer_items(kl, N, layer=0, seed=0):
+    from gguf import LLAMA_LAYER_SHAPES, q4_k_m_layer_types
+    dev = _dev()
+    types = q4_k_m_layer_types(layer, 32)
+    raw, A = _layer(types, seed=seed)
+    x = random_activations(N, 4096, seed=seed + 1)
+    h = random_activations(N, 11008, seed=seed + 2)
+    wx = _prepare(kl, torch.from_numpy(x).to(dev), N, 4096)
+    wh = _prepare(kl, torch.from_numpy(h).to(dev), N, 11008)
+    items, names = [], []
+    for n, (M, K) in LLAMA_LAYER_SHAPES.items():
+        names.append(n)
+        items.append((kl.TYPES[types[n]], A[n], wh if K == 11008 else wx, M, K, None))
+    return types, raw, x, h, items, names
+
+
+@pytest.mark.parametrize("N", [5, 16, 40, 128, 200])
+@pytest.mark.parametrize("splits", [1, 4])
+def test_grouped_gemm_bit_identical_to_per_matrix(N, splits, tune):
+    """splits pinned: every projection = its own prepared call with the same split.  One split is
+    gemm_kernel's per-row MFMA sequence (GQ_SGEMM=0 GQ_GEMM_SPLITS=1); four the per-matrix
+    streaming kernel's (GQ_SGEMM=1 GQ_SGEMM_SPLITS=4), the grouped reduce = gemm_reduce_f16."""
+    import kernels._lib as kl
+    tune(GQ_SGEMM_SPLITS=splits)
+    types, raw, x, h, items, names = _layer_items(kl, N, layer=0, seed=N)
+    outs = kl.mmq_grouped_prepared(items, N)
+    assert outs is not None, kl.lib().gq_last_error()
+    torch.cuda.synchronize()
+    if splits == 1:
+        tune(GQ_SGEMM=0, GQ_RGEMM=0, GQ_WGEMM=0, GQ_SKINNY=0, GQ_GEMM_SPLITS=1)
+    else:
+        tune(GQ_SGEMM=1, GQ_RGEMM=0, GQ_SKINNY=0, GQ_SGEMM_SPLITS=splits)
+    for (t, A, ws, M, K, _), n, C in zip(items, names, outs):
+        solo = kl.mmq_prepared(t, A, ws, M, N, K)
+        torch.cuda.synchronize()
+        assert torch.equal(C.view(torch.int16), solo.view(torch.int16)), n
+
+
+@pytest.mark.parametrize("N", [16, 128, 512])
+def test_grouped_gemm_llama_layer_parity(N):
+    """The seven Llama-7B projections (layer 0: attn_v / ffn_down in Q6_K) in one grouped launch
+    at the automatic split plan, every projection on sampled rows against the oracle."""
+    import kernels._lib as kl
+    from gguf import LLAMA_LAYER_SHAPES
+    types, raw, x, h, items, names = _layer_items(kl, N, layer=0, seed=7 * N)
+    outs = kl.mmq_grouped_prepared(items, N)
+    assert outs is not None, kl.lib().gq_last_error()
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(N)
+    for n, C in zip(names, outs):
+        M, K = LLAMA_LAYER_SHAPES[n]
+        got = C.cpu().numpy()
+        assert np.isfinite(got.astype(np.float32)).all(), n
+        rows = np.sort(rng.choice(M, size=16, replace=False))
+        rb = raw[n].size // M
+        sub = np.concatenate([raw[n][r * rb:(r + 1) * rb] for r in rows])
+        B = h if K == 11008 else x
+        ideal = O.mmq_from_fp16(types[n], sub, B, len(rows), N, K, O.IDEAL)
+        assert O.max_rel_err(got[:, rows], ideal) <= TIGHT, n
+        exact = O.mmq_from_fp16(types[n], sub, B, len(rows), N, K, O.EXACT)
+        assert O.allclose(exact, got[:, rows], 0.01), n
+
+
+def test_grouped_gemm_ragged_strided_outputs():
+    """Ragged rows and uneven K per item, one shared prepared input, outputs written into column
+    ranges of one wide buffer (ldc > M): each range = the item's own call, the rest untouched."""
+    import kernels._lib as kl
+    dev = _dev()
+    N = 70
+    specs = [("q8_0", 333, 1024), ("q4_k", 1000, 2048), ("q6_k", 257, 1536), ("q4_k", 64, 2048), ("q8_0", 4096, 4096)]
+    ws = {K: _prepare(kl, torch.from_numpy(random_activations(N, K, seed=K)).to(dev), N, K) for K in {s[2] for s in specs}}
+    width = sum(M for _, M, _ in specs) + 5
+    buf = torch.full((N, width), -7.0, dtype=torch.float16, device=dev)
+    items, col, qs = [], 0, []
+    for i, (fmt, M, K) in enumerate(specs):
+        qA = torch.from_numpy(random_blocks(fmt, M, K, seed=i).view(np.int8)).to(dev)
+        qs.append(qA)
+        items.append((kl.TYPES[fmt], qA, ws[K], M, K, buf[:, col:col + M]))
+        col += M
+    with kl.Tuning(GQ_SGEMM_SPLITS=2):
+        outs = kl.mmq_grouped_prepared(items, N)
+        assert outs is not None, kl.lib().gq_last_error()
+        torch.cuda.synchronize()
+    with kl.Tuning(GQ_SGEMM=1, GQ_RGEMM=0, GQ_SKINNY=0, GQ_SGEMM_SPLITS=2):
+        col = 0
+        for (fmt, M, K), qA in zip(specs, qs):
+            solo = kl.mmq_prepared(kl.TYPES[fmt], qA, ws[K], M, N, K)
+            torch.cuda.synchronize()
+            assert torch.equal(buf[:, col:col + M].view(torch.int16), solo.view(torch.int16)), fmt
+            col += M
+    assert torch.all(buf[:, col:] == -7.0)
+
+
+def test_grouped_gemm_refuses():
+    """Decode sizes (1..4 tokens: the decode form's), K not a multiple of 256 and more than 16
+    items are refused (None), nothing launched, the outputs untouched."""
+    import kernels._lib as kl
+    dev = _dev()
+    qA = torch.from_numpy(random_blocks("q8_0", 64, 1024, seed=1).view(np.int8)).to(dev)
+    for N, K, n in ((4, 1024, 1), (8, 1056, 1), (8, 1024, 17)):
+        qK = qA if K == 1024 else torch.from_numpy(random_blocks("q8_0", 64, K, seed=2).view(np.int8)).to(dev)
+        ws = _prepare(kl, torch.from_numpy(random_activations(N, K, seed=3)).to(dev), N, K)
+        outs = [torch.full((N, 64), 3.0, dtype=torch.float16, device=dev) for _ in range(n)]
+        assert kl.mmq_grouped_prepared([(kl.GQ_Q8_0, qK, ws, 64, K, o) for o in outs], N) is None
+        torch.cuda.synchronize()
+        assert all(torch.all(o == 3.0) for o in outs)
+
+
+@pytest.mark.parametrize("N", [17, 128, 512])
+def test_layer_mix_grouped_gemm_route(N):
+    """LayerMix from 17 tokens runs the layer as one grouped GEMM launch: within the GEMM
+    tolerance of its per-call route (grouped=False), `out` buffers honoured."""
+    from gguf import LLAMA_LAYER_SHAPES, q4_k_m_layer_types
+    from kernels.layer_mix import GGUFLinear, LayerMix
+    dev = _dev()
+    types = q4_k_m_layer_types(0, 32)
+    _, A = _layer(types, seed=3)
+    lins = {n: GGUFLinear(types[n], A[n], M, K) for n, (M, K) in LLAMA_LAYER_SHAPES.items()}
+    x, a, y = (torch.from_numpy(random_activations(N, 4096, seed=s)).to(dev) for s in (5, 6, 7))
+    h = torch.from_numpy(random_activations(N, 11008, seed=8)).to(dev)
+    out = {n: torch.empty(N, M, dtype=torch.float16, device=dev) for n, (M, K) in LLAMA_LAYER_SHAPES.items()}
+    rg = LayerMix(lins, grouped=True, fuse=False).forward(x, h, attn=a, x_ffn=y, out=out)
+    ru = LayerMix(lins, grouped=False, fuse=False).forward(x, h, attn=a, x_ffn=y)
+    torch.cuda.synchronize()
+    for n in LLAMA_LAYER_SHAPES:
+        assert rg[n].data_ptr() == out[n].data_ptr(), n
+        assert O.max_rel_err(rg[n].cpu().numpy(), ru[n].cpu().numpy()) <= TIGHT, n

@@ -179,7 +179,8 @@ def test_act_prepare_grouped_matches_individual(act):
                                    (1, "fp8"), (2, "fp8"), (3, "fp8"), (8, "fp8"), (128, "fp8")])
 def test_layer_mix_prepared_matches_per_call(N, act):
     """LayerMix from 5 tokens (the four inputs quantized in one gq_act_prepare_grouped launch, every
-    projection prepared): unfused, every projection bit-identical to its own mmq(); fused (q+k and
+    projection prepared; grouped=False: one launch per projection, not the grouped GEMM of
+    tests/test_gpu_gemm_grouped.py): unfused, every projection bit-identical to its own mmq(); fused (q+k and
     gate+up as one taller matrix, whose split-K plan may differ from the parts') within the GEMM
     tolerance of the unfused result."""
     import kernels._lib as kl
@@ -193,7 +194,7 @@ def test_layer_mix_prepared_matches_per_call(N, act):
     a = torch.from_numpy(random_activations(N, 4096, seed=16)).to(dev)
     y = torch.from_numpy(random_activations(N, 4096, seed=17)).to(dev)
     h = torch.from_numpy(random_activations(N, 11008, seed=18)).to(dev)
-    res = LayerMix(lins, act=act, fuse=False).forward(x, h, attn=a, x_ffn=y)
+    res = LayerMix(lins, act=act, fuse=False, grouped=False).forward(x, h, attn=a, x_ffn=y)
     fused = LayerMix(lins, act=act).forward(x, h, attn=a, x_ffn=y)
     inp = {"attn_q": x, "attn_k": x, "attn_v": x, "attn_output": a, "ffn_gate": y, "ffn_up": y, "ffn_down": h}
     torch.cuda.synchronize()

@@ -115,3 +115,44 @@ def test_rgemm_headline_full_size():
     exact = O.mmq_from_fp16("q8_0", sub, B, len(rows), N, K, O.EXACT)
     assert O.allclose(exact, C[:, rows], 0.01)
     assert kl.lib() is not None
+
+
+# ---- the streaming form (sgemm_kernel): prepared x~, half-super-block stages through an LDS ring
+
+
+@pytest.mark.parametrize("fmt", FMTS)
+@pytest.mark.parametrize("M,N,K,S", [(600, 100, 4096, 0), (300, 128, 8192, 3), (257, 40, 2816, 0), (700, 20, 1024, 1),
+                                     (129, 17, 3072, 5), (1000, 64, 2048, 2)])
+def test_sgemm_parity(fmt, M, N, K, S, tune):
+    """Every format and token tile, ragged rows and tokens, uneven split lengths (S not dividing
+    the super-blocks), one split (no partials) and the automatic split."""
+    tune(GQ_RGEMM=0, GQ_SGEMM=1, GQ_SKINNY=0, GQ_SGEMM_SPLITS=S)
+    qA = random_blocks(fmt, M, K, seed=M + 2 * N + K)
+    B = random_activations(N, K, seed=5 * K + N)
+    C = _prepared(fmt, _t(qA.view(np.int8)), _t(B), M, N, K)
+    got = C.cpu().numpy()
+    assert np.isfinite(got.astype(np.float32)).all()
+    ideal = O.mmq_from_fp16(fmt, qA, B, M, N, K, O.IDEAL)
+    assert O.max_rel_err(got, ideal) <= TIGHT, O.max_rel_err(got, ideal)
+    exact = O.mmq_from_fp16(fmt, qA, B, M, N, K, O.EXACT)
+    assert O.allclose(exact, got, 0.01)
+
+
+@pytest.mark.parametrize("fmt", FMTS)
+def test_sgemm_bit_identities(fmt, tune):
+    """With one super-block per split the streaming form is the resident form (same partials,
+    same reduce): identical bits; with one split it is gemm_kernel's MFMA sequence per row."""
+    M, N, K = 520, 96, 2048
+    qA = random_blocks(fmt, M, K, seed=3)
+    B = random_activations(N, K, seed=4)
+    A_t, B_t = _t(qA.view(np.int8)), _t(B)
+    tune(GQ_RGEMM=1, GQ_SKINNY=0)
+    Cr = _prepared(fmt, A_t, B_t, M, N, K)
+    tune(GQ_RGEMM=0, GQ_SGEMM=1, GQ_SGEMM_SPLITS=K // 256)
+    Cs = _prepared(fmt, A_t, B_t, M, N, K)
+    assert torch.equal(Cr.view(torch.int16), Cs.view(torch.int16))
+    tune(GQ_SGEMM_SPLITS=1)
+    C1 = _prepared(fmt, A_t, B_t, M, N, K)
+    tune(GQ_SGEMM=0, GQ_WGEMM=0, GQ_GEMM_SPLITS=1)
+    C0 = _prepared(fmt, A_t, B_t, M, N, K)
+    assert torch.equal(C0.view(torch.int16), C1.view(torch.int16))

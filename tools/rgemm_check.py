@@ -18,7 +18,8 @@ import wgemm_check as W  # noqa: E402
 CONFIGS = dict(W.CONFIGS)
 CONFIGS.update({"q6_k_4096x4096_m128": ("q6_k", 4096, 4096, 128), "q8_0_4096x4096_m32": ("q8_0", 4096, 4096, 32),
                 "q4_k_4096x4096_m32": ("q4_k", 4096, 4096, 32), "q8_0_2048x4096_m128": ("q8_0", 2048, 4096, 128),
-                "q8_0_8192x4096_m128": ("q8_0", 8192, 4096, 128), "q4_k_4096x4096_m96": ("q4_k", 4096, 4096, 96)})
+                "q8_0_8192x4096_m128": ("q8_0", 8192, 4096, 128), "q4_k_4096x4096_m96": ("q4_k", 4096, 4096, 96),
+                "q8_0_11008x4096_m128": ("q8_0", 11008, 4096, 128), "q6_k_11008x4096_m128": ("q6_k", 11008, 4096, 128)})
 
 
 def main():
