@@ -754,10 +754,11 @@ def bench_layer(Ns, acts, steps, warmup, dev, fuse=True, grouped="auto"):
     attn_v and ffn_down in Q6_K, the rest Q4_K), shared inputs quantized once per group
     (kernels.layer_mix.LayerMix; fuse: q+k and gate+up as one call each), for each token count in
     Ns and activation format in acts ("q8_1": the reference's semantics; "fp8": the e4m3 variant).
-    Weights rotate over >= 1 GiB.  grouped: LayerMix's grouped-decode setting ("auto" / True: the
-    whole layer as one gq_mmq_grouped launch at 1..4 tokens; False: one launch per set)."""
+    Weights rotate over >= 1 GiB.  grouped: LayerMix's grouped setting ("auto" / True: the whole
+    layer as one gq_mmq_grouped launch at 1..4 tokens and one gq_mmq_grouped_prepared launch from
+    17 tokens; False: one launch per set)."""
     from gguf import LLAMA_LAYER_SHAPES, q4_k_m_layer_types
-    from kernels.layer_mix import GROUPED_MAX_TOKENS, GGUFLinear, LayerMix
+    from kernels.layer_mix import GEMM_GROUPED_MIN_TOKENS, GROUPED_MAX_TOKENS, GGUFLinear, LayerMix
     types = q4_k_m_layer_types(0, 32)
     one = {n: device_random_blocks(types[n], M, K, dev, seed=i) for i, (n, (M, K)) in enumerate(LLAMA_LAYER_SHAPES.items())}
     layer_bytes = sum(t.numel() for t in one.values())
@@ -796,6 +797,7 @@ def bench_layer(Ns, acts, steps, warmup, dev, fuse=True, grouped="auto"):
             t = timed_rotation(grs, dev) / steps
             res.append({"config": f"q4_k_m_llama7b_layer_m{N}", "act": act, "fused": fuse,
                         "grouped": act == "q8_1" and N <= GROUPED_MAX_TOKENS[grouped],
+                        "gemm_grouped": N >= GEMM_GROUPED_MIN_TOKENS[grouped],
                         "fmt": "q4_k+q6_k", "M_tok": N,
                         "us_per_step": round(t * 1e6, 2), "tflops": round(flops / t / 1e12, 3),
                         "weight_GBps": round(layer_bytes / t / 1e9, 1)})
@@ -969,8 +971,8 @@ def main():
     torch.cuda.set_device(dev)
     if args.layer_only:
         Ns = (1, 2, 4, 8, 16, 32, 64, 128, 256, 512)
-        print(json.dumps([bench_layer(Ns, ("q8_1",), max(20, args.steps // 4), args.warmup, dev, fuse=f)
-                          for f in (True, False)]), flush=True)
+        print(json.dumps([bench_layer(Ns, ("q8_1",), max(20, args.steps // 4), args.warmup, dev, fuse=f, grouped=g)
+                          for f in (True, False) for g in ("auto", False)]), flush=True)
         return
     name = args.config
     fmt, M, K, N = CONFIGS[name]

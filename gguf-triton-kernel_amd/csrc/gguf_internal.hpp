@@ -16,6 +16,7 @@ struct Tuning {
     int fused_decode = 1;                     // GQ_NO_FUSED_DECODE=1 -> 0
     int decode_maxnt = 0;                     // GQ_DECODE_MAXNT: token-group cap of the fused decode (0: auto)
     int decode_nt4_cache = 1;                 // GQ_DECODE_NT4_CACHE
+    int decode_early = -1;                    // GQ_DECODE_EARLY: ring refill vs quantization (-1: auto)
     int decode_q6_img = -1;                   // GQ_DECODE_Q6_IMG: Q6_K aligned ring image (-1: K <= 4096)
     int gemm_aq = 1;                          // GQ_GEMM_AQ: in-kernel quantization of 16/32-token tiles
     int gemm_aq_nb4 = 0;                      // GQ_GEMM_AQ_NB4
@@ -38,7 +39,7 @@ struct Tuning {
     int rgemm = -1;                           // GQ_RGEMM: resident-split GEMM -1 auto / 0 off / 1 wherever it applies
     int sgemm = -1;                           // GQ_SGEMM: streaming 256-row GEMM -1 auto / 0 off / 1 wherever it applies
     int sgemm_splits = 0;                     // GQ_SGEMM_SPLITS (0: auto)
-    int rgemm_spol = 0;                       // GQ_RGEMM_SPOL: its partial stores' cache policy 0 / 2 (nt) / 16 (sc1)
+    int rgemm_spol = 16;                      // GQ_RGEMM_SPOL: its partial stores' cache policy 0 / 2 (nt) / 16 (sc1)
     int cus = 0;                              // GQ_CUS: compute units to plan for (0: the device's count)
     int ablate = 0;                           // GQ_ABLATE (GQ_ABLATION diagnostic builds only)
 };

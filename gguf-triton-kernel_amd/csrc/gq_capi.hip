@@ -38,6 +38,10 @@ bool parse_key(Tuning &t, const char *key, long long v)
         if (v < 0 || v > 8) return false;
         t.decode_maxnt = (int)v;
     } else if (k == "GQ_DECODE_NT4_CACHE") t.decode_nt4_cache = v != 0;
+    else if (k == "GQ_DECODE_EARLY") {
+        if (!in({-1, 0, 1, 2})) return false;
+        t.decode_early = (int)v;
+    }
     else if (k == "GQ_DECODE_Q6_IMG") {
         if (!in({-1, 0, 1})) return false;
         t.decode_q6_img = (int)v;
@@ -238,7 +242,7 @@ int64_t gemm_toks_per_launch(int64_t N, int64_t K)
 // Q6_K stay on the LDS-DMA GEMM (4096^2 x128 Q8_0 20.8 vs 17.3; Q6_K 28672x8192 x128 115.6 vs
 // 111.9).
 constexpr int64_t kWgemmMinTokens = 33;
-constexpr int64_t kRgemmMinTokens = 17;
+constexpr int64_t kRgemmMinTokens = 5;
 bool use_wgemm(int t, int form, int64_t N)
 {
     const int w = gq::tuning().wgemm;
@@ -300,6 +304,15 @@ bool use_rgemm(int t, int form, int64_t M, int64_t N, int64_t K)
     if (gq::tuning().gemm_splits > 0 || N < kRgemmMinTokens) return false;
     const int64_t grid = (int64_t)p.tiles_m * p.tiles_n * p.splits, cus = gq::num_cus();
     return grid <= cus && 2 * grid >= cus;
+}
+
+// The resident GEMM where it applies, ahead of the skinny kernel (4096^2 x16 step: Q4_K 6.8 vs
+// 9.7 us, Q8_0 7.8 vs 11.2, Q6_K 8.1 vs 12.9; x8 Q4_K 6.8 vs 9.3 -- profiles/r04/rg_small.txt)
+// unless the skinny kernel is forced (GQ_SKINNY=1)
+bool rgemm_route(int t, int form, int64_t M, int64_t N, int64_t K, int act)
+{
+    if (!use_rgemm(t, form, M, N, K)) return false;
+    return gq::tuning().skinny != 1 || !use_skinny(t, form, N, act);
 }
 
 // Streaming 256-row GEMM (mmq_rgemm.hip sgemm_kernel) on the prepared x~: GQ_SGEMM=1 wherever
@@ -605,13 +618,13 @@ static int compute(gq_type t, int act, const void *A, void *workspace, size_t wo
         // (the kernel is chosen by the call's token count: every chunk runs the same arithmetic)
         // (<= 32 skinny tokens are never cut: their x~ is far below the guard, and the token
         // count sets the kernel's K split)
-        if (!use_skinny(t, r.form, N, act) && use_rgemm(t, r.form, M, N, K)) {
+        if (rgemm_route(t, r.form, M, N, K, act)) {
             e = gq::launch_rgemm(t, 0, (const uint8_t *)A, c.xdeq, K, (uint16_t *)C, c.partials, gq::plan_rgemm(M, N, K),
                                  M, N, K, ldc, s);
             if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (rgemm): %s", hipGetErrorString(e));
             return GQ_OK;
         }
-        if (!use_skinny(t, r.form, N, act) && use_sgemm(t, r.form, M, N, K)) {
+        if (!rgemm_route(t, r.form, M, N, K, act) && !use_skinny(t, r.form, N, act) && use_sgemm(t, r.form, M, N, K)) {
             e = gq::launch_sgemm(t, (const uint8_t *)A, c.xdeq, (uint16_t *)C, c.partials, sgemm_plan(M, N, K), M, N, K,
                                  ldc, s);
             if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (sgemm): %s", hipGetErrorString(e));
@@ -670,7 +683,7 @@ int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int6
         if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (decode): %s", hipGetErrorString(e));
         return GQ_OK;
     }
-    if (!use_skinny(t, r.form, N, act) && use_rgemm(t, r.form, M, N, K) && ldb % 8 == 0 &&
+    if (rgemm_route(t, r.form, M, N, K, act) && ldb % 8 == 0 &&
         ((uintptr_t)B & 15) == 0) {
         // one launch (+ the split-K reduce): the activations quantized inside the GEMM (q8_1, or
         // the fp8 variant's e4m3), bit-identical to the act_quant forms it would read

@@ -91,6 +91,8 @@ struct DecodeGeom {
     int nseg;    // segments per row
     int segu;    // units per segment (nseg > 1; a multiple of 64)
     int lp2;     // log2(P): lanes per row
+    int early;   // ring slots 1.. issued: 0 after the quantization, 1 once the activations
+                 // arrived (under the quantization), 2 with task 0 (ahead of the arrival)
 };
 
 // byte offset of unit u (64 elements) within a row
@@ -351,26 +353,32 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
 
     u32x4 xv[XP];
     load_x(0, xv);
-    // Task 0 goes out with the activation loads; the rest of the ring once the activations are
-    // quantized (issued together, they queue the activations behind twice the weight traffic,
-    // and a small matrix waits on exactly that latency).  Task 0 always issues (past the
+    // Task 0 goes out with the activation loads; by default (early = 0) the rest of the ring
+    // once the activations are quantized (issued together, they queue the activations behind
+    // twice the weight traffic, and a small matrix waits on exactly that latency); long rows
+    // (early = 1, 2) refill under the quantization instead.  Task 0 always issues (past the
     // wave's tasks: an offset beyond the buffer -- zeros, no memory access), so the wait below
-    // for the activations, the older loads, is a fixed vmcnt(NI).
+    // for the activations, the older loads, is a fixed vmcnt.
     issue(0);
+    auto issue_rest = [&]() {
 #pragma unroll
-    for (int q = 0; q < XP; ++q) asm volatile("" ::"v"(xv[q].x), "v"(xv[q].y), "v"(xv[q].z), "v"(xv[q].w)); // waits vmcnt(NI)
+        for (int j = 1; j < NS; ++j)
+            if (j < ntask) issue(j);
+    };
+    if (geo.early == 2) issue_rest();
+#pragma unroll
+    for (int q = 0; q < XP; ++q) asm volatile("" ::"v"(xv[q].x), "v"(xv[q].y), "v"(xv[q].z), "v"(xv[q].w)); // waits for the x loads
 #ifdef GQ_DECODE_STAMPS
     const unsigned long long t_xw = __builtin_amdgcn_s_memtime();
 #endif
+    if (geo.early == 1) issue_rest();
     quantize(0, xv);
     for (int r = 1; r < xrounds; ++r) { // long activations: further rounds (their loads wait behind the DMAs)
         u32x4 xr[XP];
         load_x(r, xr);
         quantize(r, xr);
     }
-#pragma unroll
-    for (int j = 1; j < NS; ++j)
-        if (j < ntask) issue(j);
+    if (geo.early == 0) issue_rest();
     int issued = NS < ntask ? NS : ntask;
     int gc = g_begin, sc = 0; // task being multiplied
 #ifdef GQ_DECODE_STAMPS
@@ -724,6 +732,7 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p, int wgs = 0)
     if (p.nt == 4 && units == 1 && tuning().decode_nt4_cache)
         p.itc = 1;
     if (p.fp8) p.itc = 0;
+    g.early = tuning().decode_early >= 0 ? tuning().decode_early : 0;
     const int64_t waves = g.ngroups < W ? g.ngroups : W;
     p.grid = (int)((waves + DW - 1) / DW);
     return true;

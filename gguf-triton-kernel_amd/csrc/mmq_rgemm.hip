@@ -247,7 +247,6 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
     __shared__ __attribute__((aligned(1024))) uint8_t lds[G::LDS];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int g = lane >> 4, l16 = lane & 15;
     const int64_t m0 = (int64_t)blockIdx.x * RBM, n0 = (int64_t)blockIdx.y * G::BN, sb = blockIdx.z;
     const int64_t row_bytes = (K / Layout<F>::QK) * Layout<F>::BYTES;
     uint8_t *const ximg = lds + G::X_OFF;
@@ -355,6 +354,10 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
 // lands -> barrier -> stage j+NS-1 is issued into the slot stage j-1 left -> stage j is multiplied.
 // For the matrices whose row tiles x super-blocks exceed one round of the chip (the 70B Q6_K
 // matrices, 11008-row Q4_K); split-K partials as rgemm_kernel's.
+#ifndef GQ_SGEMM_NSMAX
+#define GQ_SGEMM_NSMAX 6
+#endif
+constexpr int SG_NSMAX = GQ_SGEMM_NSMAX; // ring slots at most (A/B builds: -DGQ_SGEMM_NSMAX=n)
 template <int F, int NB> struct SCfg {
     static constexpr int BN = 16 * NB;
     static constexpr int NPH = HImg<F>::NPH, HRB = 16 * NPH, SB = Layout<F>::BYTES * (256 / Layout<F>::QK);
@@ -364,7 +367,7 @@ template <int F, int NB> struct SCfg {
     static constexpr int XH_INSTR = X_BYTES / 1024, NXH = (XH_INSTR + RW - 1) / RW;
     static constexpr int NPS = NWH + NXH; // DMA instructions per wave and stage
     static constexpr bool PAD = WH_INSTR % RW != 0 || XH_INSTR % RW != 0 || XH_INSTR < RW;
-    static constexpr int NS = (LDS_CAP - 1024) / SLOT > 4 ? 4 : (LDS_CAP - 1024) / SLOT; // ring slots
+    static constexpr int NS = (LDS_CAP - 1024) / SLOT > SG_NSMAX ? SG_NSMAX : (LDS_CAP - 1024) / SLOT; // ring slots
     static constexpr int SCRATCH = NS * SLOT;
     static constexpr int LDS = SCRATCH + (PAD ? 1024 : 0);
     static_assert(NS >= 2, "two ring slots");
@@ -655,18 +658,23 @@ SGroupPlan plan_sgemm_grouped(const SGroupItem *items, int n, int64_t N, int spl
     if (n < 1 || n > kMaxSParts || N < 1) return g;
     g.nb = N > 64 ? 8 : (N > 32 ? 4 : (N > 16 ? 2 : 1));
     const int tn = (int)((N + 16 * g.nb - 1) / (16 * g.nb));
-    int64_t units = 0, tiles = 0, Lmax = 1;
+    int64_t units = 0, Lmax = 1;
     for (int i = 0; i < n; ++i) {
         if (items[i].M < 1 || items[i].K < 256 || items[i].K % 256 != 0) return g;
         g.tiles_m[i] = (int)((items[i].M + RBM - 1) / RBM);
         const int64_t t = (int64_t)g.tiles_m[i] * tn, nsb = items[i].K / 256;
         units += t * nsb;
-        tiles += t;
         Lmax = nsb > Lmax ? nsb : Lmax;
     }
     // the fewest super-blocks per workgroup L that keeps every part's (tiles x ceil(nsb / L))
-    // grid within one round of the chip: the work spread evenly, the splits (partials) fewest
+    // grid within one round of the chip: the work spread evenly, the splits (partials) fewest.
+    // More tiles than the chip holds (a 7B layer from ~200 tokens): not a grouped shape -- the
+    // rounds' tails cost more than the launches saved (layer x256 317 vs 211 us per call,
+    // profiles/r04/layer.txt)
     const int64_t cus = num_cus();
+    int64_t tiles = 0;
+    for (int i = 0; i < n; ++i) tiles += (int64_t)g.tiles_m[i] * tn;
+    if (tiles > cus) return g;
     int64_t L = (units + cus - 1) / cus;
     if (L < 1) L = 1;
     for (;; ++L) {

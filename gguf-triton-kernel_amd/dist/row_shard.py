@@ -121,7 +121,12 @@ class RowShardedMMQ:
         """The step in `chunks` row chunks of the shard (pipeline the all-gather):
         chunk c's local MMQ, then its all_gather issued asynchronously (on a GPU it runs on the
         collective's stream under chunk c+1's compute), each gathered chunk placed into its
-        column range of every rank's part; same values as one un-chunked step."""
+        column range of every rank's part.  Values: at decode sizes (1..4 tokens) and on the
+        skinny route bit-identical to one un-chunked step (a row's arithmetic depends on K and the
+        token count only); on the GEMM routes (LDS-DMA, weight-register, resident / streaming
+        split-K) the split-K factor -- and the route itself -- follow the chunk's row count, so a
+        chunk sums K in another order: equal within the GEMM tolerance, bit-identical only with
+        split-K pinned (GQ_GEMM_SPLITS=1 GQ_WGEMM_SPLITS=1 GQ_RGEMM=0, as the GPU tests do)."""
         if not dist.is_initialized() and self.world != 1:
             raise RuntimeError("pipelined() needs an initialised process group for world > 1")
         qk, nbytes = BLOCK[self.fmt]

@@ -30,8 +30,9 @@ def _layer(types, seed=0):
     return raw, {n: torch.from_numpy(raw[n].view(np.int8)).to(dev) for n in raw}
 
 
-def _prepare(kl, B, N, K, act="q8_1"):
-    ws = torch.empty(kl.workspace_size(kl.GQ_Q4_K, 256, N, K, act), dtype=torch.uint8, device=_dev())
+def _prepare(kl, B, N, K, act="q8_1", need=None):
+    need = need if need is not None else kl.workspace_size(kl.GQ_Q4_K, 256, N, K, act)
+    ws = torch.empty(need, dtype=torch.uint8, device=_dev())
     kl.act_prepare(B, N, K, ws, act=act)
     return ws
 
@@ -43,16 +44,18 @@ def _layer_items(kl, N, layer=0, seed=0):
     raw, A = _layer(types, seed=seed)
     x = random_activations(N, 4096, seed=seed + 1)
     h = random_activations(N, 11008, seed=seed + 2)
-    wx = _prepare(kl, torch.from_numpy(x).to(dev), N, 4096)
-    wh = _prepare(kl, torch.from_numpy(h).to(dev), N, 11008)
-    items, names = [], []
+    xt, ht = torch.from_numpy(x).to(dev), torch.from_numpy(h).to(dev)
+    wx = _prepare(kl, xt, N, 4096)
+    wh = _prepare(kl, ht, N, 11008)
+    items, names, inputs = [], [], []
     for n, (M, K) in LLAMA_LAYER_SHAPES.items():
         names.append(n)
         items.append((kl.TYPES[types[n]], A[n], wh if K == 11008 else wx, M, K, None))
-    return types, raw, x, h, items, names
+        inputs.append(ht if K == 11008 else xt)
+    return types, raw, x, h, items, names, inputs
 
 
-@pytest.mark.parametrize("N", [5, 16, 40, 128, 200])
+@pytest.mark.parametrize("N", [5, 16, 40, 128])
 @pytest.mark.parametrize("splits", [1, 4])
 def test_grouped_gemm_bit_identical_to_per_matrix(N, splits, tune):
     """splits pinned: every projection = its own prepared call with the same split.  One split is
@@ -60,7 +63,7 @@ def test_grouped_gemm_bit_identical_to_per_matrix(N, splits, tune):
     streaming kernel's (GQ_SGEMM=1 GQ_SGEMM_SPLITS=4), the grouped reduce = gemm_reduce_f16."""
     import kernels._lib as kl
     tune(GQ_SGEMM_SPLITS=splits)
-    types, raw, x, h, items, names = _layer_items(kl, N, layer=0, seed=N)
+    types, raw, x, h, items, names, inputs = _layer_items(kl, N, layer=0, seed=N)
     outs = kl.mmq_grouped_prepared(items, N)
     assert outs is not None, kl.lib().gq_last_error()
     torch.cuda.synchronize()
@@ -68,7 +71,9 @@ def test_grouped_gemm_bit_identical_to_per_matrix(N, splits, tune):
         tune(GQ_SGEMM=0, GQ_RGEMM=0, GQ_WGEMM=0, GQ_SKINNY=0, GQ_GEMM_SPLITS=1)
     else:
         tune(GQ_SGEMM=1, GQ_RGEMM=0, GQ_SKINNY=0, GQ_SGEMM_SPLITS=splits)
-    for (t, A, ws, M, K, _), n, C in zip(items, names, outs):
+    for (t, A, _, M, K, _), n, C, B in zip(items, names, outs, inputs):
+        ws = torch.empty(kl.workspace_size(t, M, N, K), dtype=torch.uint8, device=_dev())  # (+ this route's partials)
+        kl.act_prepare(B, N, K, ws)
         solo = kl.mmq_prepared(t, A, ws, M, N, K)
         torch.cuda.synchronize()
         assert torch.equal(C.view(torch.int16), solo.view(torch.int16)), n
@@ -77,11 +82,21 @@ def test_grouped_gemm_bit_identical_to_per_matrix(N, splits, tune):
 @pytest.mark.parametrize("N", [16, 128, 512])
 def test_grouped_gemm_llama_layer_parity(N):
     """The seven Llama-7B projections (layer 0: attn_v / ffn_down in Q6_K) in one grouped launch
-    at the automatic split plan, every projection on sampled rows against the oracle."""
+    at the automatic split plan (16, 128 tokens; at 512 the layer's 664 tiles exceed one round of
+    the chip: refused, and LayerMix's per-call route is what runs), every projection on sampled
+    rows against the oracle."""
     import kernels._lib as kl
     from gguf import LLAMA_LAYER_SHAPES
-    types, raw, x, h, items, names = _layer_items(kl, N, layer=0, seed=7 * N)
+    from kernels.layer_mix import GGUFLinear, LayerMix
+    types, raw, x, h, items, names, inputs = _layer_items(kl, N, layer=0, seed=7 * N)
     outs = kl.mmq_grouped_prepared(items, N)
+    if N == 512:
+        assert outs is None
+        lins = {n: GGUFLinear(types[n], A, M, K) for n, (_, A, _, M, K, _) in zip(names, items)}
+        xt = inputs[0]
+        ht = inputs[names.index("ffn_down")]
+        res = LayerMix(lins, fuse=False).forward(xt, ht, attn=xt, x_ffn=xt)
+        outs = [res[n] for n in names]
     assert outs is not None, kl.lib().gq_last_error()
     torch.cuda.synchronize()
     rng = np.random.default_rng(N)
@@ -106,7 +121,8 @@ def test_grouped_gemm_ragged_strided_outputs():
     dev = _dev()
     N = 70
     specs = [("q8_0", 333, 1024), ("q4_k", 1000, 2048), ("q6_k", 257, 1536), ("q4_k", 64, 2048), ("q8_0", 4096, 4096)]
-    ws = {K: _prepare(kl, torch.from_numpy(random_activations(N, K, seed=K)).to(dev), N, K) for K in {s[2] for s in specs}}
+    X = {K: torch.from_numpy(random_activations(N, K, seed=K)).to(dev) for K in {s[2] for s in specs}}
+    ws = {K: _prepare(kl, X[K], N, K) for K in X}
     width = sum(M for _, M, _ in specs) + 5
     buf = torch.full((N, width), -7.0, dtype=torch.float16, device=dev)
     items, col, qs = [], 0, []
@@ -122,7 +138,8 @@ def test_grouped_gemm_ragged_strided_outputs():
     with kl.Tuning(GQ_SGEMM=1, GQ_RGEMM=0, GQ_SKINNY=0, GQ_SGEMM_SPLITS=2):
         col = 0
         for (fmt, M, K), qA in zip(specs, qs):
-            solo = kl.mmq_prepared(kl.TYPES[fmt], qA, ws[K], M, N, K)
+            wsi = _prepare(kl, X[K], N, K, need=kl.workspace_size(kl.TYPES[fmt], M, N, K))  # (+ partials)
+            solo = kl.mmq_prepared(kl.TYPES[fmt], qA, wsi, M, N, K)
             torch.cuda.synchronize()
             assert torch.equal(buf[:, col:col + M].view(torch.int16), solo.view(torch.int16)), fmt
             col += M
@@ -130,8 +147,9 @@ def test_grouped_gemm_ragged_strided_outputs():
 
 
 def test_grouped_gemm_refuses():
-    """Decode sizes (1..4 tokens: the decode form's), K not a multiple of 256 and more than 16
-    items are refused (None), nothing launched, the outputs untouched."""
+    """Decode sizes (1..4 tokens: the decode form's), K not a multiple of 256, more than 16
+    items and more tiles than one round of the chip are refused (None), nothing launched, the
+    outputs untouched."""
     import kernels._lib as kl
     dev = _dev()
     qA = torch.from_numpy(random_blocks("q8_0", 64, 1024, seed=1).view(np.int8)).to(dev)
@@ -142,6 +160,14 @@ def test_grouped_gemm_refuses():
         assert kl.mmq_grouped_prepared([(kl.GQ_Q8_0, qK, ws, 64, K, o) for o in outs], N) is None
         torch.cuda.synchronize()
         assert all(torch.all(o == 3.0) for o in outs)
+    M, K, N = 257 * 256, 256, 16  # 257 row tiles
+    qB = torch.from_numpy(random_blocks("q8_0", M, K, seed=4).view(np.int8)).to(dev)
+    ws = _prepare(kl, torch.from_numpy(random_activations(N, K, seed=5)).to(dev), N, K)
+    out = torch.full((N, M), 3.0, dtype=torch.float16, device=dev)
+    with kl.Tuning(GQ_CUS=256):
+        assert kl.mmq_grouped_prepared([(kl.GQ_Q8_0, qB, ws, M, K, out)], N) is None
+    torch.cuda.synchronize()
+    assert torch.all(out == 3.0)
 
 
 @pytest.mark.parametrize("N", [17, 128, 512])

@@ -344,6 +344,28 @@ def test_row_sharded_pipelined_world1(fmt, M, N, K, chunks, tune):
     assert torch.equal(got.view(torch.int16), want.view(torch.int16))
 
 
+@pytest.mark.parametrize("fmt,M,N,K,chunks", [("q6_k", 1000, 1, 8192, 3), ("q4_k", 4096, 128, 4096, 4),
+                                               ("q8_0", 4096, 128, 4096, 2), ("q6_k", 2048, 64, 4096, 3)])
+def test_row_sharded_pipelined_default_tuning(fmt, M, N, K, chunks):
+    """pipelined() with the library's default routing: a row chunk may take another GEMM route
+    or split-K factor than the whole matrix (dist/row_shard.py pipelined), so the values agree
+    within the GEMM tolerance (fp16 partials), bit for bit at decode sizes."""
+    import oracle as O
+    from dist.row_shard import RowShardedMMQ
+    from kernels._lib import TYPES, mmq
+    dev = _dev()
+    qA = random_blocks(fmt, M, K, seed=M + 5)
+    A_t = torch.from_numpy(qA.view(np.int8)).to(dev)
+    B_t = torch.from_numpy(random_activations(N, K, seed=K + 1)).to(dev)
+    want = mmq(TYPES[fmt], A_t, B_t, M, N, K)
+    got = RowShardedMMQ(fmt, A_t, M, K, world=1, rank=0).pipelined(B_t, N, chunks)
+    torch.cuda.synchronize()
+    if N <= 4:
+        assert torch.equal(got.view(torch.int16), want.view(torch.int16))
+    else:
+        assert O.max_rel_err(got.cpu().numpy(), want.cpu().numpy()) <= 4e-3
+
+
 @pytest.mark.parametrize("fmt,M,N,K", [("q6_k", 1000, 1, 8192), ("q4_k", 4096, 128, 4096), ("q8_0", 300, 16, 1024)])
 def test_mmq_sharded_entry_point_world1(fmt, M, N, K):
     """gq_mmq_sharded through the C ABI at world 1 (no communicator): the same bits as gq_mmq."""

@@ -22,26 +22,39 @@ CONFIGS.update({"q6_k_4096x4096_m128": ("q6_k", 4096, 4096, 128), "q8_0_4096x409
                 "q8_0_11008x4096_m128": ("q8_0", 11008, 4096, 128), "q6_k_11008x4096_m128": ("q6_k", 11008, 4096, 128)})
 
 
+def parse_cfg(name):
+    """A CONFIGS name, or any "<fmt>_<M>x<K>_m<N>" (e.g. q6_k_28672x8192_m2)."""
+    if name in CONFIGS:
+        return CONFIGS[name]
+    fmt, mk, n = name.rsplit("_", 2)
+    M, K = (int(v) for v in mk.split("x"))
+    return fmt, M, K, int(n[1:])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="q8_0_4096x4096_m128,q4_k_4096x4096_m128,q6_k_4096x4096_m128,"
                                           "q8_0_4096x4096_m64,q4_k_4096x4096_m64,q8_0_4096x4096_m32")
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--variants", default="rgemm=GQ_RGEMM:1,old=GQ_RGEMM:0")
-    ap.add_argument("--libs", default=None, help="name=path,... : time GQ_RGEMM=1 in each build (ablations)")
+    ap.add_argument("--libs", default=None,
+                    help="name=path,... : time each build (ablations) under the first --variants entry "
+                         "(default GQ_RGEMM=1)")
     ap.add_argument("--steps-only", action="store_true", help="time the step (gq_mmq) only")
     a = ap.parse_args()
     if a.libs:  # one process per build would cost minutes: load each .so under its own handle
         import kernels._lib as kl
+        v0 = a.variants.split(",")[0].split("=", 1)[1]
+        lcfg = {k: int(x) for k, x in (p.split(":") for p in v0.split("+"))}
         for name in a.configs.split(","):
-            fmt, M, K, N = CONFIGS[name]
+            fmt, M, K, N = parse_cfg(name)
             row = {"config": name}
             for spec in a.libs.split(","):
                 lname, path = spec.split("=")
                 kl._lib, kl._mmq_ex, kl.LIB_PATH = None, None, path
                 kl._call_ws.clear()
                 for prep in ((False,) if a.steps_only else (True, False)):
-                    us = min(W.time_cfg(fmt, M, K, N, torch.device("cuda:0"), dict(GQ_RGEMM=1), prepared=prep)
+                    us = min(W.time_cfg(fmt, M, K, N, torch.device("cuda:0"), lcfg, prepared=prep)
                              for _ in range(a.rounds))
                     row[lname + ("_mmq" if prep else "_step")] = round(us, 2)
             print(json.dumps(row), flush=True)
@@ -53,12 +66,12 @@ def main():
         cfg = {k: int(x) for k, x in (p.split(":") for p in kv.split("+"))}
         variants.append((name, cfg))
     for name in a.configs.split(","):
-        fmt, M, K, N = CONFIGS[name]
+        fmt, M, K, N = parse_cfg(name)
         flops = 2.0 * M * N * K
         row = {"config": name}
         for r in range(a.rounds):
             for vname, cfg in variants:
-                for prep in (True, False):
+                for prep in ((False,) if a.steps_only else (True, False)):
                     us = W.time_cfg(fmt, M, K, N, dev, cfg, prepared=prep)
                     key = vname + ("_mmq" if prep else "_step")
                     row[key] = min(row.get(key, 1e9), round(us, 2))
