@@ -16,6 +16,7 @@ struct Tuning {
     int fused_decode = 1;                     // GQ_NO_FUSED_DECODE=1 -> 0
     int decode_maxnt = 0;                     // GQ_DECODE_MAXNT: token-group cap of the fused decode (0: auto)
     int decode_nt4_cache = 1;                 // GQ_DECODE_NT4_CACHE
+    int decode_f8_itc = 1;                    // GQ_DECODE_F8_ITC: fp8 decode keeps x~ in registers at one token
     int decode_early = -1;                    // GQ_DECODE_EARLY: ring refill vs quantization (-1: auto)
     int decode_q6_img = -1;                   // GQ_DECODE_Q6_IMG: Q6_K aligned ring image (-1: K <= 4096)
     int gemm_aq = 1;                          // GQ_GEMM_AQ: in-kernel quantization of 16/32-token tiles

@@ -38,6 +38,7 @@ bool parse_key(Tuning &t, const char *key, long long v)
         if (v < 0 || v > 8) return false;
         t.decode_maxnt = (int)v;
     } else if (k == "GQ_DECODE_NT4_CACHE") t.decode_nt4_cache = v != 0;
+    else if (k == "GQ_DECODE_F8_ITC") t.decode_f8_itc = v != 0;
     else if (k == "GQ_DECODE_EARLY") {
         if (!in({-1, 0, 1, 2})) return false;
         t.decode_early = (int)v;
@@ -116,7 +117,7 @@ void tuning_from_env(Tuning &t)
 {
     t = Tuning{};
     static const char *const keys[] = {"GQ_BLAS_MIN_TOKENS", "GQ_GEMM_MAX_BYTES", "GQ_GEMM_I8", "GQ_NO_FUSED_DECODE",
-                                       "GQ_DECODE_MAXNT", "GQ_DECODE_NT4_CACHE", "GQ_DECODE_Q6_IMG", "GQ_GEMM_AQ", "GQ_GEMM_AQ_NB4",
+                                       "GQ_DECODE_MAXNT", "GQ_DECODE_NT4_CACHE", "GQ_DECODE_Q6_IMG", "GQ_DECODE_F8_ITC", "GQ_DECODE_EARLY", "GQ_GEMM_AQ", "GQ_GEMM_AQ_NB4",
                                        "GQ_GEMM_NB", "GQ_GEMM_RG", "GQ_GEMM_LOADERS", "GQ_GEMM_SPLITS",
                                        "GQ_GEMM_PARTIAL", "GQ_GEMM_FUSED_REDUCE", "GQ_GEMV_CAP", "GQ_GEMV_R",
                                        "GQ_WGEMM", "GQ_WGEMM_RG", "GQ_WGEMM_NB", "GQ_WGEMM_SPLITS", "GQ_WGEMM_WD",
@@ -293,6 +294,16 @@ gq::WGemmPlan wgemm_plan(int t, int64_t M, int64_t N, int64_t K)
 // prepared (gq_mmq_prepared).  With split-K over every super-block its partial sums differ from
 // gemm_kernel's (other splits), so a forced split factor (GQ_GEMM_SPLITS) keeps gemm_kernel.
 // GQ_RGEMM=1: wherever it applies (tests), 0: off.
+// A knob of the LDS-DMA or weight-register GEMM set (tests, A/B of those kernels): the automatic
+// resident / streaming routes stand aside so the call reaches the kernel the knob is for.
+bool gemm_knob_pinned()
+{
+    const gq::Tuning &u = gq::tuning();
+    return u.gemm_splits > 0 || u.gemm_nb || u.gemm_rg || u.gemm_loaders >= 0 || u.gemm_partial_f32 ||
+           u.gemm_fused_reduce || u.gemm_aq_nb4 || u.wgemm == 1 || u.wgemm_splits || u.wgemm_rg || u.wgemm_nb ||
+           u.wgemm_wd;
+}
+
 bool use_rgemm(int t, int form, int64_t M, int64_t N, int64_t K)
 {
     const int rg = gq::tuning().rgemm;
@@ -301,7 +312,7 @@ bool use_rgemm(int t, int form, int64_t M, int64_t N, int64_t K)
     const gq::RGemmPlan p = gq::plan_rgemm(M, N, K);
     if (!p.ok) return false;
     if (rg == 1) return true;
-    if (gq::tuning().gemm_splits > 0 || N < kRgemmMinTokens) return false;
+    if (gemm_knob_pinned() || N < kRgemmMinTokens) return false;
     const int64_t grid = (int64_t)p.tiles_m * p.tiles_n * p.splits, cus = gq::num_cus();
     return grid <= cus && 2 * grid >= cus;
 }
@@ -315,14 +326,24 @@ bool rgemm_route(int t, int form, int64_t M, int64_t N, int64_t K, int act)
     return gq::tuning().skinny != 1 || !use_skinny(t, form, N, act);
 }
 
-// Streaming 256-row GEMM (mmq_rgemm.hip sgemm_kernel) on the prepared x~: GQ_SGEMM=1 wherever
-// the resident form does not apply (tests, A/B), 0 off; auto: not yet the default anywhere.
+// Streaming 256-row GEMM (mmq_rgemm.hip sgemm_kernel) on the prepared x~, where the resident
+// form does not apply (its grid is more than one round of the chip, or under half of one): by
+// default from 17 tokens for every type, and Q6_K from 5 (the skinny kernel keeps Q4_K / Q8_0
+// at 5..16) -- profiles/r04/sg_v1.txt, sg_n.txt, sg_small.txt (MMQ us, old route -> sgemm): Q6_K
+// 28672x8192 x32/x64/x128/x256/x512 73.2/79.9/110.1/207.8/386.5 -> 71.5/78.1/102.2/178.4/342.3,
+// 8192x28672 x64/x128 81.1/107.0 -> 75.5/96.5; Q8_0 11008x4096 x64/x128/x256 27.2/36.5/54.9 ->
+// 23.8/28.8/45.4; Q4_K 11008x4096 x32/x64/x128 20.8/24.4/30.7 -> 20.0/22.7/28.9 (x256 46.8 vs
+// 47.3); Q6_K 11008x4096 x16 23.5 -> 19.8.  GQ_SGEMM=1: wherever it applies (tests, A/B), 0: off.
+constexpr int64_t kSgemmMinTokens = 17, kSgemmQ6MinTokens = 5;
 bool use_sgemm(int t, int form, int64_t M, int64_t N, int64_t K)
 {
     const int sg = gq::tuning().sgemm;
-    if (sg <= 0 || form != gq::AF_F16 || use_gemv(N, K) || use_blas(N, K) || K % 256 != 0) return false;
+    if (sg == 0 || form != gq::AF_F16 || use_gemv(N, K) || use_blas(N, K) || K % 256 != 0) return false;
     if (gemm_rows_per_launch(t, M, K) < M || gemm_toks_per_launch(N, K) < N) return false;
-    return gq::plan_sgemm(M, N, K, gq::tuning().sgemm_splits).ok;
+    if (!gq::plan_sgemm(M, N, K, gq::tuning().sgemm_splits).ok) return false;
+    if (sg == 1) return true;
+    if (gemm_knob_pinned()) return false;
+    return N >= kSgemmMinTokens || (t == GQ_Q6_K && N >= kSgemmQ6MinTokens);
 }
 gq::RGemmPlan sgemm_plan(int64_t M, int64_t N, int64_t K) { return gq::plan_sgemm(M, N, K, gq::tuning().sgemm_splits); }
 
@@ -695,6 +716,7 @@ int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int6
         return GQ_OK;
     }
     if (!r.gemv && !r.blas && act == GQ_ACT_Q8_1 && r.form == gq::AF_F16 && !use_wgemm(t, r.form, N) && !use_skinny(t, r.form, N) &&
+        !use_sgemm(t, r.form, M, N, K) &&
         gemm_rows_per_launch(t, M, K) >= M &&
         gemm_toks_per_launch(N, K) >= N) {
         // 16/32-token tiles whose split fits LDS: the GEMM quantizes the activations itself (no

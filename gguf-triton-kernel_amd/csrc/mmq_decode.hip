@@ -200,7 +200,7 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
     uint8_t *codes = smem + RING;
     float *sd = (float *)(codes + NT * kp * (FP8 ? 2 : 1)); // FP8: quarter sums [NT][2*nb]
     float *sx = sd + NT * nb; // Q4_K: s [NT][nb] (float); Q6_K: code sums [NT][2*nb] (int)
-    static_assert(!FP8 || ITC == 0, "fp8 decode: activations read from LDS per unit");
+    static_assert(!FP8 || NT == 1 || ITC == 0, "fp8 decode: cached activations at one token only");
     // FP8: x~ 16-byte piece P of a token row at piece P ^ ((P >> 4) & 7) (the lanes of a unit
     // read hit distinct banks)
     auto xpiece = [](int P) { return P ^ ((P >> 4) & 7); };
@@ -395,8 +395,8 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
     const int P = 1 << geo.lp2;
     const int lrow = lane >> geo.lp2, lunit = lane & (P - 1);
     const int ntok = N - tok0 < NT ? (int)(N - tok0) : NT;
-    Act<F, NT> ca[ITC > 0 ? ITC * UPC : 1];
-    if constexpr (ITC > 0) {
+    Act<F, NT> ca[ITC > 0 && !FP8 ? ITC * UPC : 1];
+    if constexpr (ITC > 0 && !FP8) {
 #pragma unroll
         for (int i = 0; i < ITC; ++i) {
             const int c = lunit + P * i < cpr ? lunit + P * i : cpr - 1;
@@ -439,9 +439,22 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
             a.s[t][3] = has1 ? sq[(e1 >> 4) + 1] : 0.f;
         }
     };
+    // FP8, ITC > 0 (one token): the lane's units' x~ (32 words each) kept in registers across
+    // its rows, as the int8 form's Act cache -- no LDS reads in the row loop
+    ActH<NT> ch[FP8 && ITC > 0 ? ITC * UPC : 1];
+    if constexpr (FP8 && ITC > 0) {
+#pragma unroll
+        for (int i = 0; i < ITC; ++i) {
+            const int c = lunit + P * i < cpr ? lunit + P * i : cpr - 1;
+#pragma unroll
+            for (int e = 0; e < UPC; ++e) act_h(ch[UPC * i + e], UPC * c + e);
+        }
+    }
     // the contribution of unit u (activation slot i when cached) of the row at rowp
     auto unit = [&](const UnitLoad<F> &l, int u, int i, float (&acc)[NT]) {
-        if constexpr (FP8) {
+        if constexpr (FP8 && ITC > 0) {
+            dot_unit_h<F, NT>(UnitRaw<F>::from(l, u, nb), ch[i], acc);
+        } else if constexpr (FP8) {
             ActH<NT> a;
             act_h(a, u);
             dot_unit_h<F, NT>(UnitRaw<F>::from(l, u, nb), a, acc);
@@ -649,7 +662,9 @@ size_t act_lds(int fmt, int nt, int64_t K, bool fp8 = false)
     return (size_t)nt * kp + (size_t)nt * nb * 4 * (fmt == Q8_0 ? 1 : (fmt == Q4_K ? 2 : 3));
 }
 
-// the largest cached-chunk count ITC instantiated for (format, token tile)
+// the largest cached-chunk count ITC instantiated for (format, token tile); the fp8 form caches
+// at one token only, at most two units (64 VGPRs of x~ pairs)
+int fp8_itc_max(int fmt, int nt) { return nt == 1 ? (fmt == Q6_K ? 1 : 2) : 0; }
 int itc_max(int fmt, int nt)
 {
     if (nt == 1) return fmt == Q6_K ? 4 : 7;
@@ -731,7 +746,10 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p, int wgs = 0)
     // profiles/r02/decode_nt4_cache_ab.txt; GQ_DECODE_NT4_CACHE=0: off)
     if (p.nt == 4 && units == 1 && tuning().decode_nt4_cache)
         p.itc = 1;
-    if (p.fp8) p.itc = 0;
+    if (p.fp8) { // (cached x~ at one token: GQ_DECODE_F8_ITC=0 turns it off)
+        const int64_t fitc = (cpr + (1 << g.lp2) - 1) >> g.lp2;
+        p.itc = p.nt == 1 && tuning().decode_f8_itc && fitc <= fp8_itc_max(fmt, 1) ? (int)fitc : 0;
+    }
     g.early = tuning().decode_early >= 0 ? tuning().decode_early : 0;
     const int64_t waves = g.ngroups < W ? g.ngroups : W;
     p.grid = (int)((waves + DW - 1) / DW);
@@ -760,7 +778,15 @@ hipError_t launch_f(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *
 {
 #define GQ_LT(nt, itc) launch_t<F, nt, itc>(A, X, ldx, C, M, N, K, ldc, p, s)
 #define GQ_LTI(nt, itc) launch_t<F, nt, itc, 1>(A, X, ldx, C, M, N, K, ldc, p, s)
-    if (p.fp8) { // (itc = 0)
+    if (p.fp8) { // (itc: one token only, fp8_itc_max)
+        if (p.nt == 1 && p.itc == 1) {
+            if constexpr (F == Q6_K)
+                if (p.img) return launch_t<F, 1, 1, 1, 1>(A, X, ldx, C, M, N, K, ldc, p, s);
+            return launch_t<F, 1, 1, 0, 1>(A, X, ldx, C, M, N, K, ldc, p, s);
+        }
+        if constexpr (F != Q6_K)
+            if (p.nt == 1 && p.itc == 2) return launch_t<F, 1, 2, 0, 1>(A, X, ldx, C, M, N, K, ldc, p, s);
+        if (p.itc != 0) return hipErrorInvalidValue;
         if constexpr (F == Q6_K)
             if (p.img) switch (p.nt) {
                 case 1: return launch_t<F, 1, 0, 1, 1>(A, X, ldx, C, M, N, K, ldc, p, s);
@@ -861,12 +887,19 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_grouped_kernel(const Gr
     case Q6_K * 16 + 8 + itc:                                                                                          \
         decode_body<Q6_K, NT, itc, 1>(q.A, q.X, q.ldx, q.C, q.M, args.N, q.K, q.ldc, q.geo, bx, q.gx, q.by, smem);   \
         return;
-    if constexpr (FP8) { // (itc = 0)
+#define GQ_GF(f, itc, im)                                                                                              \
+    case f * 16 + itc + 8 * im:                                                                                        \
+        decode_body<f, NT, itc, im, 1>(q.A, q.X, q.ldx, q.C, q.M, args.N, q.K, q.ldc, q.geo, bx, q.gx, q.by, smem);    \
+        return;
+    if constexpr (FP8 && NT == 1) { // (fp8_itc_max: Q8_0 / Q4_K 0..2, Q6_K 0..1)
         switch (q.code) {
-        case Q8_0 * 16: decode_body<Q8_0, NT, 0, 0, 1>(q.A, q.X, q.ldx, q.C, q.M, args.N, q.K, q.ldc, q.geo, bx, q.gx, q.by, smem); return;
-        case Q4_K * 16: decode_body<Q4_K, NT, 0, 0, 1>(q.A, q.X, q.ldx, q.C, q.M, args.N, q.K, q.ldc, q.geo, bx, q.gx, q.by, smem); return;
-        case Q6_K * 16: decode_body<Q6_K, NT, 0, 0, 1>(q.A, q.X, q.ldx, q.C, q.M, args.N, q.K, q.ldc, q.geo, bx, q.gx, q.by, smem); return;
-        case Q6_K * 16 + 8: decode_body<Q6_K, NT, 0, 1, 1>(q.A, q.X, q.ldx, q.C, q.M, args.N, q.K, q.ldc, q.geo, bx, q.gx, q.by, smem); return;
+            GQ_GF(Q8_0, 0, 0) GQ_GF(Q8_0, 1, 0) GQ_GF(Q8_0, 2, 0) GQ_GF(Q4_K, 0, 0) GQ_GF(Q4_K, 1, 0) GQ_GF(Q4_K, 2, 0)
+            GQ_GF(Q6_K, 0, 0) GQ_GF(Q6_K, 1, 0) GQ_GF(Q6_K, 0, 1) GQ_GF(Q6_K, 1, 1)
+        default: return; // (the host checks every code against this set before the launch)
+        }
+    } else if constexpr (FP8) { // (itc = 0)
+        switch (q.code) {
+            GQ_GF(Q8_0, 0, 0) GQ_GF(Q4_K, 0, 0) GQ_GF(Q6_K, 0, 0) GQ_GF(Q6_K, 0, 1)
         default: return;
         }
     } else if constexpr (NT == 1) {
@@ -891,6 +924,7 @@ __global__ __launch_bounds__(DW * 64) void stream_decode_grouped_kernel(const Gr
     }
 #undef GQ_GB
 #undef GQ_GBI
+#undef GQ_GF
 }
 
 template <int NT, int FP8 = 0>
@@ -1037,7 +1071,8 @@ hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipS
             q.M = (int)items[i].M;
             q.K = (int)items[i].K;
             q.geo = p.geo;
-            if (p.itc > itc_max(items[i].fmt, nt) || (fp8 && p.itc != 0)) return hipErrorInvalidValue; // no kernel case
+            if (p.itc > (fp8 ? fp8_itc_max(items[i].fmt, nt) : itc_max(items[i].fmt, nt)))
+                return hipErrorInvalidValue; // no kernel case
             q.code = items[i].fmt * 16 + p.itc + (p.img ? 8 : 0);
             q.block0 = blocks;
             q.gx = p.grid;

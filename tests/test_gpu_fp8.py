@@ -116,3 +116,31 @@ def test_layer_mix_fp8():
         for n, (M, K) in shapes.items():
             ideal = O.mmq_fp8_ideal(types[n], raw[n], x if K == 512 else h, M, N, K)
             assert O.max_rel_err(out[n].cpu().numpy(), ideal) <= TIGHT_FP8, (n, N)
+
+
+@pytest.mark.parametrize("fmt,M,K", [("q4_k", 4096, 4096), ("q8_0", 2048, 4096), ("q4_k", 1024, 8192),
+                                     ("q8_0", 512, 8192), ("q6_k", 4096, 4096), ("q6_k", 1024, 8192),
+                                     ("q4_k", 300, 12288)])
+def test_fp8_decode_register_cache_bit_identical(fmt, M, K, tune):
+    """The fp8 decode form at one token with the lane's x~ kept in registers across its rows
+    (GQ_DECODE_F8_ITC=1, the default: one or two units per lane, Q6_K one half super-block pair;
+    image and packed Q6_K rings) = the per-row LDS reads (=0), bit for bit; alone and grouped;
+    and within the fp8 gate of the fp8-exact product."""
+    import kernels._lib as kl
+    dev = _dev()
+    qA = random_blocks(fmt, M, K, seed=M + K)
+    B = random_activations(1, K, seed=K)
+    A_t, B_t = torch.from_numpy(qA.view(np.int8)).to(dev), torch.from_numpy(B).to(dev)
+    got = {}
+    for itc in (1, 0):
+        tune(GQ_DECODE_F8_ITC=itc)
+        C = kl.mmq(kl.TYPES[fmt], A_t, B_t, M, 1, K, act="fp8")
+        G = kl.mmq_grouped([(kl.TYPES[fmt], A_t, B_t, M, K, None)], 1, act="fp8")
+        assert G is not None, kl.lib().gq_last_error()
+        torch.cuda.synchronize()
+        got[itc] = (C.view(torch.int16).clone(), G[0].view(torch.int16).clone())
+    assert torch.equal(got[1][0], got[0][0])
+    assert torch.equal(got[1][1], got[0][1])
+    assert torch.equal(got[1][0], got[1][1])
+    ideal = O.mmq_fp8_ideal(fmt, qA, B, M, 1, K)
+    assert O.max_rel_err(got[1][0].view(torch.float16).cpu().numpy(), ideal) <= TIGHT_FP8

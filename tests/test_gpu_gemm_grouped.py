@@ -131,11 +131,11 @@ def test_grouped_gemm_ragged_strided_outputs():
         qs.append(qA)
         items.append((kl.TYPES[fmt], qA, ws[K], M, K, buf[:, col:col + M]))
         col += M
-    with kl.Tuning(GQ_SGEMM_SPLITS=2):
+    with kl.tuning(GQ_SGEMM_SPLITS=2):
         outs = kl.mmq_grouped_prepared(items, N)
         assert outs is not None, kl.lib().gq_last_error()
         torch.cuda.synchronize()
-    with kl.Tuning(GQ_SGEMM=1, GQ_RGEMM=0, GQ_SKINNY=0, GQ_SGEMM_SPLITS=2):
+    with kl.tuning(GQ_SGEMM=1, GQ_RGEMM=0, GQ_SKINNY=0, GQ_SGEMM_SPLITS=2):
         col = 0
         for (fmt, M, K), qA in zip(specs, qs):
             wsi = _prepare(kl, X[K], N, K, need=kl.workspace_size(kl.TYPES[fmt], M, N, K))  # (+ partials)
@@ -164,7 +164,7 @@ def test_grouped_gemm_refuses():
     qB = torch.from_numpy(random_blocks("q8_0", M, K, seed=4).view(np.int8)).to(dev)
     ws = _prepare(kl, torch.from_numpy(random_activations(N, K, seed=5)).to(dev), N, K)
     out = torch.full((N, M), 3.0, dtype=torch.float16, device=dev)
-    with kl.Tuning(GQ_CUS=256):
+    with kl.tuning(GQ_CUS=256):
         assert kl.mmq_grouped_prepared([(kl.GQ_Q8_0, qB, ws, M, K, out)], N) is None
     torch.cuda.synchronize()
     assert torch.all(out == 3.0)

@@ -21,7 +21,7 @@ for cfg in sys.argv[1:] or ["q6_k_28672x8192_m1"]:
     fmt, M, K, N = bench.CONFIGS[cfg]
     r = bench.Runner(fmt, M, K, N, dev, 4)
     for i in range(8):
-        r.step(i)
+        r.step(i, i % r.ncopies)
     torch.cuda.synchronize()
     buf = np.zeros((65536, 12), np.uint64)
     assert kl.lib().gq_debug_decode_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes) == 0
