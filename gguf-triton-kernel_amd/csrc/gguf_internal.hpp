@@ -143,6 +143,8 @@ struct RGemmPlan {
     size_t partial_bytes = 0;
 };
 RGemmPlan plan_rgemm(int64_t M, int64_t N, int64_t K);
+// resident workgroups one CU holds at once (LDS-bound: Q4_K at 16 tokens 3, at 32 two, else one)
+int rgemm_per_cu(int fmt, int nb);
 hipError_t launch_rgemm(int fmt, int aq, const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, void *partials,
                         const RGemmPlan &p, int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
 // Streaming form (mmq_rgemm.hip sgemm_kernel): the same tile over K splits of several

@@ -123,6 +123,12 @@ __device__ __forceinline__ Q81Quad q8_1_quad(u32x4 w)
     r.d = h2f(dbits);
     const float div = r.d == 0.f ? 1.0f : r.d;
     const float rdiv = __builtin_amdgcn_rcpf(div);
+    // The per-element tail on packed fp16 (deq_quad's): the fp16-exact quotients packed by one
+    // v_cvt_pk_f16_f32 (RNE, = f2h_bits per element), rint + bias as q + 1536 (|q| < 512: the
+    // sum's ulp is 1, so its round-to-nearest-even is rintf's), the clamp in the biased domain
+    // [1409, 1663]; fp16(1536 + q) is 0x6600 + q, so the int8 code is its low byte (one v_perm
+    // per 4 codes) and sum(q) one v_dot4 of the codes with ones -- the scalar loop's exact bits.
+#ifdef GQ_Q81_SCALAR // (diagnostic A/B build: the scalar per-element loop)
     int sum = 0;
     r.codes[0] = r.codes[1] = 0;
 #pragma unroll
@@ -133,6 +139,23 @@ __device__ __forceinline__ Q81Quad q8_1_quad(u32x4 w)
         sum += qi;
         r.codes[i >> 2] |= (uint32_t)(qi & 0xff) << (8 * (i & 3));
     }
+#else
+    typedef _Float16 h2t __attribute__((ext_vector_type(2)));
+    typedef float f2t __attribute__((ext_vector_type(2)));
+    const h2t magic = {(_Float16)1536.f, (_Float16)1536.f};
+    const h2t lo = {(_Float16)1409.f, (_Float16)1409.f}, hi = {(_Float16)1663.f, (_Float16)1663.f};
+    uint32_t t[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const f2t qf = {q81_div(x[2 * p], div, rdiv), q81_div(x[2 * p + 1], div, rdiv)};
+        h2t q = __builtin_convertvector(qf, h2t) + magic;
+        q = __builtin_elementwise_min(__builtin_elementwise_max(q, lo), hi);
+        t[p] = __builtin_bit_cast(uint32_t, q);
+    }
+    r.codes[0] = __builtin_amdgcn_perm(t[1], t[0], 0x06040200u);
+    r.codes[1] = __builtin_amdgcn_perm(t[3], t[2], 0x06040200u);
+    int sum = __builtin_amdgcn_sdot4((int)r.codes[1], 0x01010101, __builtin_amdgcn_sdot4((int)r.codes[0], 0x01010101, 0, false), false);
+#endif
     sum += __builtin_amdgcn_mov_dpp(sum, 0xb1, 0xf, 0xf, false);
     r.s4 = sum; // lanes (0,1) and (2,3) of the group: the two 16-element halves
     sum += __builtin_amdgcn_mov_dpp(sum, 0x4e, 0xf, 0xf, false);

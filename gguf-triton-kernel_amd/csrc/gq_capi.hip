@@ -313,8 +313,10 @@ bool use_rgemm(int t, int form, int64_t M, int64_t N, int64_t K)
     if (!p.ok) return false;
     if (rg == 1) return true;
     if (gemm_knob_pinned() || N < kRgemmMinTokens) return false;
+    // one round of the chip at the workgroups a CU holds (Q4_K at 16 tokens: three -- 11008x4096
+    // and 4096x11008 at 688 workgroups)
     const int64_t grid = (int64_t)p.tiles_m * p.tiles_n * p.splits, cus = gq::num_cus();
-    return grid <= cus && 2 * grid >= cus;
+    return grid <= cus * gq::rgemm_per_cu(t, p.nb) && 2 * grid >= cus;
 }
 
 // The resident GEMM where it applies, ahead of the skinny kernel (4096^2 x16 step: Q4_K 6.8 vs

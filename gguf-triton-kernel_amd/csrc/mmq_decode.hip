@@ -359,7 +359,9 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
     // (early = 1, 2) refill under the quantization instead.  Task 0 always issues (past the
     // wave's tasks: an offset beyond the buffer -- zeros, no memory access), so the wait below
     // for the activations, the older loads, is a fixed vmcnt.
+#ifndef GQ_DECODE_XFIRST // (diagnostic build -DGQ_DECODE_XFIRST: task 0 only once the activations arrived)
     issue(0);
+#endif
     auto issue_rest = [&]() {
 #pragma unroll
         for (int j = 1; j < NS; ++j)
@@ -368,6 +370,10 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
     if (geo.early == 2) issue_rest();
 #pragma unroll
     for (int q = 0; q < XP; ++q) asm volatile("" ::"v"(xv[q].x), "v"(xv[q].y), "v"(xv[q].z), "v"(xv[q].w)); // waits for the x loads
+#ifdef GQ_DECODE_XFIRST
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    issue(0);
+#endif
 #ifdef GQ_DECODE_STAMPS
     const unsigned long long t_xw = __builtin_amdgcn_s_memtime();
 #endif

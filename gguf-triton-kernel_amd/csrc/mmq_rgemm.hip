@@ -608,6 +608,23 @@ hipError_t launch_f(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *
 
 } // namespace
 
+int rgemm_per_cu(int fmt, int nb)
+{
+#define GQ_RPC(F)                                                                                                      \
+    switch (nb) {                                                                                                      \
+    case 1: return LDS_CAP / RCfg<F, 1>::LDS;                                                                          \
+    case 2: return LDS_CAP / RCfg<F, 2>::LDS;                                                                          \
+    case 4: return LDS_CAP / RCfg<F, 4>::LDS;                                                                          \
+    default: return LDS_CAP / RCfg<F, 8>::LDS;                                                                         \
+    }
+    switch (fmt) {
+    case Q8_0: GQ_RPC(Q8_0)
+    case Q4_K: GQ_RPC(Q4_K)
+    default: GQ_RPC(Q6_K)
+    }
+#undef GQ_RPC
+}
+
 RGemmPlan plan_rgemm(int64_t M, int64_t N, int64_t K)
 {
     RGemmPlan p;

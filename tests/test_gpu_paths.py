@@ -290,7 +290,7 @@ def test_fused_split_k_reduce_bit_identical(fmt, M, N, K, splits, tune):
     split counts that are not multiples of 8, ragged M/N."""
     from kernels._lib import TYPES, mmq
     dev = _dev()
-    tune(GQ_WGEMM=0)  # (the fused reduce belongs to the LDS-DMA GEMM)
+    tune(GQ_WGEMM=0, GQ_RGEMM=0, GQ_SGEMM=0)  # (the fused reduce belongs to the LDS-DMA GEMM)
     if splits:
         tune(GQ_GEMM_SPLITS=splits)
     qA = random_blocks(fmt, M, K, seed=M + 7 * N)
