@@ -169,6 +169,9 @@ struct SGroupPlan {
     bool ok = false;
     int nb = 8, tiles_n = 1, blocks = 0;
     int tiles_m[16] = {}, splits[16] = {}, wg0[16] = {};
+    bool streamk = false;  // (tile, super-block) units spread evenly over the workgroups (auto splits)
+    int U = 0;             // stream-K: units; blocks = the workgroups
+    int ustart[16] = {}, scap[16] = {};
     size_t poff[16] = {};
     size_t partial_bytes = 0;
 };

@@ -348,6 +348,22 @@ bool use_sgemm(int t, int form, int64_t M, int64_t N, int64_t K)
     return N >= kSgemmMinTokens || (t == GQ_Q6_K && N >= kSgemmQ6MinTokens);
 }
 gq::RGemmPlan sgemm_plan(int64_t M, int64_t N, int64_t K) { return gq::plan_sgemm(M, N, K, gq::tuning().sgemm_splits); }
+// The streaming GEMM of one matrix as the grouped kernel's one-part stream-K plan (splits not
+// pinned, tiles within one round of the chip): every workgroup L or L+1 super-blocks instead of
+// whole-tile splits (Q6_K 28672x8192 x128: 224 workgroups x 16 super-blocks -> 256 x 14)
+bool sgemm_streamk(int t, int64_t M, int64_t N, int64_t K, gq::SGroupItem &it, gq::SGroupPlan &g)
+{
+    if (gq::tuning().sgemm_splits > 0) return false;
+    it = gq::SGroupItem{t, nullptr, nullptr, nullptr, M, M, K};
+    g = gq::plan_sgemm_grouped(&it, 1, N, 0);
+    return g.ok && g.streamk;
+}
+size_t sgemm_partial_bytes(int t, int64_t M, int64_t N, int64_t K)
+{
+    gq::SGroupItem it;
+    gq::SGroupPlan g;
+    return sgemm_streamk(t, M, N, K, it, g) ? g.partial_bytes : sgemm_plan(M, N, K).partial_bytes;
+}
 
 bool use_i8(int t, int64_t N, int64_t K)
 {
@@ -408,7 +424,7 @@ size_t ws_bytes(int t, int act, int64_t M, int64_t N, int64_t K)
         const bool sk = use_skinny(t, r.form, N, act), wg = use_wgemm(t, r.form, N);
         const int64_t mr = gemm_rows_per_launch(t, M, K), nt = sk ? N : gemm_toks_per_launch(N, K);
         size_t p = use_rgemm(t, r.form, M, N, K) ? gq::plan_rgemm(M, N, K).partial_bytes
-                   : use_sgemm(t, r.form, M, N, K) ? sgemm_plan(M, N, K).partial_bytes : 0;
+                   : use_sgemm(t, r.form, M, N, K) ? sgemm_partial_bytes(t, M, N, K) : 0;
         for (int64_t mc : {mr, M % mr})
             for (int64_t nc : {nt, N % nt})
                 if (mc > 0 && nc > 0) {
@@ -648,8 +664,18 @@ static int compute(gq_type t, int act, const void *A, void *workspace, size_t wo
             return GQ_OK;
         }
         if (!rgemm_route(t, r.form, M, N, K, act) && !use_skinny(t, r.form, N, act) && use_sgemm(t, r.form, M, N, K)) {
-            e = gq::launch_sgemm(t, (const uint8_t *)A, c.xdeq, (uint16_t *)C, c.partials, sgemm_plan(M, N, K), M, N, K,
-                                 ldc, s);
+            gq::SGroupItem it;
+            gq::SGroupPlan g;
+            if (sgemm_streamk(t, M, N, K, it, g)) {
+                it.A = (const uint8_t *)A;
+                it.X = c.xdeq;
+                it.C = (uint16_t *)C;
+                it.ldc = ldc;
+                e = gq::launch_sgemm_grouped(&it, 1, N, g, c.partials, s);
+            } else {
+                e = gq::launch_sgemm(t, (const uint8_t *)A, c.xdeq, (uint16_t *)C, c.partials, sgemm_plan(M, N, K), M, N,
+                                     K, ldc, s);
+            }
             if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (sgemm): %s", hipGetErrorString(e));
             return GQ_OK;
         }

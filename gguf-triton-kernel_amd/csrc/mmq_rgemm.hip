@@ -383,11 +383,13 @@ struct SPart {
     uint16_t *C, *P;
     int64_t M, K, ldc;
     int tiles_m, tiles_n, splits, wg0;
+    int ustart, scap; // stream-K: the part's first unit (tile-major (tile, super-block) order), partial slots per tile
 };
 struct SParts {
     int n;
     int64_t N;
     int spol;
+    int streamk, U, W; // stream-K: U units over W workgroups, workgroup w = units [wU/W, (w+1)U/W)
     SPart p[kMaxSParts];
 };
 struct RPart {
@@ -395,26 +397,31 @@ struct RPart {
     uint16_t *C;
     int64_t M, ldc;
     int tiles_m, tiles_n, splits, wg0;
+    int ustart, nsb, scap;
 };
 struct RParts {
     int n;
     int64_t N;
+    int streamk, U, W;
     RPart p[kMaxSParts];
 };
+
+// stream-K: the workgroups whose unit ranges hold the first and the last unit of [u0, u1)
+__device__ __forceinline__ int sk_first_wg(int u0, int U, int W) { return (int)(((int64_t)(u0 + 1) * W + U - 1) / U) - 1; }
+__device__ __forceinline__ int sk_last_wg(int u1, int U, int W) { return (int)(((int64_t)u1 * W + U - 1) / U) - 1; }
 
 template <int F, int NB>
 __device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
                                            uint16_t *__restrict__ C, uint16_t *__restrict__ P, int64_t M, int64_t N,
-                                           int64_t K, int64_t ldc, int spol, const TileId &id, uint8_t *lds)
+                                           int64_t K, int64_t ldc, int spol, const TileId &id, int64_t sb0, int64_t sb1,
+                                           uint8_t *lds)
 {
     using G = SCfg<F, NB>;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t m0 = (int64_t)id.x * RBM, n0 = (int64_t)id.y * G::BN;
-    const int64_t row_bytes = (K / Layout<F>::QK) * Layout<F>::BYTES, nsb = K / 256;
-    // split z: super-blocks [z*nsb/S, (z+1)*nsb/S) (split lengths differ by one when S does not divide)
-    const int64_t S = id.gz, z = id.z;
-    const int64_t sb0 = z * nsb / S, sb1 = (z + 1) * nsb / S;
+    const int64_t row_bytes = (K / Layout<F>::QK) * Layout<F>::BYTES;
+    // super-blocks [sb0, sb1) of the tile; the partial (or C when id.gz == 1) as split id.z
     const int nst = (int)(2 * (sb1 - sb0)); // half stages
     const __amdgpu_buffer_rsrc_t wrs =
         __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, (int)(uint32_t)((M * row_bytes + 15) & ~(int64_t)15), 0x00020000);
@@ -474,7 +481,10 @@ __global__ __launch_bounds__(64 * RW) void sgemm_kernel(const uint8_t *__restric
                                                        int64_t N, int64_t K, int64_t ldc, int spol)
 {
     __shared__ __attribute__((aligned(1024))) uint8_t lds[SCfg<F, NB>::LDS];
-    sgemm_body<F, NB>(A, X, C, P, M, N, K, ldc, spol, grid_tile(), lds);
+    // split z: super-blocks [z*nsb/S, (z+1)*nsb/S) (split lengths differ by one when S does not divide)
+    const TileId id = grid_tile();
+    const int64_t nsb = K / 256;
+    sgemm_body<F, NB>(A, X, C, P, M, N, K, ldc, spol, id, id.z * nsb / id.gz, (id.z + 1) * nsb / id.gz, lds);
 }
 
 // ---- several matrices in one launch (gq_mmq_grouped_prepared): part i = one matrix's
@@ -490,15 +500,42 @@ __global__ __launch_bounds__(64 * RW) void sgemm_grouped_kernel(const SParts a)
 {
     __shared__ __attribute__((aligned(1024))) uint8_t lds[max_slds<NB>()];
     const int b = (int)blockIdx.x;
-    int i = 0;
-    while (i + 1 < a.n && b >= a.p[i + 1].wg0) ++i;
-    const SPart &q = a.p[i];
-    const int l = b - q.wg0, txy = q.tiles_m * q.tiles_n;
-    const TileId id{l % q.tiles_m, (l % txy) / q.tiles_m, l / txy, q.tiles_m, q.tiles_n, q.splits};
-    switch (q.fmt) {
-    case Q8_0: sgemm_body<Q8_0, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, lds); return;
-    case Q4_K: sgemm_body<Q4_K, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, lds); return;
-    default: sgemm_body<Q6_K, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, lds); return;
+    auto run = [&](const SPart &q, const TileId &id, int64_t sb0, int64_t sb1) __attribute__((always_inline)) {
+        switch (q.fmt) {
+        case Q8_0: sgemm_body<Q8_0, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds); return;
+        case Q4_K: sgemm_body<Q4_K, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds); return;
+        default: sgemm_body<Q6_K, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds); return;
+        }
+    };
+    if (!a.streamk) { // tile-granular splits: workgroup = (part, tile, split)
+        int i = 0;
+        while (i + 1 < a.n && b >= a.p[i + 1].wg0) ++i;
+        const SPart &q = a.p[i];
+        const int l = b - q.wg0, txy = q.tiles_m * q.tiles_n;
+        const TileId id{l % q.tiles_m, (l % txy) / q.tiles_m, l / txy, q.tiles_m, q.tiles_n, q.splits};
+        const int64_t nsb = q.K / 256;
+        run(q, id, id.z * nsb / id.gz, (id.z + 1) * nsb / id.gz);
+        return;
+    }
+    // stream-K: this workgroup's units [u0, u1) of the parts' (tile, super-block) sequence, as
+    // segments of at most one tile each; a tile all of whose units one workgroup holds is stored
+    // whole, else each of its S_t workgroups writes partial slot k (in workgroup order)
+    int u = (int)((int64_t)b * a.U / a.W);
+    const int u1 = (int)((int64_t)(b + 1) * a.U / a.W);
+    bool first = true;
+    while (u < u1) {
+        int i = 0;
+        while (i + 1 < a.n && u >= a.p[i + 1].ustart) ++i;
+        const SPart &q = a.p[i];
+        const int nsb = (int)(q.K / 256), local = u - q.ustart, tile = local / nsb, sb = local - tile * nsb;
+        const int t0 = q.ustart + tile * nsb, t1 = t0 + nsb;
+        const int end = u1 < t1 ? u1 : t1;
+        const int wf = sk_first_wg(t0, a.U, a.W), st = sk_last_wg(t1, a.U, a.W) - wf + 1;
+        const TileId id{tile % q.tiles_m, tile / q.tiles_m, st == 1 ? 0 : b - wf, q.tiles_m, q.tiles_n, st == 1 ? 1 : q.scap};
+        if (!first) __builtin_amdgcn_s_barrier(); // (the previous segment's last stage is read by every wave)
+        run(q, id, sb, sb + (end - u));
+        first = false;
+        u = end;
     }
 }
 
@@ -519,12 +556,18 @@ __global__ __launch_bounds__(256) void reduce_grouped_kernel(const RParts a)
     const int l = b - q.wg0, tile = l / BPT, it = (l % BPT) * 256 + (int)threadIdx.x;
     const int ntiles = q.tiles_m * q.tiles_n;
     if (tile >= ntiles || it >= UPT) return;
+    int S = q.splits, ss = q.splits; // splits summed, partial slots per tile
+    if (a.streamk) {
+        const int t0 = q.ustart + tile * q.nsb;
+        S = sk_last_wg(t0 + q.nsb, a.U, a.W) - sk_first_wg(t0, a.U, a.W) + 1;
+        ss = q.scap;
+        if (S == 1) return; // (stored whole by its workgroup)
+    }
     const int lane = it & 63, u = (it >> 6) % (NB / TPU), wr = (it >> 6) / (NB / TPU);
     const int wv = __builtin_amdgcn_readfirstlane(wr / RRG);
     const int64_t m0 = (int64_t)(tile % q.tiles_m) * RBM, n0 = (int64_t)(tile / q.tiles_m) * (16 * NB);
     const int64_t blk = (int64_t)RBM * 16 * NB; // halves per (tile, split) block
-    const int S = q.splits;
-    const int *es = (const int *)(q.P + (int64_t)ntiles * S * blk);
+    const int *es = (const int *)(q.P + (int64_t)ntiles * ss * blk);
     f32x4 acc[TPU];
 #pragma unroll
     for (int j = 0; j < TPU; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -533,7 +576,7 @@ __global__ __launch_bounds__(256) void reduce_grouped_kernel(const RParts a)
         float up[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) { // unconditional (clamped) loads, the surplus zeroed after
-            const int64_t sp = (int64_t)tile * S + (s0 + k < S ? s0 + k : S - 1);
+            const int64_t sp = (int64_t)tile * ss + (s0 + k < S ? s0 + k : S - 1);
             up[k] = __builtin_bit_cast(float, (uint32_t)(127 + es[sp * RW + wv]) << 23);
             if constexpr (TPU == 2) {
                 v[k] = ((const u32x4 *)(q.P + sp * blk))[it];
@@ -692,6 +735,38 @@ SGroupPlan plan_sgemm_grouped(const SGroupItem *items, int n, int64_t N, int spl
     int64_t tiles = 0;
     for (int i = 0; i < n; ++i) tiles += (int64_t)g.tiles_m[i] * tn;
     if (tiles > cus) return g;
+    g.tiles_n = tn;
+    if (splits <= 0 && units < ((int64_t)1 << 30)) {
+        // stream-K (the default): the units (tile, super-block), part by part and tile by tile,
+        // split evenly over one round of the chip -- every workgroup L or L+1 super-blocks, where
+        // whole-tile splits leave the largest part's workgroups up to ceil(nsb / L) (a 7B layer at
+        // 128 tokens: 16 super-blocks on 198 workgroups vs 12-13 on 256)
+        const int W = (int)(units < cus ? units : cus), U = (int)units;
+        auto first_wg = [&](int64_t u0) { return (int)(((u0 + 1) * W + U - 1) / U) - 1; };
+        auto last_wg = [&](int64_t u1) { return (int)((u1 * W + U - 1) / U) - 1; };
+        int64_t ust = 0;
+        size_t pb = 0;
+        for (int i = 0; i < n; ++i) {
+            const int64_t nsb = items[i].K / 256, nt = (int64_t)g.tiles_m[i] * tn;
+            int cap = 1;
+            for (int64_t t = 0; t < nt; ++t) {
+                const int64_t t0 = ust + t * nsb, st = last_wg(t0 + nsb) - first_wg(t0) + 1;
+                cap = st > cap ? (int)st : cap;
+            }
+            g.ustart[i] = (int)ust;
+            g.scap[i] = cap;
+            g.splits[i] = cap;
+            g.poff[i] = pb;
+            if (cap > 1) pb += ((size_t)cap * nt * (RBM * 16 * g.nb * 2 + RW * 4) + 255) & ~(size_t)255;
+            ust += nt * nsb;
+        }
+        g.streamk = true;
+        g.U = U;
+        g.blocks = W;
+        g.partial_bytes = pb;
+        g.ok = true;
+        return g;
+    }
     int64_t L = (units + cus - 1) / cus;
     if (L < 1) L = 1;
     for (;; ++L) {
@@ -727,16 +802,20 @@ hipError_t launch_sgemm_grouped(const SGroupItem *items, int n, int64_t N, const
     a.n = n;
     a.N = N;
     a.spol = tuning().rgemm_spol;
+    a.streamk = r.streamk = g.streamk ? 1 : 0;
+    a.U = r.U = g.U;
+    a.W = r.W = g.blocks;
     r.N = N;
     int rb = 0;
     constexpr int UPB = 256; // reduce: threads per workgroup
     for (int i = 0; i < n; ++i) {
         uint16_t *P = (uint16_t *)((uint8_t *)partials + g.poff[i]);
         a.p[i] = SPart{items[i].fmt, items[i].A, items[i].X, items[i].C, P, items[i].M, items[i].K, items[i].ldc,
-                       g.tiles_m[i], g.tiles_n, g.splits[i], g.wg0[i]};
+                       g.tiles_m[i], g.tiles_n, g.splits[i], g.wg0[i], g.ustart[i], g.scap[i]};
         if (g.splits[i] > 1) {
             const int tpu = g.nb == 1 ? 1 : 2, upt = RW * RRG * (g.nb / tpu) * 64, bpt = (upt + UPB - 1) / UPB;
-            r.p[r.n++] = RPart{P, items[i].C, items[i].M, items[i].ldc, g.tiles_m[i], g.tiles_n, g.splits[i], rb};
+            r.p[r.n++] = RPart{P,         items[i].C, items[i].M, items[i].ldc, g.tiles_m[i], g.tiles_n, g.splits[i], rb,
+                               g.ustart[i], (int)(items[i].K / 256), g.scap[i]};
             rb += g.tiles_m[i] * g.tiles_n * bpt;
         }
     }

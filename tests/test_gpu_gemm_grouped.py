@@ -189,3 +189,37 @@ def test_layer_mix_grouped_gemm_route(N):
     for n in LLAMA_LAYER_SHAPES:
         assert rg[n].data_ptr() == out[n].data_ptr(), n
         assert O.max_rel_err(rg[n].cpu().numpy(), ru[n].cpu().numpy()) <= TIGHT, n
+
+
+@pytest.mark.parametrize("cus", [256, 97, 37])
+def test_grouped_gemm_stream_k(cus, tune):
+    """The automatic plan spreads the (tile, super-block) units evenly over the workgroups
+    (stream-K): a workgroup may end one tile and start the next, a tile's partial sums come from
+    a varying number of workgroups (odd workgroup counts forced by GQ_CUS), and tiles one
+    workgroup holds whole are stored without partials.  Against the oracle on sampled rows,
+    and the same bits call after call."""
+    import kernels._lib as kl
+    dev = _dev()
+    tune(GQ_CUS=cus)
+    N = 40
+    specs = [("q4_k", 1000, 4096), ("q6_k", 300, 2816), ("q8_0", 2048, 1024), ("q4_k", 256, 11008), ("q6_k", 64, 256)]
+    X = {K: random_activations(N, K, seed=K) for K in {s[2] for s in specs}}
+    ws = {K: _prepare(kl, torch.from_numpy(X[K]).to(dev), N, K) for K in X}
+    raws, items = [], []
+    for i, (fmt, M, K) in enumerate(specs):
+        raw = random_blocks(fmt, M, K, seed=10 + i)
+        raws.append(raw)
+        items.append((kl.TYPES[fmt], torch.from_numpy(raw.view(np.int8)).to(dev), ws[K], M, K, None))
+    outs = kl.mmq_grouped_prepared(items, N)
+    assert outs is not None, kl.lib().gq_last_error()
+    again = kl.mmq_grouped_prepared(items, N)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(cus)
+    for (fmt, M, K), raw, C, C2 in zip(specs, raws, outs, again):
+        assert torch.equal(C.view(torch.int16), C2.view(torch.int16)), fmt
+        rows = np.sort(rng.choice(M, size=min(M, 24), replace=False))
+        rb = raw.size // M
+        sub = np.concatenate([raw[r * rb:(r + 1) * rb] for r in rows])
+        got = C.cpu().numpy()[:, rows]
+        ideal = O.mmq_from_fp16(fmt, sub, X[K], len(rows), N, K, O.IDEAL)
+        assert O.max_rel_err(got, ideal) <= TIGHT, (fmt, M, K)
