@@ -39,6 +39,7 @@ bool parse_key(Tuning &t, const char *key, long long v)
         t.decode_maxnt = (int)v;
     } else if (k == "GQ_DECODE_NT4_CACHE") t.decode_nt4_cache = v != 0;
     else if (k == "GQ_DECODE_F8_ITC") t.decode_f8_itc = v != 0;
+    else if (k == "GQ_SGEMM_STREAMK") t.sgemm_streamk = v != 0;
     else if (k == "GQ_DECODE_EARLY") {
         if (!in({-1, 0, 1, 2})) return false;
         t.decode_early = (int)v;
@@ -121,7 +122,7 @@ void tuning_from_env(Tuning &t)
                                        "GQ_GEMM_NB", "GQ_GEMM_RG", "GQ_GEMM_LOADERS", "GQ_GEMM_SPLITS",
                                        "GQ_GEMM_PARTIAL", "GQ_GEMM_FUSED_REDUCE", "GQ_GEMV_CAP", "GQ_GEMV_R",
                                        "GQ_WGEMM", "GQ_WGEMM_RG", "GQ_WGEMM_NB", "GQ_WGEMM_SPLITS", "GQ_WGEMM_WD",
-                                       "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D", "GQ_RGEMM", "GQ_SGEMM", "GQ_SGEMM_SPLITS", "GQ_RGEMM_SPOL", "GQ_CUS", "GQ_ABLATE"};
+                                       "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D", "GQ_RGEMM", "GQ_SGEMM", "GQ_SGEMM_SPLITS", "GQ_SGEMM_STREAMK", "GQ_RGEMM_SPOL", "GQ_CUS", "GQ_ABLATE"};
     for (const char *k : keys) {
         const char *e = getenv(k); // the only getenv of the library: once per process
         if (!e || !*e) continue;
@@ -348,12 +349,15 @@ bool use_sgemm(int t, int form, int64_t M, int64_t N, int64_t K)
     return N >= kSgemmMinTokens || (t == GQ_Q6_K && N >= kSgemmQ6MinTokens);
 }
 gq::RGemmPlan sgemm_plan(int64_t M, int64_t N, int64_t K) { return gq::plan_sgemm(M, N, K, gq::tuning().sgemm_splits); }
-// The streaming GEMM of one matrix as the grouped kernel's one-part stream-K plan (splits not
-// pinned, tiles within one round of the chip): every workgroup L or L+1 super-blocks instead of
-// whole-tile splits (Q6_K 28672x8192 x128: 224 workgroups x 16 super-blocks -> 256 x 14)
+// The streaming GEMM of one matrix as the grouped kernel's one-part stream-K plan (GQ_SGEMM_STREAMK=1,
+// splits not pinned, tiles within one round of the chip): every workgroup L or L+1 super-blocks
+// instead of whole-tile splits (Q6_K 28672x8192 x128: 224 workgroups x 16 super-blocks -> 256 x
+// 14).  Measured no faster (104.7 vs 101.9 us there; 11008x4096 x128 33.7 vs 28.9: a workgroup
+// of 2-3 super-blocks spanning two tiles fills and drains its ring twice and stores two
+// partials; profiles/r04/b4_sk.txt), so off by default.
 bool sgemm_streamk(int t, int64_t M, int64_t N, int64_t K, gq::SGroupItem &it, gq::SGroupPlan &g)
 {
-    if (gq::tuning().sgemm_splits > 0) return false;
+    if (gq::tuning().sgemm_splits > 0 || !gq::tuning().sgemm_streamk) return false;
     it = gq::SGroupItem{t, nullptr, nullptr, nullptr, M, M, K};
     g = gq::plan_sgemm_grouped(&it, 1, N, 0);
     return g.ok && g.streamk;

@@ -736,11 +736,12 @@ SGroupPlan plan_sgemm_grouped(const SGroupItem *items, int n, int64_t N, int spl
     for (int i = 0; i < n; ++i) tiles += (int64_t)g.tiles_m[i] * tn;
     if (tiles > cus) return g;
     g.tiles_n = tn;
-    if (splits <= 0 && units < ((int64_t)1 << 30)) {
-        // stream-K (the default): the units (tile, super-block), part by part and tile by tile,
-        // split evenly over one round of the chip -- every workgroup L or L+1 super-blocks, where
-        // whole-tile splits leave the largest part's workgroups up to ceil(nsb / L) (a 7B layer at
-        // 128 tokens: 16 super-blocks on 198 workgroups vs 12-13 on 256)
+    if (splits <= 0 && tuning().sgemm_streamk && units < ((int64_t)1 << 30)) {
+        // stream-K (GQ_SGEMM_STREAMK=1): the units (tile, super-block), part by part and tile by
+        // tile, split evenly over one round of the chip -- every workgroup L or L+1 super-blocks,
+        // where whole-tile splits leave the largest part's workgroups up to ceil(nsb / L) (a 7B
+        // layer at 128 tokens: 16 super-blocks on 198 workgroups vs 12-13 on 256).  Measured no
+        // faster (layer x128 102.1 vs 102.6 us; single matrices slower, gq_capi.hip sgemm_streamk)
         const int W = (int)(units < cus ? units : cus), U = (int)units;
         auto first_wg = [&](int64_t u0) { return (int)(((u0 + 1) * W + U - 1) / U) - 1; };
         auto last_wg = [&](int64_t u1) { return (int)((u1 * W + U - 1) / U) - 1; };

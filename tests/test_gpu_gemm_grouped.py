@@ -193,14 +193,14 @@ def test_layer_mix_grouped_gemm_route(N):
 
 @pytest.mark.parametrize("cus", [256, 97, 37])
 def test_grouped_gemm_stream_k(cus, tune):
-    """The automatic plan spreads the (tile, super-block) units evenly over the workgroups
-    (stream-K): a workgroup may end one tile and start the next, a tile's partial sums come from
+    """The stream-K plan (GQ_SGEMM_STREAMK=1) spreads the (tile, super-block) units evenly over
+    the workgroups: a workgroup may end one tile and start the next, a tile's partial sums come from
     a varying number of workgroups (odd workgroup counts forced by GQ_CUS), and tiles one
     workgroup holds whole are stored without partials.  Against the oracle on sampled rows,
     and the same bits call after call."""
     import kernels._lib as kl
     dev = _dev()
-    tune(GQ_CUS=cus)
+    tune(GQ_CUS=cus, GQ_SGEMM_STREAMK=1)
     N = 40
     specs = [("q4_k", 1000, 4096), ("q6_k", 300, 2816), ("q8_0", 2048, 1024), ("q4_k", 256, 11008), ("q6_k", 64, 256)]
     X = {K: random_activations(N, K, seed=K) for K in {s[2] for s in specs}}
@@ -223,3 +223,25 @@ def test_grouped_gemm_stream_k(cus, tune):
         got = C.cpu().numpy()[:, rows]
         ideal = O.mmq_from_fp16(fmt, sub, X[K], len(rows), N, K, O.IDEAL)
         assert O.max_rel_err(got, ideal) <= TIGHT, (fmt, M, K)
+
+
+@pytest.mark.parametrize("fmt,M,K,N", [("q6_k", 2048, 8192, 128), ("q4_k", 1000, 4096, 40), ("q8_0", 777, 2816, 20)])
+def test_single_matrix_stream_k(fmt, M, K, N, tune):
+    """The streaming GEMM of one matrix through the one-part stream-K plan (GQ_SGEMM_STREAMK=1)
+    against the oracle, and equal to the whole-tile plan within the GEMM tolerance."""
+    import kernels._lib as kl
+    dev = _dev()
+    raw = random_blocks(fmt, M, K, seed=M)
+    B = random_activations(N, K, seed=K)
+    A_t, B_t = torch.from_numpy(raw.view(np.int8)).to(dev), torch.from_numpy(B).to(dev)
+    tune(GQ_RGEMM=0, GQ_SKINNY=0, GQ_SGEMM=1, GQ_SGEMM_STREAMK=1, GQ_CUS=61)
+    ws = _prepare(kl, B_t, N, K, need=kl.workspace_size(kl.TYPES[fmt], M, N, K))
+    C = kl.mmq_prepared(kl.TYPES[fmt], A_t, ws, M, N, K).cpu().numpy()
+    tune(GQ_SGEMM_STREAMK=0)
+    ws0 = _prepare(kl, B_t, N, K, need=kl.workspace_size(kl.TYPES[fmt], M, N, K))
+    C0 = kl.mmq_prepared(kl.TYPES[fmt], A_t, ws0, M, N, K).cpu().numpy()
+    assert O.max_rel_err(C, C0) <= TIGHT
+    rows = np.sort(np.random.default_rng(M).choice(M, size=24, replace=False))
+    rb = raw.size // M
+    sub = np.concatenate([raw[r * rb:(r + 1) * rb] for r in rows])
+    assert O.max_rel_err(C[:, rows], O.mmq_from_fp16(fmt, sub, B, len(rows), N, K, O.IDEAL)) <= TIGHT
