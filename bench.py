@@ -723,16 +723,14 @@ def bench_config(name, steps, warmup, dev):
     # dominant kernel: decode (N <= 4) -- the step IS one launch (fused quantizer + weight
     # stream), so its time is the step's; GEMM -- the MMQ call alone (gemm_kernel [+ split-K
     # reduce]) with the activations prepared once, K launches per graph, the same rotation
+    import kernels._lib as kl
     if N <= 4:
         t_k = per_step
-        kname = "stream_decode_kernel (fused q8_1 + decode)"
+        kname = kl.route_name(kl.TYPES[fmt], M, N, K) + " (fused q8_1 + decode)"
     else:
         r.prepare()
         t_k = r.timed(r.kernel)
-        # (the library's routing, csrc/gq_capi.hip use_wgemm: Q4_K from 33 tokens on takes the
-        # weight-register GEMM)
-        kname = ("wgemm_kernel (+ wreduce_kernel when split-K)" if fmt == "q4_k" and N >= 33
-                 else "gemm_kernel (+ gemm_reduce_kernel when split-K)")
+        kname = kl.route_name(kl.TYPES[fmt], M, N, K, prepared=True)  # (the library's own routing)
     wbytes, alg_bytes, flops = model(fmt, M, K, N)
     out = {
         "config": name, "fmt": fmt, "N_out": M, "K": K, "M_tok": N,

@@ -546,6 +546,7 @@ int gq_debug_set_tuning(const char *key, long long value)
 }
 void gq_debug_reset_tuning(void) { gq::reset_tuning(); }
 
+
 int gq_block_elems(gq_type t) { return block_elems(t); }
 int gq_block_bytes(gq_type t) { return block_bytes(t); }
 int gq_version(void) { return 102; }
@@ -1087,3 +1088,24 @@ int gq_mmq_sharded(gq_type t, const void *A_shard, const void *B, void *C, int64
 }
 
 } // extern "C"
+
+const char *gq_debug_route(gq_type t, gq_act act, int64_t M, int64_t N, int64_t K, int prepared)
+{
+    // the same decisions, in the same order, as gq_mmq_ex (prepared = 0) and compute()
+    if (check_common(t, M, N, K) != GQ_OK || check_act(act, K) != GQ_OK || M <= 0 || N <= 0 || K <= 0) return "none";
+    g_err.clear();
+    const Route r = route(t, act, N, K);
+    if (!prepared && fused_decode_route(t, act, N, K)) return "stream_decode_kernel";
+    if (r.blas) return "dequant_kernel + hipBLASLt";
+    if (r.gemv) return "gemv_kernel";
+    if (rgemm_route(t, r.form, M, N, K, act)) return "rgemm_kernel + gemm_reduce_f16_kernel";
+    if (use_skinny(t, r.form, N, act)) return "skinny_kernel";
+    if (use_sgemm(t, r.form, M, N, K)) {
+        gq::SGroupItem it;
+        gq::SGroupPlan g;
+        return sgemm_streamk(t, M, N, K, it, g) ? "sgemm_grouped_kernel + reduce_grouped_kernel (stream-K)"
+                                               : "sgemm_kernel + gemm_reduce_f16_kernel";
+    }
+    if (use_wgemm(t, r.form, N)) return "wgemm_kernel + wreduce_kernel";
+    return "gemm_kernel + gemm_reduce_f16_kernel";
+}

@@ -67,6 +67,7 @@ SIGNATURES = {
     "gq_mmq_grouped": ([ctypes.POINTER(GroupItem), _I, _I64, _P], _I),
     "gq_mmq_grouped_ex": ([_I, ctypes.POINTER(GroupItem), _I, _I64, _P], _I),
     "gq_act_prepare_grouped": ([_I, ctypes.POINTER(PrepItem), _I, _P], _I),
+    "gq_debug_route": ([_I, _I, _I64, _I64, _I64, _I], ctypes.c_char_p),
     "gq_mmq_grouped_prepared_workspace_size": ([_I, ctypes.POINTER(GemmItem), _I, _I64], _SZ),
     "gq_mmq_grouped_prepared": ([_I, ctypes.POINTER(GemmItem), _I, _I64, _P, _SZ, _P], _I),
     "gq_last_error": ([], ctypes.c_char_p),
@@ -101,6 +102,11 @@ def set_tuning(key: str, value: int):
     library reads the environment once, so setting os.environ later has no effect)."""
     _call_ws.clear()  # (the workspace a shape needs depends on the tuning)
     _check(lib().gq_debug_set_tuning(key.encode(), int(value)))
+
+
+def route_name(gtype: int, M: int, N: int, K: int, act: str = "q8_1", prepared: bool = False) -> str:
+    """The kernel(s) the library would launch for this call (gq_debug_route)."""
+    return lib().gq_debug_route(gtype, ACTS[act], M, N, K, int(prepared)).decode()
 
 
 def reset_tuning():

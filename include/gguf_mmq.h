@@ -250,6 +250,11 @@ int gq_version(void);
  */
 int gq_debug_set_tuning(const char *key, long long value);
 void gq_debug_reset_tuning(void);
+/* The kernel(s) a gq_mmq_ex call (prepared = 0) or a gq_mmq_prepared_ex call (prepared = 1) of
+ * this shape would launch under the current tuning ("none" for an invalid shape): what bench.py
+ * names as its roofline kernel.  Split-K reduce kernels are listed whether or not the plan
+ * splits. */
+const char *gq_debug_route(gq_type t, gq_act act, int64_t M, int64_t N, int64_t K, int prepared);
 
 #ifdef __cplusplus
 }
