@@ -466,6 +466,10 @@ class ShardStep:
             body(1, copies[1 % n], True)
         torch.cuda.current_stream(self.dev).wait_stream(s)
         torch.cuda.synchronize(self.dev)
+        if self.world > 1 or _dist_on():
+            # let the watchdog reap the warm steps' finished work (it polls every ~100 ms)
+            # before anything is recorded inside the capture
+            time.sleep(0.3)
         g = torch.cuda.CUDAGraph()
         # thread_local: the process group's watchdog thread polls its work events during capture
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
@@ -702,6 +706,11 @@ def bench_sharded(fmt, Mg, K, N, steps, warmup, dev, world, rank, cpu, unsharded
         out["speedup_vs_1gpu"] = {"compute": round(t1 / t["compute"], 3), "e2e_overlap": round(t1 / t["overlap"], 3),
                                   "e2e_chain": round(t1 / chains[best], 3)}
     return out
+
+
+def _dist_on() -> bool:
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
 
 
 def dist_backend():
@@ -952,6 +961,16 @@ def main():
     # graph capture on a 1-GPU box)
     cpu = os.environ.get("BENCH_REHEARSAL") == "1"
     multi = world > 1 or args.strong or os.environ.get("BENCH_FORCE_DIST") == "1"
+    if multi and not cpu:
+        # The process group's watchdog thread polls the end events of its enqueued work.  With
+        # its event cache on, an event can be recorded again inside a graph capture while a
+        # finished work still holds it, and the watchdog's query then fails with
+        # hipErrorCapturedEvent ("operation not permitted on an event last recorded in a
+        # capturing stream") -- which it rethrows, terminating the process (seen at world 1,
+        # profiles/r04/b6_tests.txt).  Fresh events per work, and a watchdog that logs CUDA
+        # errors instead of rethrowing them (set before the process group exists).
+        os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+        os.environ.setdefault("TORCH_NCCL_RETHROW_CUDA_ERRORS", "0")
     dev = torch.device("cpu") if cpu else torch.device("cuda", local)
     if multi:
         import torch.distributed as dist

@@ -23,7 +23,7 @@ for cfg in sys.argv[1:] or ["q8_0_4096x4096_m128"]:
     r = bench.Runner(fmt, M, K, N, dev, 4)
     r.prepare()
     for i in range(8):
-        r.kernel(i)
+        r.kernel(i, i % r.ncopies)
     torch.cuda.synchronize()
     buf = np.zeros((65536, 8), np.uint64)
     kl.lib().gq_debug_gemm_stamps.restype = ctypes.c_int

@@ -48,7 +48,7 @@ for spec in args:
         N = int(n)
     r = bench.Runner(fmt, M, K, N, dev, 40)
     r.prepare()
-    g = r.capture(r.step if STEP else r.kernel, 40)
+    g = r.capture(r.step if STEP else r.kernel, [i % r.ncopies for i in range(40)])
     g.replay()
     t = min(bench.timed_replay(g, dev) for _ in range(5)) / 40
     _, alg_bytes, flops = bench.model(fmt, M, K, N)

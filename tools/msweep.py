@@ -35,7 +35,7 @@ def main():
         row = {"shape": shp, "act": a.act, "tune": a.tune, "lib": os.path.basename(kl.LIB_PATH), "us": {}, "hbm_frac": {}}
         for N in (int(t) for t in a.tokens.split(",")):
             r = bench.Runner(fmt, M, K, N, dev, a.steps, act=a.act)
-            g = r.capture(r.step, a.steps)
+            g = r.capture(r.step, [i % r.ncopies for i in range(a.steps)])
             g.replay()
             t = min(bench.timed_replay(g, dev) for _ in range(3)) / a.steps
             _, alg, _ = bench.model(fmt, M, K, N)
