@@ -79,7 +79,10 @@ round)
   mkdir -p gpurun_out/round_prof && cd /tmp && export TMPDIR=/tmp &&
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/round_prof" -o run -- \
     python3 "$ROOT/bench.py" > "$ROOT/gpurun_out/round_prof/bench.json" 2> "$ROOT/gpurun_out/round_prof/bench.err" &&
-  python3 "$ROOT/tools/kstats.py" "$ROOT/gpurun_out/round_prof/run_kernel_stats.csv" > "$ROOT/gpurun_out/round_prof/kstats.txt" ;;
+  python3 "$ROOT/tools/kstats.py" "$ROOT/gpurun_out/round_prof/run_kernel_stats.csv" > "$ROOT/gpurun_out/round_prof/kstats.txt" &&
+  # the per-dispatch CSVs are summarized above (summary.txt, pmc_*.json, kstats.txt): drop them so
+  # gpurun_out stays under the copy-back limit
+  find "$ROOT/gpurun_out" \( -name "*kernel_trace.csv" -o -name "*counter_collection.csv" \) -delete ;;
 *)
   echo "unknown recipe: $cmd" >&2; exit 2 ;;
 esac
