@@ -194,6 +194,7 @@ def _stream(dev) -> int:
 
 
 _F16, _I8, _U8 = torch.float16, torch.int8, torch.uint8
+_empty, _get_device, _raw_stream = torch.empty, torch._C._cuda_getDevice, torch._C._cuda_getCurrentRawStream
 _mmq_ex = None  # the bound gq_mmq_ex (set on first use)
 
 
@@ -209,23 +210,26 @@ def mmq(gtype: int, A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int,
         ns, ks = B.shape
         if ns == N and ks == K and B.stride(1) == 1 and A.is_contiguous() and \
                 A.numel() == M * (K // BLOCK_ELEMS[gtype]) * BLOCK_BYTES[gtype]:
-            dev = A.device
-            if B.device != dev:
-                raise RuntimeError(f"A on {dev} but B on {B.device}")
+            idx = A.get_device()  # (an int: cheaper than building A.device)
+            if B.get_device() != idx:
+                raise RuntimeError(f"A on {A.device} but B on {B.device}")
             if M == 0 or N == 0:
-                return torch.empty((N, M), dtype=_F16, device=dev)
+                return _empty((N, M), dtype=_F16, device=A.device)
             key = (gtype, act, M, N, K)
             need = _call_ws.get(key)
             if need is None:
                 need = _call_ws[key] = int(lib().gq_mmq_call_workspace_size(gtype, ACTS[act], M, N, K))
             if _mmq_ex is None:
                 _mmq_ex = lib().gq_mmq_ex
-            idx = dev.index
-            if idx == torch._C._cuda_getDevice():
-                C = torch.empty((N, M), dtype=_F16, device=dev)
-                ws = torch.empty(need, dtype=_U8, device=dev) if need else None
-                rc = _mmq_ex(gtype, ACTS[act], A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, B.stride(0), M,
-                             ws.data_ptr() if need else None, need, torch._C._cuda_getCurrentRawStream(idx))
+            if idx == _get_device():
+                C = _empty((N, M), dtype=_F16, device=idx)
+                if need:
+                    ws = _empty(need, dtype=_U8, device=idx)
+                    rc = _mmq_ex(gtype, ACTS[act], A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, B.stride(0), M,
+                                 ws.data_ptr(), need, _raw_stream(idx))
+                else:
+                    rc = _mmq_ex(gtype, ACTS[act], A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, B.stride(0), M,
+                                 None, 0, _raw_stream(idx))
                 if rc:
                     _check(rc)
                 return C
