@@ -244,7 +244,7 @@ int64_t gemm_toks_per_launch(int64_t N, int64_t K)
 // Q6_K stay on the LDS-DMA GEMM (4096^2 x128 Q8_0 20.8 vs 17.3; Q6_K 28672x8192 x128 115.6 vs
 // 111.9).
 constexpr int64_t kWgemmMinTokens = 33;
-constexpr int64_t kRgemmMinTokens = 5;
+constexpr int64_t kRgemmMinTokens = 5, kRgemmMultiRoundTokens = 32, kRgemmMultiRoundTokensQ4 = 64;
 bool use_wgemm(int t, int form, int64_t N)
 {
     const int w = gq::tuning().wgemm;
@@ -315,9 +315,16 @@ bool use_rgemm(int t, int form, int64_t M, int64_t N, int64_t K)
     if (rg == 1) return true;
     if (gemm_knob_pinned() || N < kRgemmMinTokens) return false;
     // one round of the chip at the workgroups a CU holds (Q4_K at 16 tokens: three -- 11008x4096
-    // and 4096x11008 at 688 workgroups)
+    // and 4096x11008 at 688 workgroups); up to 32 tokens, up to four rounds (the one-super-block
+    // workgroups are short, so later rounds fill in behind the first; step us, default route ->
+    // resident, profiles/r04/b6_rg2.txt: Q4_K 22016x4096 x16 27.4 -> 21.6, x8 26.5 -> 20.9,
+    // 14336x4096 x16 18.3 -> 14.5, 4096x14336 x16 20.6 -> 14.6, 11008x4096 x32 22.3 -> 15.6;
+    // Q6_K 11008x4096 x16 22.2 -> 21.0; Q8_0 11008x4096 x16 20.1 -> 19.4)
     const int64_t grid = (int64_t)p.tiles_m * p.tiles_n * p.splits, cus = gq::num_cus();
-    return grid <= cus * gq::rgemm_per_cu(t, p.nb) && 2 * grid >= cus;
+    // (Q4_K to 64 tokens: 11008x4096 x48/x64 25.3/25.4 -> 19.5/20.5, 22016x4096 x64 40.6 -> 36.6,
+    // 4096x11008 x64 23.1 -> 18.7; not at 128, nor Q6_K at 64: profiles/r04/b7_rg64.txt)
+    const int64_t rounds = N <= (t == GQ_Q4_K ? kRgemmMultiRoundTokensQ4 : kRgemmMultiRoundTokens) ? 4 : 1;
+    return grid <= rounds * cus * gq::rgemm_per_cu(t, p.nb) && 2 * grid >= cus;
 }
 
 // The resident GEMM where it applies, ahead of the skinny kernel (4096^2 x16 step: Q4_K 6.8 vs
