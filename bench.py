@@ -756,7 +756,7 @@ def bench_config(name, steps, warmup, dev):
     return out
 
 
-def bench_layer(Ns, acts, steps, warmup, dev, fuse=True, grouped="auto"):
+def bench_layer(Ns, acts, steps, warmup, dev, fuse=True, grouped="auto", gemm_grouped_min=None):
     """BASELINE configs[4]: the seven projections of a Llama-7B block under GGUF Q4_K_M (layer 0:
     attn_v and ffn_down in Q6_K, the rest Q4_K), shared inputs quantized once per group
     (kernels.layer_mix.LayerMix; fuse: q+k and gate+up as one call each), for each token count in
@@ -774,7 +774,7 @@ def bench_layer(Ns, acts, steps, warmup, dev, fuse=True, grouped="auto"):
              for n in LLAMA_LAYER_SHAPES} for c in range(ncopies)]
     res = []
     for act in acts:
-        layers = [LayerMix(lin, act=act, fuse=fuse, grouped=grouped) for lin in lins]
+        layers = [LayerMix(lin, act=act, fuse=fuse, grouped=grouped, gemm_grouped_min=gemm_grouped_min) for lin in lins]
         for N in Ns:
             g = torch.Generator(device=dev).manual_seed(7)
             x = torch.randn(N, 4096, device=dev, generator=g).to(torch.float16)

@@ -128,10 +128,74 @@ __device__ __forceinline__ uint32_t b02(uint32_t c) { return __builtin_amdgcn_pe
 __device__ __forceinline__ uint32_t b13(uint32_t c) { return __builtin_amdgcn_perm(0x64646464u, c, 0x04030401u); }
 __device__ __forceinline__ uint32_t n02(uint32_t v) { return (v & 0x000f000fu) | 0x64006400u; }
 
-template <int F, int NT>
+// NS (two or more tokens): the code pairs made exact (1024 + c - bias as one v_pk_add) so no
+// quarter sums are needed -- Q8_0 and Q6_K keep none in LDS, Q4_K only the per-32 x~ sum of its
+// min term (a.s[t][0], a.s[t][2]): the 2-token x~ image of an 11008-long row then fits beside
+// the ring (the sums were the 384 bytes over)
+template <int F, int NT, bool NS = false>
 __device__ __forceinline__ void dot_unit_h(const UnitRaw<F> &r, const ActH<NT> &a, float (&acc)[NT])
 {
-    if constexpr (F == Q8_0) { // codes + 128 (xor 0x80): pairs 1152 + q
+    typedef _Float16 hb2 __attribute__((ext_vector_type(2)));
+    auto unbias = [](uint32_t v, float b) {
+        const hb2 bb = {(_Float16)b, (_Float16)b};
+        return __builtin_bit_cast(uint32_t, __builtin_bit_cast(hb2, v) - bb);
+    };
+    if constexpr (NS && F == Q8_0) {
+        uint32_t p[32];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t c = r.w[i] ^ 0x80808080u;
+            p[2 * i] = unbias(b02(c), 1152.f);
+            p[2 * i + 1] = unbias(b13(c), 1152.f);
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                s0 = fdot2u(p[i], a.x[t][i], s0);
+                s1 = fdot2u(p[16 + i], a.x[t][16 + i], s1);
+            }
+            acc[t] += r.d0 * s0 + r.d1 * s1;
+        }
+    } else if constexpr (NS && F == Q4_K) {
+        uint32_t p[32];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            p[2 * i] = unbias(n02(r.w[i]), 1024.f);
+            p[2 * i + 1] = unbias(n02(r.w[i] >> 8), 1024.f);
+            p[16 + 2 * i] = unbias(n02(r.w[i] >> 4), 1024.f);
+            p[16 + 2 * i + 1] = unbias(n02(r.w[i] >> 12), 1024.f);
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                s0 = fdot2u(p[i], a.x[t][i], s0);
+                s1 = fdot2u(p[16 + i], a.x[t][16 + i], s1);
+            }
+            acc[t] += r.ds0 * s0 - r.dm0 * a.s[t][0] + r.ds1 * s1 - r.dm1 * a.s[t][2];
+        }
+    } else if constexpr (NS) { // Q6_K: pairs (c - 32)
+        uint32_t p[32];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            p[2 * i] = unbias(b02(r.ca[i]), 1056.f);
+            p[2 * i + 1] = unbias(b13(r.ca[i]), 1056.f);
+            p[16 + 2 * i] = unbias(b02(r.cb[i]), 1056.f);
+            p[16 + 2 * i + 1] = unbias(b13(r.cb[i]), 1056.f);
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            float q[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) q[k] = fdot2u(p[8 * k + i], a.x[t][8 * k + i], q[k]);
+            acc[t] += r.fa1 * q[0] + r.fa2 * q[1] + r.fb1 * q[2] + r.fb2 * q[3];
+        }
+    } else if constexpr (F == Q8_0) { // codes + 128 (xor 0x80): pairs 1152 + q
         uint32_t p[32];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {

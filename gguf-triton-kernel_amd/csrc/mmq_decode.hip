@@ -201,6 +201,8 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
     float *sd = (float *)(codes + NT * kp * (FP8 ? 2 : 1)); // FP8: quarter sums [NT][2*nb]
     float *sx = sd + NT * nb; // Q4_K: s [NT][nb] (float); Q6_K: code sums [NT][2*nb] (int)
     static_assert(!FP8 || NT == 1 || ITC == 0, "fp8 decode: cached activations at one token only");
+    // FP8 at 2+ tokens: exact code pairs, no quarter sums (gguf_dot.hpp dot_unit_h NS; act_lds)
+    constexpr bool F8NS = FP8 && NT >= 2;
     // FP8: x~ 16-byte piece P of a token row at piece P ^ ((P >> 4) & 7) (the lanes of a unit
     // read hit distinct banks)
     auto xpiece = [](int P) { return P ^ ((P >> 4) & 7); };
@@ -324,7 +326,12 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
         tok_split(b, t, j);
         const int P = 4 * j + (lane & 3); // 16-byte piece of the token row
         *(u32x4 *)(codes + 2 * t * kp + 16 * xpiece(P)) = (u32x4){f.xt[0], f.xt[1], f.xt[2], f.xt[3]};
-        if ((lane & 1) == 0) sd[t * 2 * nb + 2 * j + ((lane >> 1) & 1)] = ls;
+        if constexpr (F8NS) { // (Q4_K: the block's sum, two quarters; Q8_0 / Q6_K: no sums)
+            if constexpr (F == Q4_K)
+                if ((lane & 3) == 0) sd[t * nb + j] = ls;
+        } else {
+            if ((lane & 1) == 0) sd[t * 2 * nb + 2 * j + ((lane >> 1) & 1)] = ls;
+        }
     };
     auto quantize = [&](int r, const u32x4 (&xv)[XP]) {
         const int np = npass(r);
@@ -338,6 +345,8 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
 #pragma unroll
                     for (int i = 0; i < 4; ++i) ls += h2f(f.xt[i] & 0xffffu) + h2f(f.xt[i] >> 16);
                     ls += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, ls), 0xb1, 0xf, 0xf, false));
+                    if constexpr (F8NS && F == Q4_K) // + the other lane pair's quarter: the 32-block's sum
+                        ls += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, ls), 0x4e, 0xf, 0xf, false));
                     if (b < xblocks) store_f(b, f, ls);
                 } else {
                     const Q81Quad qq = q8_1_quad(xv[q]);
@@ -438,6 +447,13 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
                     a.x[t][16 * rr + 4 * i + 2] = v.z;
                     a.x[t][16 * rr + 4 * i + 3] = v.w;
                 }
+            if constexpr (F8NS) {
+                if constexpr (F == Q4_K) { // the two 32-blocks' sums
+                    a.s[t][0] = sd[t * nb + (e0 >> 5)];
+                    a.s[t][2] = sd[t * nb + (e1 >> 5)];
+                }
+                continue;
+            }
             const float *sq = sd + t * 2 * nb;
             a.s[t][0] = sq[e0 >> 4];
             a.s[t][1] = sq[(e0 >> 4) + 1];
@@ -459,11 +475,11 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
     // the contribution of unit u (activation slot i when cached) of the row at rowp
     auto unit = [&](const UnitLoad<F> &l, int u, int i, float (&acc)[NT]) {
         if constexpr (FP8 && ITC > 0) {
-            dot_unit_h<F, NT>(UnitRaw<F>::from(l, u, nb), ch[i], acc);
+            dot_unit_h<F, NT, F8NS>(UnitRaw<F>::from(l, u, nb), ch[i], acc);
         } else if constexpr (FP8) {
             ActH<NT> a;
             act_h(a, u);
-            dot_unit_h<F, NT>(UnitRaw<F>::from(l, u, nb), a, acc);
+            dot_unit_h<F, NT, F8NS>(UnitRaw<F>::from(l, u, nb), a, acc);
         } else if constexpr (ITC > 0) {
             dot_unit<F, NT>(UnitRaw<F>::from(l, u, nb), ca[i], acc);
         } else {
@@ -664,7 +680,8 @@ struct Pick {
 size_t act_lds(int fmt, int nt, int64_t K, bool fp8 = false)
 {
     const int64_t kp = (K + 63) / 64 * 64, nb = K / 32;
-    if (fp8) return (size_t)nt * kp * 2 + (size_t)nt * nb * 2 * 4; // x~ + quarter sums
+    if (fp8) // x~ + quarter sums (2+ tokens: Q4_K's block sums only, gguf_dot.hpp dot_unit_h NS)
+        return (size_t)nt * kp * 2 + (nt == 1 ? (size_t)nt * nb * 2 * 4 : (fmt == Q4_K ? (size_t)nt * nb * 4 : 0));
     return (size_t)nt * kp + (size_t)nt * nb * 4 * (fmt == Q8_0 ? 1 : (fmt == Q4_K ? 2 : 3));
 }
 

@@ -58,13 +58,14 @@ class LayerMix:
 
     GROUPS = (("attn_q", "attn_k", "attn_v"), ("attn_output",), ("ffn_gate", "ffn_up"), ("ffn_down",))
 
-    def __init__(self, linears: dict, act: str = "q8_1", fuse: bool = True, grouped="auto"):
+    def __init__(self, linears: dict, act: str = "q8_1", fuse: bool = True, grouped="auto",
+                 gemm_grouped_min: int | None = None):
         self.act = act  # "q8_1" (the reference's activation quantization) or "fp8" (e4m3 variant)
         # one gq_mmq_grouped launch for the whole layer: "auto" / True at 1..4 tokens, False never
         self.max_grouped = GROUPED_MAX_TOKENS[grouped]
         # one gq_mmq_grouped_prepared launch (the streaming GEMM) for the whole layer from this
         # many tokens ("auto" / True; False never)
-        self.min_gemm_grouped = GEMM_GROUPED_MIN_TOKENS[grouped]
+        self.min_gemm_grouped = GEMM_GROUPED_MIN_TOKENS[grouped] if gemm_grouped_min is None else gemm_grouped_min
         self.lin = {}     # name -> GGUFLinear (unfused projections)
         self.parts = {}   # name -> (fused key, first column, rows)
         # per input group: the calls to make, each (key, GGUFLinear); fused keys join names by "+"

@@ -22,9 +22,11 @@ if "--tune" in args:  # library tuning overrides (gq_debug_set_tuning)
         k, v = kv.split("=")
         kl.set_tuning(k, int(v))
 act = args[args.index("--act") + 1] if "--act" in args else "q8_1"
-pos = [a for i, a in enumerate(args) if not a.startswith("--") and (i == 0 or args[i - 1] not in ("--lib", "--tune", "--act"))]
+gmin = int(args[args.index("--gemm-min") + 1]) if "--gemm-min" in args else None  # LayerMix gemm_grouped_min
+pos = [a for i, a in enumerate(args)
+       if not a.startswith("--") and (i == 0 or args[i - 1] not in ("--lib", "--tune", "--act", "--gemm-min"))]
 Ns = tuple(int(n) for n in (pos[0] if pos else "1,2,3,4").split(","))
 for grouped in ((True,) if "--grouped-only" in args else (True, False)):  # (True: grouped at 1..4 tokens)
-    r = bench.bench_layer(Ns, (act,), 50, 5, dev, fuse=True, grouped=grouped)
-    print(json.dumps({"grouped": grouped, "act": act, "tune": args[args.index("--tune") + 1] if "--tune" in args else "", "lib": os.path.basename(lib or "libgguf_mmq.so"), "weight_bytes": r["weight_bytes"],
+    r = bench.bench_layer(Ns, (act,), 50, 5, dev, fuse=True, grouped=grouped, gemm_grouped_min=gmin)
+    print(json.dumps({"grouped": grouped, "act": act, "tune": args[args.index("--tune") + 1] if "--tune" in args else "", "gemm_min": gmin, "lib": os.path.basename(lib or "libgguf_mmq.so"), "weight_bytes": r["weight_bytes"],
                       "points": [(p["M_tok"], p["us_per_step"], p["weight_GBps"]) for p in r["points"]]}), flush=True)
