@@ -41,6 +41,7 @@ struct Tuning {
     int sgemm = -1;                           // GQ_SGEMM: streaming 256-row GEMM -1 auto / 0 off / 1 wherever it applies
     int sgemm_splits = 0;                     // GQ_SGEMM_SPLITS (0: auto)
     int sgemm_streamk = 0;                    // GQ_SGEMM_STREAMK: stream-K unit split of the auto plan (measured: no gain)
+    int rgemm_nb = 0;                         // GQ_RGEMM_NB: the resident GEMM's token tile, 1/2/4/8 x 16 (0: auto)
     int rgemm_spol = 16;                      // GQ_RGEMM_SPOL: its partial stores' cache policy 0 / 2 (nt) / 16 (sc1)
     int cus = 0;                              // GQ_CUS: compute units to plan for (0: the device's count)
     int ablate = 0;                           // GQ_ABLATE (GQ_ABLATION diagnostic builds only)

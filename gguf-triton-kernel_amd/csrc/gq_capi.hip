@@ -40,6 +40,10 @@ bool parse_key(Tuning &t, const char *key, long long v)
     } else if (k == "GQ_DECODE_NT4_CACHE") t.decode_nt4_cache = v != 0;
     else if (k == "GQ_DECODE_F8_ITC") t.decode_f8_itc = v != 0;
     else if (k == "GQ_SGEMM_STREAMK") t.sgemm_streamk = v != 0;
+    else if (k == "GQ_RGEMM_NB") {
+        if (!in({0, 1, 2, 4, 8})) return false;
+        t.rgemm_nb = (int)v;
+    }
     else if (k == "GQ_DECODE_EARLY") {
         if (!in({-1, 0, 1, 2})) return false;
         t.decode_early = (int)v;
@@ -122,7 +126,7 @@ void tuning_from_env(Tuning &t)
                                        "GQ_GEMM_NB", "GQ_GEMM_RG", "GQ_GEMM_LOADERS", "GQ_GEMM_SPLITS",
                                        "GQ_GEMM_PARTIAL", "GQ_GEMM_FUSED_REDUCE", "GQ_GEMV_CAP", "GQ_GEMV_R",
                                        "GQ_WGEMM", "GQ_WGEMM_RG", "GQ_WGEMM_NB", "GQ_WGEMM_SPLITS", "GQ_WGEMM_WD",
-                                       "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D", "GQ_RGEMM", "GQ_SGEMM", "GQ_SGEMM_SPLITS", "GQ_SGEMM_STREAMK", "GQ_RGEMM_SPOL", "GQ_CUS", "GQ_ABLATE"};
+                                       "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D", "GQ_RGEMM", "GQ_SGEMM", "GQ_SGEMM_SPLITS", "GQ_SGEMM_STREAMK", "GQ_RGEMM_NB", "GQ_RGEMM_SPOL", "GQ_CUS", "GQ_ABLATE"};
     for (const char *k : keys) {
         const char *e = getenv(k); // the only getenv of the library: once per process
         if (!e || !*e) continue;

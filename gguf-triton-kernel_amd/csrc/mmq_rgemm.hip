@@ -673,6 +673,7 @@ RGemmPlan plan_rgemm(int64_t M, int64_t N, int64_t K)
     RGemmPlan p;
     if (M < 1 || N < 1 || K < 256 || K % 256 != 0) return p;
     p.nb = N > 64 ? 8 : (N > 32 ? 4 : (N > 16 ? 2 : 1));
+    if (tuning().rgemm_nb > 0) p.nb = tuning().rgemm_nb; // (A/B knob)
     p.tiles_m = (int)((M + RBM - 1) / RBM);
     p.tiles_n = (int)((N + 16 * p.nb - 1) / (16 * p.nb));
     p.splits = (int)(K / 256);
