@@ -76,7 +76,10 @@ __device__ __forceinline__ void act_quant_body(const uint16_t *__restrict__ X, i
         }
     } else if constexpr (MODE == ACT_I8) {
         *(u32x2 *)(codes + row * K + 32 * j + 8 * sub) = (u32x2){q.codes[0], q.codes[1]};
-        if (sub == 0) dout[j * ((rows + 3) & ~(int64_t)3) + row] = q.d;
+        if (sub == 0) {
+            dout[j * ((rows + 3) & ~(int64_t)3) + row] = q.d;
+            if (sout) sout[j * ((rows + 3) & ~(int64_t)3) + row] = h2f(q.sbits); // (the integer-MFMA skinny kernel's s)
+        }
     } else {
         // x~ = fp16(d*q); each 4-element group in the order (0,2,1,3): the order mmq_gemm.hip's
         // packed dequantization produces weight pairs in (its k-permutation; the MFMA k-sum is
@@ -163,7 +166,7 @@ hipError_t launch_act_quant(int mode, const uint16_t *X, int64_t ldx, int64_t ro
         break;
     case ACT_I8:
         act_quant_kernel<ACT_I8><<<grid, block, 0, s>>>(X, ldx, rows, K, nullptr, (int8_t *)out0, (float *)out1,
-                                                         nullptr, nullptr);
+                                                         (float *)out2, nullptr);
         break;
     default:
         act_quant_kernel<ACT_DEQ><<<grid, block, 0, s>>>(X, ldx, rows, K, nullptr, nullptr, nullptr, nullptr,

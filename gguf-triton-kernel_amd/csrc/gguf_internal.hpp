@@ -41,6 +41,8 @@ struct Tuning {
     int sgemm = -1;                           // GQ_SGEMM: streaming 256-row GEMM -1 auto / 0 off / 1 wherever it applies
     int sgemm_splits = 0;                     // GQ_SGEMM_SPLITS (0: auto)
     int sgemm_streamk = 0;                    // GQ_SGEMM_STREAMK: stream-K unit split of the auto plan (measured: no gain)
+    int iskinny = 0;                          // GQ_ISKINNY: integer-MFMA skinny kernel (Q4_K 5..16 tokens) 0 off / 1 on
+    int iskinny_rg = 0;                       // GQ_ISKINNY_RG: its 16-row fragments per unit, 1..4 (0: auto)
     int rgemm_nb = 0;                         // GQ_RGEMM_NB: the resident GEMM's token tile, 1/2/4/8 x 16 (0: auto)
     int rgemm_spol = 16;                      // GQ_RGEMM_SPOL: its partial stores' cache policy 0 / 2 (nt) / 16 (sc1)
     int cus = 0;                              // GQ_CUS: compute units to plan for (0: the device's count)
@@ -144,6 +146,11 @@ struct RGemmPlan {
     int nb = 8, tiles_m = 0, tiles_n = 0, splits = 1;
     size_t partial_bytes = 0;
 };
+// Integer-MFMA skinny kernel (mmq_iskinny.hip): Q4_K, 1..16 tokens, act_quant's I8 form
+// (codes [N][K], d and s block-major [K/32][ldd], s at Xs)
+int iskinny_rg(int64_t M);
+hipError_t launch_iskinny(int fmt, const uint8_t *A, const int8_t *Xq, const float *Xd, const float *Xs, int64_t ldd,
+                          uint16_t *C, int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
 RGemmPlan plan_rgemm(int64_t M, int64_t N, int64_t K);
 // resident workgroups one CU holds at once (LDS-bound: Q4_K at 16 tokens 3, at 32 two, else one)
 int rgemm_per_cu(int fmt, int nb);

@@ -40,6 +40,11 @@ bool parse_key(Tuning &t, const char *key, long long v)
     } else if (k == "GQ_DECODE_NT4_CACHE") t.decode_nt4_cache = v != 0;
     else if (k == "GQ_DECODE_F8_ITC") t.decode_f8_itc = v != 0;
     else if (k == "GQ_SGEMM_STREAMK") t.sgemm_streamk = v != 0;
+    else if (k == "GQ_ISKINNY") t.iskinny = v != 0;
+    else if (k == "GQ_ISKINNY_RG") {
+        if (v < 0 || v > 4) return false;
+        t.iskinny_rg = (int)v;
+    }
     else if (k == "GQ_RGEMM_NB") {
         if (!in({0, 1, 2, 4, 8})) return false;
         t.rgemm_nb = (int)v;
@@ -126,7 +131,7 @@ void tuning_from_env(Tuning &t)
                                        "GQ_GEMM_NB", "GQ_GEMM_RG", "GQ_GEMM_LOADERS", "GQ_GEMM_SPLITS",
                                        "GQ_GEMM_PARTIAL", "GQ_GEMM_FUSED_REDUCE", "GQ_GEMV_CAP", "GQ_GEMV_R",
                                        "GQ_WGEMM", "GQ_WGEMM_RG", "GQ_WGEMM_NB", "GQ_WGEMM_SPLITS", "GQ_WGEMM_WD",
-                                       "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D", "GQ_RGEMM", "GQ_SGEMM", "GQ_SGEMM_SPLITS", "GQ_SGEMM_STREAMK", "GQ_RGEMM_NB", "GQ_RGEMM_SPOL", "GQ_CUS", "GQ_ABLATE"};
+                                       "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D", "GQ_RGEMM", "GQ_SGEMM", "GQ_SGEMM_SPLITS", "GQ_SGEMM_STREAMK", "GQ_RGEMM_NB", "GQ_ISKINNY", "GQ_ISKINNY_RG", "GQ_RGEMM_SPOL", "GQ_CUS", "GQ_ABLATE"};
     for (const char *k : keys) {
         const char *e = getenv(k); // the only getenv of the library: once per process
         if (!e || !*e) continue;
@@ -340,6 +345,14 @@ bool rgemm_route(int t, int form, int64_t M, int64_t N, int64_t K, int act)
     return gq::tuning().skinny != 1 || !use_skinny(t, form, N, act);
 }
 
+// Integer-MFMA skinny kernel (mmq_iskinny.hip): Q4_K, 5..16 tokens, gq_mmq_ex only (it quantizes
+// into the I8 form itself; the prepared calls keep the fp16 routes).  GQ_ISKINNY=1: on.
+bool use_iskinny(int t, int form, int64_t M, int64_t N, int64_t K, int act)
+{
+    if (gq::tuning().iskinny != 1 || t != GQ_Q4_K || form != gq::AF_F16 || act != GQ_ACT_Q8_1) return false;
+    return N >= 5 && N <= 16 && K % 256 == 0 && M > 0 && M * (K / 256) * 144 < ((int64_t)1 << 31) && N * K < ((int64_t)1 << 31);
+}
+
 // Streaming 256-row GEMM (mmq_rgemm.hip sgemm_kernel) on the prepared x~, where the resident
 // form does not apply (its grid is more than one round of the chip, or under half of one): by
 // default from 17 tokens for every type, and Q6_K from 5 (the skinny kernel keeps Q4_K / Q8_0
@@ -424,7 +437,7 @@ size_t act_bytes(int act, int64_t N, int64_t K)
         // SOA q8_1: codes + d + s
         return align_up((size_t)N * K) + 2 * align_up((size_t)N * (K / 32) * sizeof(float));
     }
-    return deq_bytes(N, K) + code_bytes(N, K) + scale_bytes(N, K);
+    return deq_bytes(N, K) + code_bytes(N, K) + 2 * scale_bytes(N, K); // (+ s: the integer skinny kernel)
 }
 
 // Whole workspace: activations + (GEMM split-K) fp32 partial slabs / (library path) fp16 W.
@@ -618,12 +631,14 @@ static Carved carve(int act, void *workspace, int64_t N, int64_t K)
         c.xdeq = (uint16_t *)ws;
         c.xq = (int8_t *)(ws + deq_bytes(N, K));
         c.xd = (float *)(ws + deq_bytes(N, K) + code_bytes(N, K));
+        c.xs = (float *)((uint8_t *)c.xd + scale_bytes(N, K));
     }
     c.partials = (float *)(ws + act_bytes(act, N, K));
     return c;
 }
 
-// q8_1 forms: bit 0 = fp16 x~ (DEQ), bit 1 = int8 codes + d (I8); only the GEMM path reads them
+// q8_1 forms: bit 0 = fp16 x~ (DEQ), bit 1 = int8 codes + d (I8), bit 2 = with the I8 form, s
+// too (the integer skinny kernel); only the GEMM path reads them
 static int prepare(int act, const void *B, int64_t N, int64_t K, int64_t ldb, void *workspace,
                    size_t workspace_bytes, hipStream_t s, int forms = 1)
 {
@@ -641,7 +656,7 @@ static int prepare(int act, const void *B, int64_t N, int64_t K, int64_t ldb, vo
     } else {
         if (forms & 1) e = gq::launch_act_quant(gq::ACT_DEQ, (const uint16_t *)B, ldb, N, K, c.xdeq, nullptr, nullptr, s);
         if (e == hipSuccess && (forms & 2))
-            e = gq::launch_act_quant(gq::ACT_I8, (const uint16_t *)B, ldb, N, K, c.xq, c.xd, nullptr, s);
+            e = gq::launch_act_quant(gq::ACT_I8, (const uint16_t *)B, ldb, N, K, c.xq, c.xd, (forms & 4) ? c.xs : nullptr, s);
     }
     if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (act_quant): %s", hipGetErrorString(e));
     return GQ_OK;
@@ -746,6 +761,15 @@ int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int6
         hipError_t e = gq::launch_decode_fused(t, (const uint8_t *)A, (const uint16_t *)B, ldb, (uint16_t *)C, M, N,
                                                K, ldc, (hipStream_t)stream, act == GQ_ACT_FP8_E4M3);
         if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (decode): %s", hipGetErrorString(e));
+        return GQ_OK;
+    }
+    if (use_iskinny(t, r.form, M, N, K, act)) {
+        rc = prepare(act, B, N, K, ldb, workspace, workspace_bytes, (hipStream_t)stream, 2 | 4);
+        if (rc != GQ_OK) return rc;
+        Carved c = carve(act, workspace, N, K);
+        hipError_t e = gq::launch_iskinny(t, (const uint8_t *)A, c.xq, c.xd, c.xs, scale_ld(N), (uint16_t *)C, M, N, K, ldc,
+                                          (hipStream_t)stream);
+        if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (iskinny): %s", hipGetErrorString(e));
         return GQ_OK;
     }
     if (rgemm_route(t, r.form, M, N, K, act) && ldb % 8 == 0 &&
@@ -1107,6 +1131,7 @@ const char *gq_debug_route(gq_type t, gq_act act, int64_t M, int64_t N, int64_t 
     g_err.clear();
     const Route r = route(t, act, N, K);
     if (!prepared && fused_decode_route(t, act, N, K)) return "stream_decode_kernel";
+    if (!prepared && use_iskinny(t, route(t, act, N, K).form, M, N, K, act)) return "iskinny_q4k_kernel";
     if (r.blas) return "dequant_kernel + hipBLASLt";
     if (r.gemv) return "gemv_kernel";
     if (rgemm_route(t, r.form, M, N, K, act)) return "rgemm_kernel + gemm_reduce_f16_kernel";
