@@ -97,6 +97,24 @@ def lib():
     return _lib
 
 
+def _bind_mmq_ex():
+    """gq_mmq_ex as the eager path calls it: through lib/_gqcall (csrc/gq_pycall.c, a METH_FASTCALL
+    entry bound to the ctypes-loaded library's gq_mmq_ex -- ~0.2 us per call instead of ctypes'
+    ~1.5-2 us of argument conversion), or the ctypes function when that module was not built.
+    Both reach the same gq_mmq_ex in the same loaded libgguf_mmq.so."""
+    import glob
+    import importlib.util
+    fn = lib().gq_mmq_ex
+    paths = sorted(glob.glob(os.path.join(LIB_DIR, "_gqcall*.so")))
+    if not paths:
+        return fn
+    spec = importlib.util.spec_from_file_location("_gqcall", paths[0])
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    mod.bind(ctypes.cast(fn, ctypes.c_void_p).value)
+    return mod.mmq_ex
+
+
 def set_tuning(key: str, value: int):
     """Override one GQ_* tuning default by name for later calls (gq_debug_set_tuning; the
     library reads the environment once, so setting os.environ later has no effect)."""
@@ -220,7 +238,7 @@ def mmq(gtype: int, A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int,
             if need is None:
                 need = _call_ws[key] = int(lib().gq_mmq_call_workspace_size(gtype, ACTS[act], M, N, K))
             if _mmq_ex is None:
-                _mmq_ex = lib().gq_mmq_ex
+                _mmq_ex = _bind_mmq_ex()
             if idx == _get_device():
                 C = _empty((N, M), dtype=_F16, device=idx)
                 if need:

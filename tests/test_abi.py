@@ -214,3 +214,29 @@ def test_grouped_host_argument_checks():
     assert L.gq_mmq_grouped(arr, 2, 5, None) == kl.GQ_EUNSUPPORTED              # N = 5: not decode
     arr[1] = kl.GroupItem(kl.GQ_Q4_K, None, fake, 4096, fake, 4096, 64, 4096)    # null A
     assert L.gq_mmq_grouped(arr, 2, 1, None) == kl.GQ_EINVAL
+
+
+def test_fast_call_entry_matches_ctypes():
+    """lib/_gqcall (csrc/gq_pycall.c), the eager path's METH_FASTCALL hop into gq_mmq_ex, is built,
+    bound to the loaded library's gq_mmq_ex, and returns what the ctypes call returns on the same
+    arguments (host-side refusals here: nothing is launched)."""
+    import glob
+
+    import kernels._lib as kl
+    assert glob.glob(os.path.join(LIB, "_gqcall*.so")), "lib/_gqcall was not built"
+    fast = kl._bind_mmq_ex()
+    assert fast is not kl.lib().gq_mmq_ex and type(fast).__name__ == "builtin_function_or_method"
+    L = kl.lib()
+    p = 16
+    for args in [(7, 0, p, p, p, 4, 4, 256, 256, 4, p, 1 << 20, 0),       # unknown type
+                 (1, 9, p, p, p, 8, 4, 256, 256, 8, p, 1 << 20, 0),       # unknown activation
+                 (1, 0, p, p, p, 4, 4, 100, 100, 4, p, 1 << 20, 0),       # K % 256
+                 (1, 0, 0, p, p, 4, 4, 256, 256, 4, p, 1 << 20, 0),       # null A
+                 (1, 0, p, p, p, 4, 64, 256, 256, 4, None, 0, 0),         # workspace missing
+                 (1, 0, None, None, None, 0, 4, 256, 256, 4, None, 0, 0)]:  # empty: a no-op
+        want = L.gq_mmq_ex(*args)
+        assert fast(*args) == want, args
+    with pytest.raises(TypeError):
+        fast(1, 2)
+    with pytest.raises(TypeError):
+        fast(1, 0, "x", p, p, 4, 4, 256, 256, 4, p, 0, 0)
