@@ -93,11 +93,13 @@ __device__ __forceinline__ void q4k_frags(const uint8_t *hdrp, const uint8_t *w3
     for (int n = 0; n < 2; ++n) { // n = 0: low nibbles (sub-block 2q), 1: high (2q+1)
         const h2 ds = splat(d * (float)((sc >> (sh + 8 * n)) & 0xffu));
         const h2 ndm = splat(-(dmin * (float)((mn >> (sh + 8 * n)) & 0xffu)));
-        const uint32_t x0 = w.x >> (4 * n), x1 = w.y >> (4 * n);
-        frag[n] = frag4(__builtin_elementwise_fma(magic(x0, 0x000f000fu) + bias, ds, ndm),
-                        __builtin_elementwise_fma(magic(x0 >> 8, 0x000f000fu) + bias, ds, ndm),
-                        __builtin_elementwise_fma(magic(x1, 0x000f000fu) + bias, ds, ndm),
-                        __builtin_elementwise_fma(magic(x1 >> 8, 0x000f000fu) + bias, ds, ndm));
+        // the nibbles as bytes, then (1024 + code) pairs by byte permutes: one mask per word and
+        // one v_perm per pair (the same values as masking each pair into 0x6400 0x6400)
+        const uint32_t x0 = (w.x >> (4 * n)) & 0x0f0f0f0fu, x1 = (w.y >> (4 * n)) & 0x0f0f0f0fu;
+        frag[n] = frag4(__builtin_elementwise_fma(pair02(x0) + bias, ds, ndm),
+                        __builtin_elementwise_fma(pair13(x0) + bias, ds, ndm),
+                        __builtin_elementwise_fma(pair02(x1) + bias, ds, ndm),
+                        __builtin_elementwise_fma(pair13(x1) + bias, ds, ndm));
     }
 }
 template <>
