@@ -40,7 +40,8 @@ struct Tuning {
     int rgemm = -1;                           // GQ_RGEMM: resident-split GEMM -1 auto / 0 off / 1 wherever it applies
     int sgemm = -1;                           // GQ_SGEMM: streaming 256-row GEMM -1 auto / 0 off / 1 wherever it applies
     int sgemm_splits = 0;                     // GQ_SGEMM_SPLITS (0: auto)
-    int sgemm_streamk = 0;                    // GQ_SGEMM_STREAMK: stream-K unit split of the auto plan (measured: no gain)
+    int sgemm_streamk = -1;                   // GQ_SGEMM_STREAMK: stream-K unit split of the auto plan: 1 every
+                                              // streaming GEMM, 0 none, -1 the grouped plans (the measured gain)
     int iskinny = 0;                          // GQ_ISKINNY: integer-MFMA skinny kernel (Q4_K 5..16 tokens) 0 off / 1 on
     int iskinny_rg = 0;                       // GQ_ISKINNY_RG: its 16-row fragments per unit, 1..4 (0: auto)
     int rgemm_nb = 0;                         // GQ_RGEMM_NB: the resident GEMM's token tile, 1/2/4/8 x 16 (0: auto)

@@ -39,7 +39,7 @@ bool parse_key(Tuning &t, const char *key, long long v)
         t.decode_maxnt = (int)v;
     } else if (k == "GQ_DECODE_NT4_CACHE") t.decode_nt4_cache = v != 0;
     else if (k == "GQ_DECODE_F8_ITC") t.decode_f8_itc = v != 0;
-    else if (k == "GQ_SGEMM_STREAMK") t.sgemm_streamk = v != 0;
+    else if (k == "GQ_SGEMM_STREAMK") t.sgemm_streamk = v < 0 ? -1 : (v != 0);
     else if (k == "GQ_ISKINNY") t.iskinny = v != 0;
     else if (k == "GQ_ISKINNY_RG") {
         if (v < 0 || v > 4) return false;
@@ -381,7 +381,7 @@ gq::RGemmPlan sgemm_plan(int64_t M, int64_t N, int64_t K) { return gq::plan_sgem
 // partials; profiles/r04/b4_sk.txt), so off by default.
 bool sgemm_streamk(int t, int64_t M, int64_t N, int64_t K, gq::SGroupItem &it, gq::SGroupPlan &g)
 {
-    if (gq::tuning().sgemm_splits > 0 || !gq::tuning().sgemm_streamk) return false;
+    if (gq::tuning().sgemm_splits > 0 || gq::tuning().sgemm_streamk <= 0) return false;
     it = gq::SGroupItem{t, nullptr, nullptr, nullptr, M, M, K};
     g = gq::plan_sgemm_grouped(&it, 1, N, 0);
     return g.ok && g.streamk;

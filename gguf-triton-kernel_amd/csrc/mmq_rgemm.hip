@@ -737,12 +737,15 @@ SGroupPlan plan_sgemm_grouped(const SGroupItem *items, int n, int64_t N, int spl
     for (int i = 0; i < n; ++i) tiles += (int64_t)g.tiles_m[i] * tn;
     if (tiles > cus) return g;
     g.tiles_n = tn;
-    if (splits <= 0 && tuning().sgemm_streamk && units < ((int64_t)1 << 30)) {
-        // stream-K (GQ_SGEMM_STREAMK=1): the units (tile, super-block), part by part and tile by
-        // tile, split evenly over one round of the chip -- every workgroup L or L+1 super-blocks,
-        // where whole-tile splits leave the largest part's workgroups up to ceil(nsb / L) (a 7B
-        // layer at 128 tokens: 16 super-blocks on 198 workgroups vs 12-13 on 256).  Measured no
-        // faster (layer x128 102.1 vs 102.6 us; single matrices slower, gq_capi.hip sgemm_streamk)
+    const int sk = tuning().sgemm_streamk;
+    if (splits <= 0 && sk != 0 && units < ((int64_t)1 << 30)) {
+        // stream-K: the units (tile, super-block), part by part and tile by tile, split evenly
+        // over one round of the chip -- every workgroup L or L+1 super-blocks, where whole-tile
+        // splits leave the largest part's workgroups up to ceil(nsb / L) (a 7B layer at 128
+        // tokens: 16 super-blocks on 198 workgroups vs 12-13 on 256).  The grouped default
+        // (a 7B layer at 8 / 32 / 64 / 128 tokens: 64.1 / 67.2 / 80.6 / 102.1 us against 66.3
+        // per call / 72.7 / 82.0 / 102.6 whole-tile splits: profiles/r04/ab9_layer.txt); single
+        // matrices measured slower (GQ_SGEMM_STREAMK=1 forces it there, gq_capi.hip sgemm_streamk)
         const int W = (int)(units < cus ? units : cus), U = (int)units;
         auto first_wg = [&](int64_t u0) { return (int)(((u0 + 1) * W + U - 1) / U) - 1; };
         auto last_wg = [&](int64_t u1) { return (int)((u1 * W + U - 1) / U) - 1; };

@@ -31,8 +31,9 @@ from . import _lib
 
 # grouped= setting -> the most tokens LayerMix runs as one grouped decode launch
 GROUPED_MAX_TOKENS = {"auto": 4, True: 4, False: 0}
-# grouped= setting -> the fewest tokens LayerMix runs as one grouped streaming-GEMM launch
-GEMM_GROUPED_MIN_TOKENS = {"auto": 17, True: 17, False: 1 << 62}
+# grouped= setting -> the fewest tokens LayerMix runs as one grouped streaming-GEMM launch (the
+# stream-K plan: a 7B layer at 8 tokens 64.1 vs 66.3 us one call per set; profiles/r04/ab9_layer.txt)
+GEMM_GROUPED_MIN_TOKENS = {"auto": 5, True: 5, False: 1 << 62}
 
 
 class GGUFLinear:

@@ -170,10 +170,10 @@ def test_grouped_gemm_refuses():
     assert torch.all(out == 3.0)
 
 
-@pytest.mark.parametrize("N", [17, 128, 512])
+@pytest.mark.parametrize("N", [5, 8, 16, 17, 128, 512])
 def test_layer_mix_grouped_gemm_route(N):
-    """LayerMix from 17 tokens runs the layer as one grouped GEMM launch: within the GEMM
-    tolerance of its per-call route (grouped=False), `out` buffers honoured."""
+    """LayerMix from 5 tokens runs the layer as one grouped GEMM launch (the stream-K plan):
+    within the GEMM tolerance of its per-call route (grouped=False), `out` buffers honoured."""
     from gguf import LLAMA_LAYER_SHAPES, q4_k_m_layer_types
     from kernels.layer_mix import GGUFLinear, LayerMix
     dev = _dev()
