@@ -46,6 +46,9 @@ struct Tuning {
     int iskinny_rg = 0;                       // GQ_ISKINNY_RG: its 16-row fragments per unit, 1..4 (0: auto)
     int rgemm_nb = 0;                         // GQ_RGEMM_NB: the resident GEMM's token tile, 1/2/4/8 x 16 (0: auto)
     int rgemm_spol = 16;                      // GQ_RGEMM_SPOL: its partial stores' cache policy 0 / 2 (nt) / 16 (sc1)
+    int rgemm_xcd = 0;                        // GQ_RGEMM_XCD: workgroup -> tile order per XCD (mmq_rgemm.hip xcd_tile):
+                                              // 0 blockIdx as is, 1 a tile's splits consecutive, 2 a split's row tiles
+    int sgemm_xcd = 0;                        // GQ_SGEMM_XCD: the same for the (single-matrix) streaming GEMM
     int cus = 0;                              // GQ_CUS: compute units to plan for (0: the device's count)
     int ablate = 0;                           // GQ_ABLATE (GQ_ABLATION diagnostic builds only)
 };

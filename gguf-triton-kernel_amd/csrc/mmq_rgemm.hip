@@ -147,6 +147,27 @@ __device__ __forceinline__ TileId grid_tile()
 {
     return TileId{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y, (int)gridDim.z};
 }
+// XCD-aware order (GQ_RGEMM_XCD / GQ_SGEMM_XCD): the hardware deals workgroups out to the 8 XCDs
+// round-robin by linear id, each XCD with its own L2.  xpol 0 keeps blockIdx; otherwise the
+// workgroups one XCD receives take consecutive ids w of a bijective remap (blocks of ceil or floor
+// nwg/8), decomposed 1: split fastest -- a row tile's super-blocks on one XCD, so the 128-byte
+// lines two neighbouring super-blocks of a row share (144 / 210 / 272-byte rows are not
+// line-aligned) are fetched into one L2, not two; 2: row tile fastest -- one split's K range
+// on one XCD, so each XCD reads its slice of the activations instead of all of them.
+__device__ __forceinline__ TileId xcd_tile(int xpol)
+{
+    if (xpol == 0) return grid_tile();
+    const int gx = (int)gridDim.x, gy = (int)gridDim.y, gz = (int)gridDim.z, nwg = gx * gy * gz;
+    const int orig = (int)blockIdx.x + gx * ((int)blockIdx.y + gy * (int)blockIdx.z);
+    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    const int w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    if (xpol == 1) {
+        const int t = w / gz;
+        return TileId{t % gx, t / gx, w - t * gz, gx, gy, gz};
+    }
+    const int t = w / gx;
+    return TileId{w - t * gx, t % gy, t / gy, gx, gy, gz};
+}
 
 template <int NB>
 __device__ __forceinline__ void store_tile(const f32x4 (&acc)[RRG][NB], uint16_t *__restrict__ C,
@@ -241,13 +262,14 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[RRG][NB], uint16_t
 template <int F, int NB, int AQ>
 __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
                                                        int64_t ldx, uint16_t *__restrict__ C, uint16_t *__restrict__ P,
-                                                       int64_t M, int64_t N, int64_t K, int64_t ldc, int spol)
+                                                       int64_t M, int64_t N, int64_t K, int64_t ldc, int spol, int xpol)
 {
     using G = RCfg<F, NB>;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[G::LDS];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int64_t m0 = (int64_t)blockIdx.x * RBM, n0 = (int64_t)blockIdx.y * G::BN, sb = blockIdx.z;
+    const TileId tile = xcd_tile(xpol);
+    const int64_t m0 = (int64_t)tile.x * RBM, n0 = (int64_t)tile.y * G::BN, sb = tile.z;
     const int64_t row_bytes = (K / Layout<F>::QK) * Layout<F>::BYTES;
     uint8_t *const ximg = lds + G::X_OFF;
 
@@ -344,7 +366,7 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
         if (acc[0][0][0] == 1234.5f) C[0] = 0;
         return;
     }
-    store_tile<NB>(acc, C, P, M, N, ldc, spol, grid_tile());
+    store_tile<NB>(acc, C, P, M, N, ldc, spol, tile);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -478,11 +500,11 @@ __device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const 
 template <int F, int NB>
 __global__ __launch_bounds__(64 * RW) void sgemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
                                                        uint16_t *__restrict__ C, uint16_t *__restrict__ P, int64_t M,
-                                                       int64_t N, int64_t K, int64_t ldc, int spol)
+                                                       int64_t N, int64_t K, int64_t ldc, int spol, int xpol)
 {
     __shared__ __attribute__((aligned(1024))) uint8_t lds[SCfg<F, NB>::LDS];
     // split z: super-blocks [z*nsb/S, (z+1)*nsb/S) (split lengths differ by one when S does not divide)
-    const TileId id = grid_tile();
+    const TileId id = xcd_tile(xpol);
     const int64_t nsb = K / 256;
     sgemm_body<F, NB>(A, X, C, P, M, N, K, ldc, spol, id, id.z * nsb / id.gz, (id.z + 1) * nsb / id.gz, lds);
 }
@@ -619,7 +641,8 @@ hipError_t launch_snb(const uint8_t *A, const uint16_t *X, uint16_t *C, void *P,
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
     const dim3 grid((unsigned)p.tiles_m, (unsigned)p.tiles_n, (unsigned)p.splits);
-    sgemm_kernel<F, NB><<<grid, dim3(64 * RW), 0, s>>>(A, X, C, (uint16_t *)P, M, N, K, ldc, tuning().rgemm_spol);
+    sgemm_kernel<F, NB><<<grid, dim3(64 * RW), 0, s>>>(A, X, C, (uint16_t *)P, M, N, K, ldc, tuning().rgemm_spol,
+                                                        tuning().sgemm_xcd);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.splits == 1) return e;
     return launch_gemm_reduce_f16(NB, RRG, (const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n);
@@ -630,7 +653,8 @@ hipError_t launch_nb(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t 
                      int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
     const dim3 grid((unsigned)p.tiles_m, (unsigned)p.tiles_n, (unsigned)p.splits);
-    rgemm_kernel<F, NB, AQ><<<grid, dim3(64 * RW), 0, s>>>(A, X, ldx, C, (uint16_t *)P, M, N, K, ldc, tuning().rgemm_spol);
+    rgemm_kernel<F, NB, AQ><<<grid, dim3(64 * RW), 0, s>>>(A, X, ldx, C, (uint16_t *)P, M, N, K, ldc, tuning().rgemm_spol,
+                                                            tuning().rgemm_xcd);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.splits == 1) return e;
     return launch_gemm_reduce_f16(NB, RRG, (const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n);

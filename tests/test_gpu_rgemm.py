@@ -156,3 +156,32 @@ def test_sgemm_bit_identities(fmt, tune):
     tune(GQ_SGEMM=0, GQ_WGEMM=0, GQ_GEMM_SPLITS=1)
     C0 = _prepared(fmt, A_t, B_t, M, N, K)
     assert torch.equal(C0.view(torch.int16), C1.view(torch.int16))
+
+
+@pytest.mark.parametrize("fmt", FMTS)
+@pytest.mark.parametrize("M,N,K,route", [(11008, 16, 4096, "rgemm"), (300, 70, 2816, "rgemm"), (4096, 128, 11008, "sgemm"),
+                                         (777, 20, 3072, "sgemm"), (100, 5, 256, "rgemm")])
+def test_xcd_order_same_bits(fmt, M, N, K, route, tune):
+    """The XCD-aware workgroup orders (GQ_RGEMM_XCD / GQ_SGEMM_XCD = 1: a tile's splits on one XCD,
+    2: a split's row tiles) move work between XCDs only: every (tile, split) is computed once,
+    with the same partial slot and reduce order, so the bits equal blockIdx order's -- odd grid
+    sizes included (the remap's uneven blocks)."""
+    import kernels._lib as kl
+    qA = random_blocks(fmt, M, K, seed=M + K)
+    B = random_activations(N, K, seed=N + K)
+    A_t, B_t = _t(qA.view(np.int8)), _t(B)
+    knob = "GQ_RGEMM_XCD" if route == "rgemm" else "GQ_SGEMM_XCD"
+    pin = dict(GQ_RGEMM=1, GQ_SKINNY=0) if route == "rgemm" else dict(GQ_RGEMM=0, GQ_SKINNY=0, GQ_SGEMM=1)
+    outs = []
+    for pol in (0, 1, 2):
+        tune(**pin, **{knob: pol})
+        name = kl.route_name(kl.TYPES[fmt], M, N, K)
+        assert name.startswith(route + "_kernel"), name
+        outs.append(_mmq(fmt, A_t, B_t, M, N, K))
+    assert torch.equal(outs[1].view(torch.int16), outs[0].view(torch.int16))
+    assert torch.equal(outs[2].view(torch.int16), outs[0].view(torch.int16))
+    rows = np.sort(np.random.default_rng(M).choice(M, size=min(M, 16), replace=False))
+    rb = qA.size // M
+    sub = np.concatenate([qA[r * rb:(r + 1) * rb] for r in rows])
+    got = outs[1].cpu().numpy()[:, rows]
+    assert O.max_rel_err(got, O.mmq_from_fp16(fmt, sub, B, len(rows), N, K, O.IDEAL)) <= TIGHT
