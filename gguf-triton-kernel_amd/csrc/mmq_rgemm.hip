@@ -31,7 +31,8 @@ namespace gq {
 namespace {
 
 // diagnostic ablation builds only (make rabl RABL=n; never the product): 1 = no weight DMA,
-// 2 = no activation load, 4 = no multiply (fragments + MFMA), 8 = no epilogue stores
+// 2 = no activation load, 4 = no multiply (fragments + MFMA; the streaming kernels too),
+// 8 = no epilogue stores
 #ifndef GQ_RGEMM_ABL
 #define GQ_RGEMM_ABL 0
 #endif
@@ -387,7 +388,7 @@ template <int F, int NB> struct SCfg {
     static constexpr int SLOT = W_BYTES + X_BYTES;
     static constexpr int WH_INSTR = (RBM * NPH + 63) / 64, NWH = (WH_INSTR + RW - 1) / RW;
     static constexpr int XH_INSTR = X_BYTES / 1024, NXH = (XH_INSTR + RW - 1) / RW;
-    static constexpr int NPS = NWH + NXH; // DMA instructions per wave and stage
+    static constexpr int NPS = ((ABL & 1) ? 0 : NWH) + NXH; // DMA instructions per wave and stage
     static constexpr bool PAD = WH_INSTR % RW != 0 || XH_INSTR % RW != 0 || XH_INSTR < RW;
     static constexpr int NS = (LDS_CAP - 1024) / SLOT > SG_NSMAX ? SG_NSMAX : (LDS_CAP - 1024) / SLOT; // ring slots
     static constexpr int SCRATCH = NS * SLOT;
@@ -412,6 +413,7 @@ struct SParts {
     int64_t N;
     int spol;
     int streamk, U, W; // stream-K: U units over W workgroups, workgroup w = units [wU/W, (w+1)U/W)
+    int pair;          // GQ_SGEMM_PAIR (sgemm_body)
     SPart p[kMaxSParts];
 };
 struct RPart {
@@ -436,7 +438,7 @@ template <int F, int NB>
 __device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
                                            uint16_t *__restrict__ C, uint16_t *__restrict__ P, int64_t M, int64_t N,
                                            int64_t K, int64_t ldc, int spol, const TileId &id, int64_t sb0, int64_t sb1,
-                                           uint8_t *lds)
+                                           uint8_t *lds, int pair)
 {
     using G = SCfg<F, NB>;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -454,7 +456,7 @@ __device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const 
         const int64_t sb = sb0 + (j >> 1);
         const int h = j & 1;
 #pragma unroll
-        for (int i = 0; i < G::NWH; ++i) {
+        for (int i = 0; i < ((ABL & 1) ? 0 : G::NWH); ++i) {
             const int k = wave + RW * i, p = 64 * k + lane, r = p / G::NPH, pc = p - r * G::NPH;
             const bool real = k < G::WH_INSTR;
             const int64_t row = m0 + r < M ? m0 + r : M - 1;
@@ -478,17 +480,32 @@ __device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const 
     for (int rg = 0; rg < RRG; ++rg)
 #pragma unroll
         for (int t = 0; t < NB; ++t) acc[rg][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < G::NS - 1; ++i)
-        if (i < nst) issue(i);
+    // pair (GQ_SGEMM_PAIR, rings of 4+ slots; 2: 3+): a super-block's two half stages are issued
+    // together, so each row's bytes of the super-block are requested at once (one DRAM row
+    // activation, not two a step apart); stage s may be issued once s <= j + NS - 1 at step j
+    const bool pr = pair != 0 && G::NS >= (pair == 2 ? 3 : 4);
+    int issued = pr ? ((G::NS - 1) & ~1) : G::NS - 1;
+    issued = issued < nst ? issued : nst;
+    for (int i = 0; i < issued; ++i) issue(i);
     for (int j = 0; j < nst; ++j) {
         // stage j landed: all but the (<= NS-2) younger stages this wave issued
-        const int younger = G::NS - 2 < nst - 1 - j ? G::NS - 2 : nst - 1 - j;
+        const int younger = issued - 1 - j;
         vm_wait<(G::NS - 2) * G::NPS>(younger * G::NPS);
         __builtin_amdgcn_s_barrier();
-        if (j + G::NS - 1 < nst) issue(j + G::NS - 1); // into the slot stage j-1 left (barrier passed)
+        // into the slots the stages before j left (barrier passed)
+        if (pr) {
+            if (issued + 1 < nst && issued + 1 <= j + G::NS - 1) {
+                issue(issued);
+                issue(issued + 1);
+                issued += 2;
+            }
+        } else if (issued < nst) {
+            issue(issued);
+            ++issued;
+        }
         const uint8_t *slot = lds + (j % G::NS) * G::SLOT;
         const int h = j & 1;
+        if constexpr ((ABL & 4) != 0) continue; // (ablation builds: no multiply)
 #pragma unroll
         for (int ul = 0; ul < 2; ++ul)
             mul_substage<F, NB>(slot, slot + G::W_BYTES + ul * (G::BN * 128), 2 * h + ul, acc);
@@ -500,13 +517,13 @@ __device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const 
 template <int F, int NB>
 __global__ __launch_bounds__(64 * RW) void sgemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
                                                        uint16_t *__restrict__ C, uint16_t *__restrict__ P, int64_t M,
-                                                       int64_t N, int64_t K, int64_t ldc, int spol, int xpol)
+                                                       int64_t N, int64_t K, int64_t ldc, int spol, int xpol, int pair)
 {
     __shared__ __attribute__((aligned(1024))) uint8_t lds[SCfg<F, NB>::LDS];
     // split z: super-blocks [z*nsb/S, (z+1)*nsb/S) (split lengths differ by one when S does not divide)
     const TileId id = xcd_tile(xpol);
     const int64_t nsb = K / 256;
-    sgemm_body<F, NB>(A, X, C, P, M, N, K, ldc, spol, id, id.z * nsb / id.gz, (id.z + 1) * nsb / id.gz, lds);
+    sgemm_body<F, NB>(A, X, C, P, M, N, K, ldc, spol, id, id.z * nsb / id.gz, (id.z + 1) * nsb / id.gz, lds, pair);
 }
 
 // ---- several matrices in one launch (gq_mmq_grouped_prepared): part i = one matrix's
@@ -524,9 +541,9 @@ __global__ __launch_bounds__(64 * RW) void sgemm_grouped_kernel(const SParts a)
     const int b = (int)blockIdx.x;
     auto run = [&](const SPart &q, const TileId &id, int64_t sb0, int64_t sb1) __attribute__((always_inline)) {
         switch (q.fmt) {
-        case Q8_0: sgemm_body<Q8_0, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds); return;
-        case Q4_K: sgemm_body<Q4_K, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds); return;
-        default: sgemm_body<Q6_K, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds); return;
+        case Q8_0: sgemm_body<Q8_0, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds, a.pair); return;
+        case Q4_K: sgemm_body<Q4_K, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds, a.pair); return;
+        default: sgemm_body<Q6_K, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds, a.pair); return;
         }
     };
     if (!a.streamk) { // tile-granular splits: workgroup = (part, tile, split)
@@ -642,7 +659,7 @@ hipError_t launch_snb(const uint8_t *A, const uint16_t *X, uint16_t *C, void *P,
 {
     const dim3 grid((unsigned)p.tiles_m, (unsigned)p.tiles_n, (unsigned)p.splits);
     sgemm_kernel<F, NB><<<grid, dim3(64 * RW), 0, s>>>(A, X, C, (uint16_t *)P, M, N, K, ldc, tuning().rgemm_spol,
-                                                        tuning().sgemm_xcd);
+                                                        tuning().sgemm_xcd, tuning().sgemm_pair);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.splits == 1) return e;
     return launch_gemm_reduce_f16(NB, RRG, (const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n);
@@ -831,6 +848,7 @@ hipError_t launch_sgemm_grouped(const SGroupItem *items, int n, int64_t N, const
     a.n = n;
     a.N = N;
     a.spol = tuning().rgemm_spol;
+    a.pair = tuning().sgemm_pair;
     a.streamk = r.streamk = g.streamk ? 1 : 0;
     a.U = r.U = g.U;
     a.W = r.W = g.blocks;
