@@ -49,6 +49,8 @@ struct Tuning {
     int rgemm_xcd = 0;                        // GQ_RGEMM_XCD: workgroup -> tile order per XCD (mmq_rgemm.hip xcd_tile):
                                               // 0 blockIdx as is, 1 a tile's splits consecutive, 2 a split's row tiles
     int sgemm_xcd = 0;                        // GQ_SGEMM_XCD: the same for the (single-matrix) streaming GEMM
+    int sgemm_full = -1;                      // GQ_SGEMM_FULL: Q4_K 16/32-token tiles stream whole super-blocks:
+                                              // 1 every streaming GEMM, 0 none, -1 single matrices (measured gain)
     int sgemm_pair = 0;                       // GQ_SGEMM_PAIR: issue a super-block's two half stages together
                                               // (1: rings of 4+ slots, 2: 3+; mmq_rgemm.hip sgemm_body)
     int cus = 0;                              // GQ_CUS: compute units to plan for (0: the device's count)

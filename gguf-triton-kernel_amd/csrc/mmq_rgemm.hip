@@ -414,6 +414,7 @@ struct SParts {
     int spol;
     int streamk, U, W; // stream-K: U units over W workgroups, workgroup w = units [wU/W, (w+1)U/W)
     int pair;          // GQ_SGEMM_PAIR (sgemm_body)
+    int full;          // GQ_SGEMM_FULL (Q4_K, NB <= 2: sgemm_full_body)
     SPart p[kMaxSParts];
 };
 struct RPart {
@@ -514,23 +515,133 @@ __device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const 
     store_tile<NB>(acc, C, P, M, N, ldc, spol, id);
 }
 
+// Q4_K with whole-super-block stages (GQ_SGEMM_FULL; 16 / 32-token tiles; the default for single
+// matrices: 11008x4096x16 17.1 vs 22.3 us, 4096x11008x16 15.9 vs 20.0; the grouped layer no
+// different, 65.6 vs 65.7 at 8 tokens: profiles/r04/ab15_full_*.txt): a stage is the rows'
+// super-block as one 144-byte image per row (gemm_kernel's WStage<Q4_K> layout: the header once,
+// each row's bytes one contiguous run, 36 DMA instructions of ~7 rows each instead of 2 x 20 of
+// ~13 rows x 80 bytes) and the super-block's four x~ sub-stages.  Same fragments, same MFMA
+// sequence as the half stages (q4k_frags on the same bytes): the same bits.
+template <int NB> struct SFull {
+    static constexpr int BN = 16 * NB, NPW = 9, RBW = 16 * NPW;
+    static constexpr int W_BYTES = RBM * RBW, X_BYTES = BN * 512, SLOT = W_BYTES + X_BYTES;
+    static constexpr int W_INSTR = RBM * NPW / 64, NW = (W_INSTR + RW - 1) / RW;
+    static constexpr int X_INSTR = X_BYTES / 1024, NX = (X_INSTR + RW - 1) / RW;
+    static constexpr int NPS = NW + NX;
+    static constexpr int NS = (LDS_CAP - 1024) / SLOT > SG_NSMAX ? SG_NSMAX : (LDS_CAP - 1024) / SLOT;
+    static constexpr int SCRATCH = NS * SLOT, LDS = SCRATCH + 1024;
+    static_assert(RBM * NPW % 64 == 0 && NS >= 2 && LDS <= LDS_CAP && (NS - 2) * NPS <= 63, "SFull");
+};
+
+template <int NB>
+__device__ __forceinline__ void sgemm_full_body(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
+                                                uint16_t *__restrict__ C, uint16_t *__restrict__ P, int64_t M, int64_t N,
+                                                int64_t K, int64_t ldc, int spol, const TileId &id, int64_t sb0, int64_t sb1,
+                                                uint8_t *lds)
+{
+    using G = SFull<NB>;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, l16 = lane & 15;
+    const int64_t m0 = (int64_t)id.x * RBM, n0 = (int64_t)id.y * G::BN;
+    const int64_t row_bytes = (K / 256) * 144;
+    const int nst = (int)(sb1 - sb0);
+    const __amdgpu_buffer_rsrc_t wrs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, (int)(uint32_t)((M * row_bytes + 15) & ~(int64_t)15), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, (int)(uint32_t)(N * K * 2), 0x00020000);
+    auto issue = [&](int j) __attribute__((always_inline)) {
+        uint8_t *slot = lds + (j % G::NS) * G::SLOT;
+        const int64_t sb = sb0 + j;
+#pragma unroll
+        for (int i = 0; i < ((ABL & 1) ? 0 : G::NW); ++i) {
+            const int k = wave + RW * i, p = 64 * k + lane, r = p / G::NPW, pc = p - r * G::NPW;
+            const bool real = k < G::W_INSTR;
+            const int64_t row = m0 + r < M ? m0 + r : M - 1;
+            const uint32_t vo = real ? (uint32_t)(row * row_bytes) + 16u * pc : 0u;
+            dma16(wrs, real ? slot + 1024 * k : lds + G::SCRATCH, vo, (uint32_t)(144 * sb));
+        }
+#pragma unroll
+        for (int i = 0; i < G::NX; ++i) {
+            const int k = wave + RW * i, pp = 64 * k + lane;
+            const bool real = k < G::X_INSTR;
+            const int u = pp / (G::BN * 8), r = (pp / 8) % G::BN, qd = pp & 7, q = qd ^ act_swz(r);
+            const int64_t tok = n0 + r < N ? n0 + r : N - 1;
+            const uint32_t vo = real ? (uint32_t)(tok * K * 2) + 2u * (uint32_t)sub_elem<Q4_K>(u, q) : 0u;
+            dma16(xrs, real ? slot + G::W_BYTES + 1024 * k : lds + G::SCRATCH, vo, (uint32_t)(512 * sb));
+        }
+    };
+    f32x4 acc[RRG][NB];
+#pragma unroll
+    for (int rg = 0; rg < RRG; ++rg)
+#pragma unroll
+        for (int t = 0; t < NB; ++t) acc[rg][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    int issued = G::NS - 1 < nst ? G::NS - 1 : nst;
+    for (int i = 0; i < issued; ++i) issue(i);
+    for (int j = 0; j < nst; ++j) {
+        vm_wait<(G::NS - 2) * G::NPS>((issued - 1 - j) * G::NPS);
+        __builtin_amdgcn_s_barrier();
+        if (issued < nst) issue(issued++);
+        const uint8_t *slot = lds + (j % G::NS) * G::SLOT;
+        if constexpr ((ABL & 4) != 0) continue;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint8_t *xs = slot + G::W_BYTES + u * (G::BN * 128);
+            f16x8 af[RRG][2];
+#pragma unroll
+            for (int rg = 0; rg < RRG; ++rg) {
+                const uint8_t *wr = slot + G::RBW * (16 * (RRG * wave + rg) + l16);
+                q4k_frags(wr, wr + 16 + 32 * u, g, u, af[rg]);
+            }
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                f16x8 bk[NB];
+#pragma unroll
+                for (int t = 0; t < NB; ++t) {
+                    const int r = 16 * t + l16;
+                    bk[t] = *(const f16x8 *)(xs + 128 * r + 16 * ((4 * s + g) ^ act_swz(r)));
+                }
+#pragma unroll
+                for (int rg = 0; rg < RRG; ++rg)
+#pragma unroll
+                    for (int t = 0; t < NB; ++t)
+                        acc[rg][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[rg][s], bk[t], acc[rg][t], 0, 0, 0);
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    store_tile<NB>(acc, C, P, M, N, ldc, spol, id);
+}
+
+template <int F, int NB> constexpr int sgemm_lds()
+{
+    if constexpr (F == Q4_K && NB <= 2) return SCfg<F, NB>::LDS > SFull<NB>::LDS ? SCfg<F, NB>::LDS : SFull<NB>::LDS;
+    return SCfg<F, NB>::LDS;
+}
+
 template <int F, int NB>
 __global__ __launch_bounds__(64 * RW) void sgemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
                                                        uint16_t *__restrict__ C, uint16_t *__restrict__ P, int64_t M,
-                                                       int64_t N, int64_t K, int64_t ldc, int spol, int xpol, int pair)
+                                                       int64_t N, int64_t K, int64_t ldc, int spol, int xpol, int pair,
+                                                       int full)
 {
-    __shared__ __attribute__((aligned(1024))) uint8_t lds[SCfg<F, NB>::LDS];
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[sgemm_lds<F, NB>()];
     // split z: super-blocks [z*nsb/S, (z+1)*nsb/S) (split lengths differ by one when S does not divide)
     const TileId id = xcd_tile(xpol);
-    const int64_t nsb = K / 256;
-    sgemm_body<F, NB>(A, X, C, P, M, N, K, ldc, spol, id, id.z * nsb / id.gz, (id.z + 1) * nsb / id.gz, lds, pair);
+    const int64_t nsb = K / 256, s0 = id.z * nsb / id.gz, s1 = (id.z + 1) * nsb / id.gz;
+    if constexpr (F == Q4_K && NB <= 2) {
+        if (full) {
+            sgemm_full_body<NB>(A, X, C, P, M, N, K, ldc, spol, id, s0, s1, lds);
+            return;
+        }
+    }
+    sgemm_body<F, NB>(A, X, C, P, M, N, K, ldc, spol, id, s0, s1, lds, pair);
 }
 
 // ---- several matrices in one launch (gq_mmq_grouped_prepared): part i = one matrix's
 // (row tile, token tile, split) grid, its workgroups [wg0, wg0 + tiles_m * tiles_n * splits)
 template <int NB> constexpr int max_slds()
 {
-    constexpr int a = SCfg<Q8_0, NB>::LDS, b = SCfg<Q4_K, NB>::LDS, c = SCfg<Q6_K, NB>::LDS;
+    constexpr int a = SCfg<Q8_0, NB>::LDS, b = sgemm_lds<Q4_K, NB>(), c = SCfg<Q6_K, NB>::LDS;
     return a > b ? (a > c ? a : c) : (b > c ? b : c);
 }
 
@@ -542,7 +653,15 @@ __global__ __launch_bounds__(64 * RW) void sgemm_grouped_kernel(const SParts a)
     auto run = [&](const SPart &q, const TileId &id, int64_t sb0, int64_t sb1) __attribute__((always_inline)) {
         switch (q.fmt) {
         case Q8_0: sgemm_body<Q8_0, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds, a.pair); return;
-        case Q4_K: sgemm_body<Q4_K, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds, a.pair); return;
+        case Q4_K:
+            if constexpr (NB <= 2) {
+                if (a.full) {
+                    sgemm_full_body<NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds);
+                    return;
+                }
+            }
+            sgemm_body<Q4_K, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds, a.pair);
+            return;
         default: sgemm_body<Q6_K, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds, a.pair); return;
         }
     };
@@ -659,7 +778,7 @@ hipError_t launch_snb(const uint8_t *A, const uint16_t *X, uint16_t *C, void *P,
 {
     const dim3 grid((unsigned)p.tiles_m, (unsigned)p.tiles_n, (unsigned)p.splits);
     sgemm_kernel<F, NB><<<grid, dim3(64 * RW), 0, s>>>(A, X, C, (uint16_t *)P, M, N, K, ldc, tuning().rgemm_spol,
-                                                        tuning().sgemm_xcd, tuning().sgemm_pair);
+                                                        tuning().sgemm_xcd, tuning().sgemm_pair, tuning().sgemm_full != 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.splits == 1) return e;
     return launch_gemm_reduce_f16(NB, RRG, (const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n);
@@ -849,6 +968,7 @@ hipError_t launch_sgemm_grouped(const SGroupItem *items, int n, int64_t N, const
     a.N = N;
     a.spol = tuning().rgemm_spol;
     a.pair = tuning().sgemm_pair;
+    a.full = tuning().sgemm_full > 0;
     a.streamk = r.streamk = g.streamk ? 1 : 0;
     a.U = r.U = g.U;
     a.W = r.W = g.blocks;

@@ -247,28 +247,30 @@ def test_single_matrix_stream_k(fmt, M, K, N, tune):
     assert O.max_rel_err(C[:, rows], O.mmq_from_fp16(fmt, sub, B, len(rows), N, K, O.IDEAL)) <= TIGHT
 
 
-@pytest.mark.parametrize("N", [8, 40, 128])
-@pytest.mark.parametrize("pair", [1, 2])
-def test_paired_stage_issue_same_bits(N, pair, tune):
-    """GQ_SGEMM_PAIR (a super-block's two half stages issued together) changes when bytes are
-    requested, not what is computed: the grouped layer and a single streaming-GEMM call give the
-    bits of the one-stage-at-a-time schedule."""
+@pytest.mark.parametrize("N", [8, 20, 40, 128])
+@pytest.mark.parametrize("knob,pair", [("GQ_SGEMM_PAIR", 1), ("GQ_SGEMM_PAIR", 2), ("GQ_SGEMM_FULL", 1)])
+def test_stage_schedule_same_bits(N, knob, pair, tune):
+    """GQ_SGEMM_PAIR (a super-block's two half stages issued together) and GQ_SGEMM_FULL (Q4_K
+    16/32-token tiles streaming whole super-blocks as one 144-byte image per row) change when and
+    how bytes are requested, not what is computed: the grouped layer and a single streaming-GEMM
+    call give the bits of the one-half-stage-at-a-time schedule."""
     import kernels._lib as kl
     types, raw, x, h, items, names, inputs = _layer_items(kl, N, layer=0, seed=N + pair)
     ref = kl.mmq_grouped_prepared(items, N)
     assert ref is not None, kl.lib().gq_last_error()
     torch.cuda.synchronize()
     ref = [r.clone() for r in ref]
-    tune(GQ_SGEMM_PAIR=pair)
+    tune(**{knob: pair})
     got = kl.mmq_grouped_prepared(items, N)
     torch.cuda.synchronize()
     for n, a, b in zip(names, ref, got):
         assert torch.equal(a.view(torch.int16), b.view(torch.int16)), n
-    t, A, _, M, K, _ = items[names.index("ffn_down")]
-    B = inputs[names.index("ffn_down")]
+    one = "ffn_down" if knob == "GQ_SGEMM_PAIR" else "ffn_up"  # (a Q6_K / a Q4_K projection)
+    t, A, _, M, K, _ = items[names.index(one)]
+    B = inputs[names.index(one)]
     outs = []
     for p in (0, pair):
-        tune(GQ_RGEMM=0, GQ_SKINNY=0, GQ_SGEMM=1, GQ_SGEMM_PAIR=p)
+        tune(GQ_RGEMM=0, GQ_SKINNY=0, GQ_SGEMM=1, **{knob: p})
         ws = torch.empty(kl.workspace_size(t, M, N, K), dtype=torch.uint8, device=_dev())
         kl.act_prepare(B, N, K, ws)
         outs.append(kl.mmq_prepared(t, A, ws, M, N, K))
