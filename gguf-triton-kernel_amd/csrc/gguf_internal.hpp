@@ -51,6 +51,7 @@ struct Tuning {
     int sgemm_xcd = 0;                        // GQ_SGEMM_XCD: the same for the (single-matrix) streaming GEMM
     int sgemm_full = -1;                      // GQ_SGEMM_FULL: Q4_K 16/32-token tiles stream whole super-blocks:
                                               // 1 every streaming GEMM, 0 none, -1 single matrices (measured gain)
+    int sgemm_wring = 0;                      // GQ_SGEMM_WRING: Q4_K 16-token tiles on per-wave weight rings
     int sgemm_pair = 0;                       // GQ_SGEMM_PAIR: issue a super-block's two half stages together
                                               // (1: rings of 4+ slots, 2: 3+; mmq_rgemm.hip sgemm_body)
     int cus = 0;                              // GQ_CUS: compute units to plan for (0: the device's count)

@@ -414,7 +414,7 @@ struct SParts {
     int spol;
     int streamk, U, W; // stream-K: U units over W workgroups, workgroup w = units [wU/W, (w+1)U/W)
     int pair;          // GQ_SGEMM_PAIR (sgemm_body)
-    int full;          // GQ_SGEMM_FULL (Q4_K, NB <= 2: sgemm_full_body)
+    int full;          // bit 0: GQ_SGEMM_FULL (Q4_K, NB <= 2: sgemm_full_body); bit 1: GQ_SGEMM_WRING (NB 1)
     SPart p[kMaxSParts];
 };
 struct RPart {
@@ -612,9 +612,104 @@ __device__ __forceinline__ void sgemm_full_body(const uint8_t *__restrict__ A, c
     store_tile<NB>(acc, C, P, M, N, ldc, spol, id);
 }
 
+// Q4_K at 16-token tiles with per-wave weight rings (GQ_SGEMM_WRING): the decode kernel's
+// structure with the MFMA multiply.  Each wave streams its own 32 rows' super-blocks (one 144-byte
+// image per row, 4.6 KB per super-block) through a private ring of WR_NS slots and waits only on
+// its own DMA counter -- no workgroup barrier per stage; the x~ of up to WR_XC super-blocks is
+// resident in LDS, reloaded (one barrier) per chunk.  Same fragments and MFMA order per
+// super-block as sgemm_body: the same bits.
+constexpr int WR_NS = 3, WR_XC = 4, WR_SLOT = 5120; // (32 rows x 144 B = 4608, the DMA pad to 5 KiB)
+struct WRing {
+    static constexpr int X_BYTES = WR_XC * 16 * 512, W_OFF = X_BYTES;
+    static constexpr int LDS = X_BYTES + RW * WR_NS * WR_SLOT;
+    static_assert(LDS <= LDS_CAP && (WR_NS - 1) * 5 <= 63, "WRing");
+};
+
+__device__ __forceinline__ void wring_body(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
+                                           uint16_t *__restrict__ C, uint16_t *__restrict__ P, int64_t M, int64_t N,
+                                           int64_t K, int64_t ldc, int spol, const TileId &id, int64_t sb0, int64_t sb1,
+                                           uint8_t *lds)
+{
+    constexpr int BN = 16;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, l16 = lane & 15;
+    const int64_t m0 = (int64_t)id.x * RBM, n0 = (int64_t)id.y * BN;
+    const int64_t row_bytes = (K / 256) * 144;
+    const int nst = (int)(sb1 - sb0);
+    const __amdgpu_buffer_rsrc_t wrs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, (int)(uint32_t)((M * row_bytes + 15) & ~(int64_t)15), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, (int)(uint32_t)(N * K * 2), 0x00020000);
+    uint8_t *const ring = lds + WRing::W_OFF + wave * (WR_NS * WR_SLOT);
+    // this wave's 32 rows of super-block j: piece p = 64k + lane -> row p / 9, piece p % 9
+    auto issue_w = [&](int j) __attribute__((always_inline)) {
+        uint8_t *slot = ring + (j % WR_NS) * WR_SLOT;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const int p = 64 * k + lane, r = p / 9, pc = p - 9 * r;
+            const bool real = p < 32 * 9;
+            const int64_t row = m0 + 32 * wave + r < M ? m0 + 32 * wave + r : M - 1;
+            const uint32_t vo = real ? (uint32_t)(row * row_bytes) + 16u * pc : 0u;
+            dma16(wrs, slot + 1024 * k, vo, (uint32_t)(144 * (sb0 + j))); // (pad lanes: the slot's last 512 B)
+        }
+    };
+    // the x~ of super-blocks [c0, c0 + cn): 8 KiB each, 8 DMA instructions, one per wave
+    auto issue_x = [&](int c0, int cn) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < WR_XC; ++i) {
+            if (i >= cn) break;
+            const int pp = 64 * wave + lane; // piece of the super-block's 8 KiB image
+            const int u = pp / (BN * 8), r = (pp / 8) % BN, qd = pp & 7, q = qd ^ act_swz(r);
+            const int64_t tok = n0 + r < N ? n0 + r : N - 1;
+            const uint32_t vo = (uint32_t)(tok * K * 2) + 2u * (uint32_t)sub_elem<Q4_K>(u, q);
+            dma16(xrs, lds + i * (BN * 512) + 1024 * wave, vo, (uint32_t)(512 * (sb0 + c0 + i)));
+        }
+    };
+    f32x4 acc[RRG][1];
+#pragma unroll
+    for (int rg = 0; rg < RRG; ++rg) acc[rg][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    int issued = 0;
+    for (int c0 = 0; c0 < nst; c0 += WR_XC) {
+        const int cn = nst - c0 < WR_XC ? nst - c0 : WR_XC;
+        if (c0 > 0) __builtin_amdgcn_s_barrier(); // every wave is done with the previous chunk's x~
+        issue_x(c0, cn);
+        while (issued < nst && issued < c0 + WR_NS - 1) issue_w(issued++); // (the first chunk's prologue)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier(); // the chunk's x~ landed for every wave
+        for (int j = c0; j < c0 + cn; ++j) {
+            vm_wait<(WR_NS - 2) * 5>((issued - 1 - j) * 5); // super-block j of this wave landed
+            if (issued < nst) issue_w(issued++);             // into the slot super-block j-1 left
+            const uint8_t *slot = ring + (j % WR_NS) * WR_SLOT;
+            if constexpr ((ABL & 4) != 0) continue;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint8_t *xs = lds + (j - c0) * (BN * 512) + u * (BN * 128);
+                f16x8 af[RRG][2];
+#pragma unroll
+                for (int rg = 0; rg < RRG; ++rg) {
+                    const uint8_t *wr = slot + 144 * (16 * rg + l16);
+                    q4k_frags(wr, wr + 16 + 32 * u, g, u, af[rg]);
+                }
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const f16x8 bk = *(const f16x8 *)(xs + 128 * l16 + 16 * ((4 * s + g) ^ act_swz(l16)));
+#pragma unroll
+                    for (int rg = 0; rg < RRG; ++rg)
+                        acc[rg][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[rg][s], bk, acc[rg][0], 0, 0, 0);
+                }
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    store_tile<1>(acc, C, P, M, N, ldc, spol, id);
+}
+
 template <int F, int NB> constexpr int sgemm_lds()
 {
-    if constexpr (F == Q4_K && NB <= 2) return SCfg<F, NB>::LDS > SFull<NB>::LDS ? SCfg<F, NB>::LDS : SFull<NB>::LDS;
+    if constexpr (F == Q4_K && NB <= 2) {
+        constexpr int a = SCfg<F, NB>::LDS > SFull<NB>::LDS ? SCfg<F, NB>::LDS : SFull<NB>::LDS;
+        return NB == 1 && WRing::LDS > a ? WRing::LDS : a;
+    }
     return SCfg<F, NB>::LDS;
 }
 
@@ -629,7 +724,11 @@ __global__ __launch_bounds__(64 * RW) void sgemm_kernel(const uint8_t *__restric
     const TileId id = xcd_tile(xpol);
     const int64_t nsb = K / 256, s0 = id.z * nsb / id.gz, s1 = (id.z + 1) * nsb / id.gz;
     if constexpr (F == Q4_K && NB <= 2) {
-        if (full) {
+        if (NB == 1 && (full & 2)) {
+            wring_body(A, X, C, P, M, N, K, ldc, spol, id, s0, s1, lds);
+            return;
+        }
+        if (full & 1) {
             sgemm_full_body<NB>(A, X, C, P, M, N, K, ldc, spol, id, s0, s1, lds);
             return;
         }
@@ -654,8 +753,14 @@ __global__ __launch_bounds__(64 * RW) void sgemm_grouped_kernel(const SParts a)
         switch (q.fmt) {
         case Q8_0: sgemm_body<Q8_0, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds, a.pair); return;
         case Q4_K:
+            if constexpr (NB == 1) {
+                if (a.full & 2) {
+                    wring_body(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds);
+                    return;
+                }
+            }
             if constexpr (NB <= 2) {
-                if (a.full) {
+                if (a.full & 1) {
                     sgemm_full_body<NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds);
                     return;
                 }
@@ -778,7 +883,8 @@ hipError_t launch_snb(const uint8_t *A, const uint16_t *X, uint16_t *C, void *P,
 {
     const dim3 grid((unsigned)p.tiles_m, (unsigned)p.tiles_n, (unsigned)p.splits);
     sgemm_kernel<F, NB><<<grid, dim3(64 * RW), 0, s>>>(A, X, C, (uint16_t *)P, M, N, K, ldc, tuning().rgemm_spol,
-                                                        tuning().sgemm_xcd, tuning().sgemm_pair, tuning().sgemm_full != 0);
+                                                        tuning().sgemm_xcd, tuning().sgemm_pair,
+                                                        (tuning().sgemm_full != 0) | (tuning().sgemm_wring ? 2 : 0));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.splits == 1) return e;
     return launch_gemm_reduce_f16(NB, RRG, (const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n);
@@ -968,7 +1074,7 @@ hipError_t launch_sgemm_grouped(const SGroupItem *items, int n, int64_t N, const
     a.N = N;
     a.spol = tuning().rgemm_spol;
     a.pair = tuning().sgemm_pair;
-    a.full = tuning().sgemm_full > 0;
+    a.full = (tuning().sgemm_full > 0) | (tuning().sgemm_wring ? 2 : 0);
     a.streamk = r.streamk = g.streamk ? 1 : 0;
     a.U = r.U = g.U;
     a.W = r.W = g.blocks;

@@ -248,7 +248,8 @@ def test_single_matrix_stream_k(fmt, M, K, N, tune):
 
 
 @pytest.mark.parametrize("N", [8, 20, 40, 128])
-@pytest.mark.parametrize("knob,pair", [("GQ_SGEMM_PAIR", 1), ("GQ_SGEMM_PAIR", 2), ("GQ_SGEMM_FULL", 1)])
+@pytest.mark.parametrize("knob,pair", [("GQ_SGEMM_PAIR", 1), ("GQ_SGEMM_PAIR", 2), ("GQ_SGEMM_FULL", 1),
+                                       ("GQ_SGEMM_WRING", 1)])
 def test_stage_schedule_same_bits(N, knob, pair, tune):
     """GQ_SGEMM_PAIR (a super-block's two half stages issued together) and GQ_SGEMM_FULL (Q4_K
     16/32-token tiles streaming whole super-blocks as one 144-byte image per row) change when and
