@@ -52,6 +52,7 @@ struct Tuning {
     int sgemm_full = -1;                      // GQ_SGEMM_FULL: Q4_K 16/32-token tiles stream whole super-blocks:
                                               // 1 every streaming GEMM, 0 none, -1 single matrices (measured gain)
     int sgemm_wring = 0;                      // GQ_SGEMM_WRING: Q4_K 16-token tiles on per-wave weight rings
+    int sgemm_nt = 0;                         // GQ_SGEMM_NT: the streaming GEMM's weight DMAs non-temporal
     int sgemm_pair = 0;                       // GQ_SGEMM_PAIR: issue a super-block's two half stages together
                                               // (1: rings of 4+ slots, 2: 3+; mmq_rgemm.hip sgemm_body)
     int cus = 0;                              // GQ_CUS: compute units to plan for (0: the device's count)

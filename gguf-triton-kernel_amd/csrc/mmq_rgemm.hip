@@ -462,7 +462,10 @@ __device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const 
             const bool real = k < G::WH_INSTR;
             const int64_t row = m0 + r < M ? m0 + r : M - 1;
             const uint32_t vo = real ? (uint32_t)(row * row_bytes) + hsrc<F>(h, pc) : 0u;
-            dma16(wrs, real ? slot + 1024 * k : lds + G::SCRATCH, vo, (uint32_t)(G::SB * sb)); // (+16 lane)
+            if (pair & 4) // (GQ_SGEMM_NT: the weights non-temporal, as the decode kernel's)
+                dma16<2>(wrs, real ? slot + 1024 * k : lds + G::SCRATCH, vo, (uint32_t)(G::SB * sb));
+            else
+                dma16(wrs, real ? slot + 1024 * k : lds + G::SCRATCH, vo, (uint32_t)(G::SB * sb)); // (+16 lane)
         }
         // activation half image: piece P = 64k + lane: sub-stage ul = P / (BN*8), token r, slot qd
 #pragma unroll
@@ -484,7 +487,8 @@ __device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const 
     // pair (GQ_SGEMM_PAIR, rings of 4+ slots; 2: 3+): a super-block's two half stages are issued
     // together, so each row's bytes of the super-block are requested at once (one DRAM row
     // activation, not two a step apart); stage s may be issued once s <= j + NS - 1 at step j
-    const bool pr = pair != 0 && G::NS >= (pair == 2 ? 3 : 4);
+    const int pm = pair & 3;
+    const bool pr = pm != 0 && G::NS >= (pm == 2 ? 3 : 4);
     int issued = pr ? ((G::NS - 1) & ~1) : G::NS - 1;
     issued = issued < nst ? issued : nst;
     for (int i = 0; i < issued; ++i) issue(i);
@@ -883,7 +887,7 @@ hipError_t launch_snb(const uint8_t *A, const uint16_t *X, uint16_t *C, void *P,
 {
     const dim3 grid((unsigned)p.tiles_m, (unsigned)p.tiles_n, (unsigned)p.splits);
     sgemm_kernel<F, NB><<<grid, dim3(64 * RW), 0, s>>>(A, X, C, (uint16_t *)P, M, N, K, ldc, tuning().rgemm_spol,
-                                                        tuning().sgemm_xcd, tuning().sgemm_pair,
+                                                        tuning().sgemm_xcd, tuning().sgemm_pair | (tuning().sgemm_nt ? 4 : 0),
                                                         (tuning().sgemm_full != 0) | (tuning().sgemm_wring ? 2 : 0));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.splits == 1) return e;
@@ -1073,7 +1077,7 @@ hipError_t launch_sgemm_grouped(const SGroupItem *items, int n, int64_t N, const
     a.n = n;
     a.N = N;
     a.spol = tuning().rgemm_spol;
-    a.pair = tuning().sgemm_pair;
+    a.pair = tuning().sgemm_pair | (tuning().sgemm_nt ? 4 : 0);
     a.full = (tuning().sgemm_full > 0) | (tuning().sgemm_wring ? 2 : 0);
     a.streamk = r.streamk = g.streamk ? 1 : 0;
     a.U = r.U = g.U;
