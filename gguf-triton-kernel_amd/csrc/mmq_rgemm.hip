@@ -32,7 +32,8 @@ namespace {
 
 // diagnostic ablation builds only (make rabl RABL=n; never the product): 1 = no weight DMA,
 // 2 = no activation load, 4 = no multiply (fragments + MFMA; the streaming kernels too),
-// 8 = no epilogue stores
+// 8 = no epilogue stores, 16 = the streaming kernel's weight stages read as contiguous runs of
+// the tile's rows (same bytes per stage, wrong values: the access pattern's cost alone)
 #ifndef GQ_RGEMM_ABL
 #define GQ_RGEMM_ABL 0
 #endif
@@ -461,11 +462,17 @@ __device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const 
             const int k = wave + RW * i, p = 64 * k + lane, r = p / G::NPH, pc = p - r * G::NPH;
             const bool real = k < G::WH_INSTR;
             const int64_t row = m0 + r < M ? m0 + r : M - 1;
-            const uint32_t vo = real ? (uint32_t)(row * row_bytes) + hsrc<F>(h, pc) : 0u;
+            uint32_t vo = real ? (uint32_t)(row * row_bytes) + hsrc<F>(h, pc) : 0u, soff = (uint32_t)(G::SB * sb);
+            if constexpr ((ABL & 16) != 0) { // (ablation: the same bytes per stage, read as one contiguous run)
+                const int64_t span = (M - m0 < RBM ? M - m0 : RBM) * row_bytes - G::W_BYTES - 16;
+                const int64_t off = ((2 * sb + h) * (int64_t)G::W_BYTES) % (span > 16 ? span : 16);
+                vo = (uint32_t)(m0 * row_bytes + ((off + 16 * (int64_t)p) & ~(int64_t)15));
+                soff = 0;
+            }
             if (pair & 4) // (GQ_SGEMM_NT: the weights non-temporal, as the decode kernel's)
-                dma16<2>(wrs, real ? slot + 1024 * k : lds + G::SCRATCH, vo, (uint32_t)(G::SB * sb));
+                dma16<2>(wrs, real ? slot + 1024 * k : lds + G::SCRATCH, vo, soff);
             else
-                dma16(wrs, real ? slot + 1024 * k : lds + G::SCRATCH, vo, (uint32_t)(G::SB * sb)); // (+16 lane)
+                dma16(wrs, real ? slot + 1024 * k : lds + G::SCRATCH, vo, soff); // (+16 lane)
         }
         // activation half image: piece P = 64k + lane: sub-stage ul = P / (BN*8), token r, slot qd
 #pragma unroll
