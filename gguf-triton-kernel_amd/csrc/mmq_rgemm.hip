@@ -464,9 +464,17 @@ __device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const 
             const int64_t row = m0 + r < M ? m0 + r : M - 1;
             uint32_t vo = real ? (uint32_t)(row * row_bytes) + hsrc<F>(h, pc) : 0u, soff = (uint32_t)(G::SB * sb);
             if constexpr ((ABL & 16) != 0) { // (ablation: the same bytes per stage, read as one contiguous run)
+#ifdef GQ_ABL_RUN // (... or as runs of GQ_ABL_RUN bytes from consecutive rows of the tile)
+                constexpr int64_t RUN = GQ_ABL_RUN;
+                const int64_t byte = 16 * (int64_t)p, c = byte / RUN, o = byte - c * RUN;
+                const int64_t rows_here = M - m0 < RBM ? M - m0 : RBM;
+                const int64_t col = (((2 * sb + h) * RUN) % (row_bytes - RUN + 16)) & ~(int64_t)15;
+                vo = (uint32_t)((m0 + c % rows_here) * row_bytes + col + o);
+#else
                 const int64_t span = (M - m0 < RBM ? M - m0 : RBM) * row_bytes - G::W_BYTES - 16;
                 const int64_t off = ((2 * sb + h) * (int64_t)G::W_BYTES) % (span > 16 ? span : 16);
                 vo = (uint32_t)(m0 * row_bytes + ((off + 16 * (int64_t)p) & ~(int64_t)15));
+#endif
                 soff = 0;
             }
             if (pair & 4) // (GQ_SGEMM_NT: the weights non-temporal, as the decode kernel's)
