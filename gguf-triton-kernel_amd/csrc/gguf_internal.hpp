@@ -51,6 +51,7 @@ struct Tuning {
     int sgemm_xcd = 0;                        // GQ_SGEMM_XCD: the same for the (single-matrix) streaming GEMM
     int sgemm_full = -1;                      // GQ_SGEMM_FULL: Q4_K 16/32-token tiles stream whole super-blocks:
                                               // 1 every streaming GEMM, 0 none, -1 single matrices (measured gain)
+    int rstream = 0;                          // GQ_RSTREAM: Q4_K 1..16-token GEMMs on the row-stream kernel
     int sgemm_wring = 0;                      // GQ_SGEMM_WRING: Q4_K 16-token tiles on per-wave weight rings
     int sgemm_nt = 0;                         // GQ_SGEMM_NT: the streaming GEMM's weight DMAs non-temporal
     int sgemm_pair = 0;                       // GQ_SGEMM_PAIR: issue a super-block's two half stages together
@@ -162,6 +163,10 @@ int iskinny_rg(int64_t M);
 hipError_t launch_iskinny(int fmt, const uint8_t *A, const int8_t *Xq, const float *Xd, const float *Xs, int64_t ldd,
                           uint16_t *C, int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
 RGemmPlan plan_rgemm(int64_t M, int64_t N, int64_t K);
+// Row-stream GEMM (mmq_rgemm.hip rstream_kernel, opt-in GQ_RSTREAM): Q4_K, 1..16 tokens, prepared x~
+size_t rstream_partial_bytes(int64_t M, int64_t N, int64_t K);
+hipError_t launch_rstream(const uint8_t *A, const uint16_t *X, uint16_t *C, void *partials, int64_t M, int64_t N,
+                          int64_t K, int64_t ldc, hipStream_t s);
 // resident workgroups one CU holds at once (LDS-bound: Q4_K at 16 tokens 3, at 32 two, else one)
 int rgemm_per_cu(int fmt, int nb);
 hipError_t launch_rgemm(int fmt, int aq, const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, void *partials,

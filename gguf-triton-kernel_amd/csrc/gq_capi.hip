@@ -117,6 +117,8 @@ bool parse_key(Tuning &t, const char *key, long long v)
         t.rgemm_spol = (int)v;
     } else if (k == "GQ_SGEMM_FULL") {
         t.sgemm_full = v < 0 ? -1 : (v != 0);
+    } else if (k == "GQ_RSTREAM") {
+        t.rstream = v != 0;
     } else if (k == "GQ_SGEMM_NT") {
         t.sgemm_nt = v != 0;
     } else if (k == "GQ_SGEMM_WRING") {
@@ -143,7 +145,7 @@ void tuning_from_env(Tuning &t)
                                        "GQ_GEMM_NB", "GQ_GEMM_RG", "GQ_GEMM_LOADERS", "GQ_GEMM_SPLITS",
                                        "GQ_GEMM_PARTIAL", "GQ_GEMM_FUSED_REDUCE", "GQ_GEMV_CAP", "GQ_GEMV_R",
                                        "GQ_WGEMM", "GQ_WGEMM_RG", "GQ_WGEMM_NB", "GQ_WGEMM_SPLITS", "GQ_WGEMM_WD",
-                                       "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D", "GQ_RGEMM", "GQ_SGEMM", "GQ_SGEMM_SPLITS", "GQ_SGEMM_STREAMK", "GQ_RGEMM_NB", "GQ_ISKINNY", "GQ_ISKINNY_RG", "GQ_RGEMM_SPOL", "GQ_RGEMM_XCD", "GQ_SGEMM_XCD", "GQ_SGEMM_PAIR", "GQ_SGEMM_FULL", "GQ_SGEMM_WRING", "GQ_SGEMM_NT", "GQ_CUS", "GQ_ABLATE"};
+                                       "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D", "GQ_RGEMM", "GQ_SGEMM", "GQ_SGEMM_SPLITS", "GQ_SGEMM_STREAMK", "GQ_RGEMM_NB", "GQ_ISKINNY", "GQ_ISKINNY_RG", "GQ_RGEMM_SPOL", "GQ_RGEMM_XCD", "GQ_SGEMM_XCD", "GQ_SGEMM_PAIR", "GQ_SGEMM_FULL", "GQ_SGEMM_WRING", "GQ_SGEMM_NT", "GQ_RSTREAM", "GQ_CUS", "GQ_ABLATE"};
     for (const char *k : keys) {
         const char *e = getenv(k); // the only getenv of the library: once per process
         if (!e || !*e) continue;
@@ -351,8 +353,18 @@ bool use_rgemm(int t, int form, int64_t M, int64_t N, int64_t K)
 // The resident GEMM where it applies, ahead of the skinny kernel (4096^2 x16 step: Q4_K 6.8 vs
 // 9.7 us, Q8_0 7.8 vs 11.2, Q6_K 8.1 vs 12.9; x8 Q4_K 6.8 vs 9.3 -- profiles/r04/rg_small.txt)
 // unless the skinny kernel is forced (GQ_SKINNY=1)
+// Row-stream GEMM (mmq_rgemm.hip rstream_kernel; GQ_RSTREAM=1, opt-in): Q4_K, 1..16 tokens on the
+// prepared fp16 x~ (so gq_mmq_ex prepares first), weight rows streamed in 1152-byte runs
+bool use_rstream(int t, int form, int64_t M, int64_t N, int64_t K, int act)
+{
+    if (gq::tuning().rstream != 1 || t != GQ_Q4_K || form != gq::AF_F16 || act != GQ_ACT_Q8_1) return false;
+    return N >= 1 && N <= 16 && K % 256 == 0 && M > 0 && M * (K / 256) * 144 < ((int64_t)1 << 31) &&
+           N * K < ((int64_t)1 << 30);
+}
+
 bool rgemm_route(int t, int form, int64_t M, int64_t N, int64_t K, int act)
 {
+    if (use_rstream(t, form, M, N, K, act)) return false;
     if (!use_rgemm(t, form, M, N, K)) return false;
     return gq::tuning().skinny != 1 || !use_skinny(t, form, N, act);
 }
@@ -465,6 +477,10 @@ size_t ws_bytes(int t, int act, int64_t M, int64_t N, int64_t K)
         const int64_t mr = gemm_rows_per_launch(t, M, K), nt = sk ? N : gemm_toks_per_launch(N, K);
         size_t p = use_rgemm(t, r.form, M, N, K) ? gq::plan_rgemm(M, N, K).partial_bytes
                    : use_sgemm(t, r.form, M, N, K) ? sgemm_partial_bytes(t, M, N, K) : 0;
+        if (use_rstream(t, r.form, M, N, K, act)) {
+            const size_t q = gq::rstream_partial_bytes(M, N, K);
+            p = q > p ? q : p;
+        }
         for (int64_t mc : {mr, M % mr})
             for (int64_t nc : {nt, N % nt})
                 if (mc > 0 && nc > 0) {
@@ -700,6 +716,11 @@ static int compute(gq_type t, int act, const void *A, void *workspace, size_t wo
         // (the kernel is chosen by the call's token count: every chunk runs the same arithmetic)
         // (<= 32 skinny tokens are never cut: their x~ is far below the guard, and the token
         // count sets the kernel's K split)
+        if (use_rstream(t, r.form, M, N, K, act)) {
+            e = gq::launch_rstream((const uint8_t *)A, c.xdeq, (uint16_t *)C, c.partials, M, N, K, ldc, s);
+            if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (rstream): %s", hipGetErrorString(e));
+            return GQ_OK;
+        }
         if (rgemm_route(t, r.form, M, N, K, act)) {
             e = gq::launch_rgemm(t, 0, (const uint8_t *)A, c.xdeq, K, (uint16_t *)C, c.partials, gq::plan_rgemm(M, N, K),
                                  M, N, K, ldc, s);
@@ -796,7 +817,7 @@ int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int6
         return GQ_OK;
     }
     if (!r.gemv && !r.blas && act == GQ_ACT_Q8_1 && r.form == gq::AF_F16 && !use_wgemm(t, r.form, N) && !use_skinny(t, r.form, N) &&
-        !use_sgemm(t, r.form, M, N, K) &&
+        !use_sgemm(t, r.form, M, N, K) && !use_rstream(t, r.form, M, N, K, act) &&
         gemm_rows_per_launch(t, M, K) >= M &&
         gemm_toks_per_launch(N, K) >= N) {
         // 16/32-token tiles whose split fits LDS: the GEMM quantizes the activations itself (no
@@ -1146,6 +1167,7 @@ const char *gq_debug_route(gq_type t, gq_act act, int64_t M, int64_t N, int64_t 
     if (!prepared && use_iskinny(t, route(t, act, N, K).form, M, N, K, act)) return "iskinny_q4k_kernel";
     if (r.blas) return "dequant_kernel + hipBLASLt";
     if (r.gemv) return "gemv_kernel";
+    if (use_rstream(t, r.form, M, N, K, act)) return "rstream_kernel + rstream_reduce_kernel";
     if (rgemm_route(t, r.form, M, N, K, act)) return "rgemm_kernel + gemm_reduce_f16_kernel";
     if (use_skinny(t, r.form, N, act)) return "skinny_kernel";
     if (use_sgemm(t, r.form, M, N, K)) {

@@ -185,3 +185,30 @@ def test_xcd_order_same_bits(fmt, M, N, K, route, tune):
     sub = np.concatenate([qA[r * rb:(r + 1) * rb] for r in rows])
     got = outs[1].cpu().numpy()[:, rows]
     assert O.max_rel_err(got, O.mmq_from_fp16(fmt, sub, B, len(rows), N, K, O.IDEAL)) <= TIGHT
+
+
+@pytest.mark.parametrize("M,N,K", [(11008, 16, 4096), (4096, 8, 11008), (300, 5, 2816), (31, 6, 256), (1000, 16, 768),
+                                   (97, 13, 2304)])
+def test_rstream_parity(M, N, K, tune):
+    """The row-stream GEMM (GQ_RSTREAM=1, opt-in: Q4_K at 1..16 tokens, 32-row groups x 8 super-blocks
+    per stage, chunk partials summed by rstream_reduce) against the oracle -- ragged rows and
+    tokens, a short last K chunk (K = 11008: 43 super-blocks), fewer rows than one group -- and
+    within the GEMM tolerance of the default route, through gq_mmq_ex and the prepared call."""
+    import kernels._lib as kl
+    qA = random_blocks("q4_k", M, K, seed=M + K + N)
+    B = random_activations(N, K, seed=N + 7 * K)
+    A_t, B_t = _t(qA.view(np.int8)), _t(B)
+    ref = _mmq("q4_k", A_t, B_t, M, N, K).cpu().numpy()
+    tune(GQ_RSTREAM=1)
+    assert kl.route_name(kl.GQ_Q4_K, M, N, K).startswith("rstream_kernel")
+    assert kl.route_name(kl.GQ_Q4_K, M, N, K, prepared=True).startswith("rstream_kernel")
+    got = _mmq("q4_k", A_t, B_t, M, N, K).cpu().numpy()
+    gotp = _prepared("q4_k", A_t, B_t, M, N, K).cpu().numpy()
+    assert np.isfinite(got.astype(np.float32)).all()
+    assert np.array_equal(got.view(np.int16), gotp.view(np.int16))
+    assert O.max_rel_err(got, ref) <= TIGHT
+    rows = np.sort(np.random.default_rng(M).choice(M, size=min(M, 24), replace=False))
+    rb = qA.size // M
+    sub = np.concatenate([qA[r * rb:(r + 1) * rb] for r in rows])
+    assert O.max_rel_err(got[:, rows], O.mmq_from_fp16("q4_k", sub, B, len(rows), N, K, O.IDEAL)) <= TIGHT
+    assert O.allclose(O.mmq_from_fp16("q4_k", sub, B, len(rows), N, K, O.EXACT), got[:, rows], 0.01)
