@@ -118,7 +118,8 @@ bool parse_key(Tuning &t, const char *key, long long v)
     } else if (k == "GQ_SGEMM_FULL") {
         t.sgemm_full = v < 0 ? -1 : (v != 0);
     } else if (k == "GQ_RSTREAM") {
-        t.rstream = v != 0;
+        if (!in({0, 1, 2})) return false;
+        t.rstream = (int)v;
     } else if (k == "GQ_SGEMM_NT") {
         t.sgemm_nt = v != 0;
     } else if (k == "GQ_SGEMM_WRING") {
@@ -357,7 +358,7 @@ bool use_rgemm(int t, int form, int64_t M, int64_t N, int64_t K)
 // prepared fp16 x~ (so gq_mmq_ex prepares first), weight rows streamed in 1152-byte runs
 bool use_rstream(int t, int form, int64_t M, int64_t N, int64_t K, int act)
 {
-    if (gq::tuning().rstream != 1 || t != GQ_Q4_K || form != gq::AF_F16 || act != GQ_ACT_Q8_1) return false;
+    if (gq::tuning().rstream == 0 || t != GQ_Q4_K || form != gq::AF_F16 || act != GQ_ACT_Q8_1) return false;
     return N >= 1 && N <= 16 && K % 256 == 0 && M > 0 && M * (K / 256) * 144 < ((int64_t)1 << 31) &&
            N * K < ((int64_t)1 << 30);
 }

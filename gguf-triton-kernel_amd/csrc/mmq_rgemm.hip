@@ -1128,49 +1128,55 @@ hipError_t launch_sgemm_grouped(const SGroupItem *items, int n, int64_t N, const
 // super-block w of the group (q4k_frags + 16 MFMA), the waves' fp32 sums are added in LDS and the
 // group's chunk partial stored fp32 at P[chunk][token][row]; rstream_reduce sums the chunks.
 namespace {
-constexpr int RS_ROWS = 32, RS_KSB = 8, RS_RB = RS_KSB * 144, RS_W = RS_ROWS * RS_RB; // 36 KiB per stage
-constexpr int RS_WI = RS_W / 1024, RS_NW = (RS_WI + RW - 1) / RW;
-constexpr int RS_X = RS_KSB * 16 * 512, RS_RED = RW * 512 * 4;
-constexpr int RS_LDS = RS_X + 2 * RS_W + RS_RED + 1024;
-static_assert(RS_LDS <= LDS_CAP && RS_W % 1024 == 0, "rstream LDS");
+// KSB super-blocks per K chunk (x~ resident: KSB x 8 KiB), NS ring slots of 32 rows x KSB
+// super-blocks; KSB = 8: 1152-byte runs, 2 slots, wave w = super-block w of both 16-row halves;
+// KSB = 4: 576-byte runs, 4 slots, wave w = super-block w & 3 of half w >> 2
+template <int KSB> struct RS {
+    static constexpr int ROWS = 32, RB = KSB * 144, W = ROWS * RB, WI = W / 1024, NW = (WI + RW - 1) / RW;
+    static constexpr int NS = KSB == 8 ? 2 : 4, X = KSB * 16 * 512, RED = RW * 512 * 4;
+    static constexpr int LDS = X + NS * W + RED + 1024;
+    static_assert(LDS <= LDS_CAP && W % 1024 == 0 && (NS - 2) * NW <= 63, "rstream LDS");
+};
 
+template <int KSB>
 __global__ __launch_bounds__(64 * RW) void rstream_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
                                                          float *__restrict__ P, int64_t M, int64_t N, int64_t K, int wpc)
 {
-    __shared__ __attribute__((aligned(1024))) uint8_t lds[RS_LDS];
-    uint8_t *const xim = lds, *const ring = lds + RS_X;
-    float *const red = (float *)(lds + RS_X + 2 * RS_W);
-    uint8_t *const scratch = lds + RS_X + 2 * RS_W + RS_RED;
+    using G = RS<KSB>;
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[G::LDS];
+    uint8_t *const xim = lds, *const ring = lds + G::X;
+    float *const red = (float *)(lds + G::X + G::NS * G::W);
+    uint8_t *const scratch = lds + G::X + G::NS * G::W + G::RED;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, l16 = lane & 15;
     const int nsb = (int)(K / 256), chunk = (int)blockIdx.x / wpc, part = (int)blockIdx.x % wpc;
-    const int sb0 = RS_KSB * chunk, ksb = nsb - sb0 < RS_KSB ? nsb - sb0 : RS_KSB;
-    const int64_t groups = (M + RS_ROWS - 1) / RS_ROWS;
+    const int sb0 = KSB * chunk, ksb = nsb - sb0 < KSB ? nsb - sb0 : KSB;
+    const int64_t groups = (M + G::ROWS - 1) / G::ROWS;
     const int64_t g0 = groups * part / wpc, g1 = groups * (part + 1) / wpc;
     const int nst = (int)(g1 - g0);
     const int64_t row_bytes = (int64_t)nsb * 144;
     const __amdgpu_buffer_rsrc_t wrs =
         __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, (int)(uint32_t)((M * row_bytes + 15) & ~(int64_t)15), 0x00020000);
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, (int)(uint32_t)(N * K * 2), 0x00020000);
-    // stage j: rows 32 (g0 + j) + r, image row r at 1152 r, super-block s at position s ^ (r & 7)
+    // stage j: rows 32 (g0 + j) + r, image row r at RB r, super-block s at position s ^ (r % KSB)
     auto issue_w = [&](int j) __attribute__((always_inline)) {
-        uint8_t *slot = ring + (j & 1) * RS_W;
+        uint8_t *slot = ring + (j % G::NS) * G::W;
 #pragma unroll
-        for (int i = 0; i < RS_NW; ++i) {
+        for (int i = 0; i < G::NW; ++i) {
             const int k = wave + RW * i, p = 64 * k + lane;
-            const bool real = k < RS_WI;
-            const int r = p / 72, q = p - 72 * r, sp = q / 9, pc = q - 9 * sp, sbi = sp ^ (r & 7);
-            const int64_t row0 = (g0 + j) * RS_ROWS + r, row = row0 < M ? row0 : M - 1;
+            const bool real = k < G::WI;
+            const int r = p / (9 * KSB), q = p - 9 * KSB * r, sp = q / 9, pc = q - 9 * sp, sbi = sp ^ (r & (KSB - 1));
+            const int64_t row0 = (g0 + j) * G::ROWS + r, row = row0 < M ? row0 : M - 1;
             const int sbs = sbi < ksb ? sbi : 0;
             const uint32_t vo = real ? (uint32_t)(row * row_bytes + 144 * (int64_t)(sb0 + sbs)) + 16u * pc : 0u;
             dma16(wrs, real ? slot + 1024 * k : scratch, vo, 0u);
         }
     };
     if (nst <= 0) return;
-    // the chunk's x~ (64 DMA instructions, 8 per wave; absent super-blocks skipped)
+    // the chunk's x~ (8 DMA instructions per super-block; absent super-blocks skipped)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < KSB; ++i) {
         const int k = wave + RW * i, s = k >> 3, pp = 64 * (k & 7) + lane;
         if (s >= ksb) continue;
         const int u = pp / 128, r = (pp / 8) % 16, qd = pp & 7, q = qd ^ act_swz(r);
@@ -1178,51 +1184,56 @@ __global__ __launch_bounds__(64 * RW) void rstream_kernel(const uint8_t *__restr
         const uint32_t vo = (uint32_t)(tok * K * 2) + 2u * (uint32_t)(256 * (sb0 + s) + sub_elem<Q4_K>(u, q));
         dma16(xrs, xim + 8192 * s + 16 * pp, vo, 0u);
     }
-    issue_w(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    int issued = G::NS - 1 < nst ? G::NS - 1 : nst;
+    for (int j = 0; j < issued; ++j) issue_w(j);
+    // this wave's super-block and 16-row halves
+    constexpr int NH = KSB == 8 ? 2 : 1;
+    const int mysb = KSB == 8 ? wave : (wave & 3), h0 = KSB == 8 ? 0 : (wave >> 2);
     for (int j = 0; j < nst; ++j) {
-        if (j > 0) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // stage j (this wave's part)
-            __builtin_amdgcn_s_barrier();
-        }
-        if (j + 1 < nst) issue_w(j + 1); // into the slot stage j-1 left
-        f32x4 acc[RRG];
+        vm_wait<(G::NS - 2) * G::NW>((issued - 1 - j) * G::NW); // stage j (and, at j = 0, the x~)
+        __builtin_amdgcn_s_barrier();
+        if (issued < nst) issue_w(issued++); // into the slot stage j-1 left
+        f32x4 acc[NH];
 #pragma unroll
-        for (int rg = 0; rg < RRG; ++rg) acc[rg] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        if (wave < ksb) {
-            const uint8_t *slot = ring + (j & 1) * RS_W;
+        for (int h = 0; h < NH; ++h) acc[h] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        if (mysb < ksb) {
+            const uint8_t *slot = ring + (j % G::NS) * G::W;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const uint8_t *xs = xim + 8192 * wave + u * 2048;
-                f16x8 af[RRG][2];
+                const uint8_t *xs = xim + 8192 * mysb + u * 2048;
+                f16x8 af[NH][2];
 #pragma unroll
-                for (int rg = 0; rg < RRG; ++rg) {
-                    const int r = 16 * rg + l16;
-                    const uint8_t *wr = slot + RS_RB * r + 144 * (wave ^ (r & 7));
-                    q4k_frags(wr, wr + 16 + 32 * u, g, u, af[rg]);
+                for (int h = 0; h < NH; ++h) {
+                    const int r = 16 * (h0 + h) + l16;
+                    const uint8_t *wr = slot + G::RB * r + 144 * (mysb ^ (r & (KSB - 1)));
+                    q4k_frags(wr, wr + 16 + 32 * u, g, u, af[h]);
                 }
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
                     const f16x8 bk = *(const f16x8 *)(xs + 128 * l16 + 16 * ((4 * s + g) ^ act_swz(l16)));
 #pragma unroll
-                    for (int rg = 0; rg < RRG; ++rg)
-                        acc[rg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[rg][s], bk, acc[rg], 0, 0, 0);
+                    for (int h = 0; h < NH; ++h)
+                        acc[h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[h][s], bk, acc[h], 0, 0, 0);
                 }
             }
         }
-        // the waves' sums: red[wave][(4 rg + i) * 64 + lane], then thread t adds the 8 waves' t
+        // the waves' sums in LDS (output e = (half, i, lane)), then thread t adds its output's terms
 #pragma unroll
-        for (int rg = 0; rg < RRG; ++rg)
+        for (int h = 0; h < NH; ++h)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) red[wave * 512 + (4 * rg + i) * 64 + lane] = acc[rg][i];
+            for (int i = 0; i < 4; ++i) red[wave * 512 + (4 * h + i) * 64 + lane] = acc[h][i];
         __builtin_amdgcn_s_barrier();
         {
-            const int t = tid, e = t >> 6, ln = t & 63, rg = e >> 2, i = e & 3;
+            const int t = tid, hh = t >> 8, i = (t >> 6) & 3, ln = t & 63;
             float v = 0.f;
+            if constexpr (KSB == 8) {
 #pragma unroll
-            for (int w = 0; w < RW; ++w) v += red[w * 512 + t];
-            const int64_t row = (g0 + j) * RS_ROWS + 16 * rg + 4 * (ln >> 4) + i, tok = ln & 15;
+                for (int w = 0; w < RW; ++w) v += red[w * 512 + t];
+            } else {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) v += red[(4 * hh + w) * 512 + i * 64 + ln];
+            }
+            const int64_t row = (g0 + j) * G::ROWS + 16 * hh + 4 * (ln >> 4) + i, tok = ln & 15;
             if (row < M && tok < N) P[((int64_t)chunk * N + tok) * M + row] = v;
         }
     }
@@ -1238,11 +1249,12 @@ __global__ __launch_bounds__(256) void rstream_reduce_kernel(const float *__rest
     for (int c = 0; c < chunks; ++c) v += P[((int64_t)c * N + tok) * M + row];
     C[tok * ldc + row] = f2h_bits(v);
 }
+int rs_ksb() { return tuning().rstream == 2 ? 4 : 8; }
 } // namespace
 
 size_t rstream_partial_bytes(int64_t M, int64_t N, int64_t K)
 {
-    const int64_t chunks = (K / 256 + RS_KSB - 1) / RS_KSB;
+    const int64_t chunks = (K / 256 + rs_ksb() - 1) / rs_ksb();
     return (size_t)chunks * (size_t)N * (size_t)M * 4;
 }
 
@@ -1250,12 +1262,13 @@ hipError_t launch_rstream(const uint8_t *A, const uint16_t *X, uint16_t *C, void
                           int64_t K, int64_t ldc, hipStream_t s)
 {
     if (N < 1 || N > 16 || K % 256 != 0 || M < 1) return hipErrorInvalidValue;
-    const int chunks = (int)((K / 256 + RS_KSB - 1) / RS_KSB);
-    const int64_t groups = (M + RS_ROWS - 1) / RS_ROWS;
+    const int ksb = rs_ksb(), chunks = (int)((K / 256 + ksb - 1) / ksb);
+    const int64_t groups = (M + 31) / 32;
     int64_t wpc = num_cus() / chunks;
     if (wpc < 1) wpc = 1;
     if (wpc > groups) wpc = groups;
-    rstream_kernel<<<dim3((unsigned)(chunks * wpc)), dim3(64 * RW), 0, s>>>(A, X, (float *)partials, M, N, K, (int)wpc);
+    if (ksb == 8) rstream_kernel<8><<<dim3((unsigned)(chunks * wpc)), dim3(64 * RW), 0, s>>>(A, X, (float *)partials, M, N, K, (int)wpc);
+    else rstream_kernel<4><<<dim3((unsigned)(chunks * wpc)), dim3(64 * RW), 0, s>>>(A, X, (float *)partials, M, N, K, (int)wpc);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     rstream_reduce_kernel<<<dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s>>>((const float *)partials, C, M, N,
