@@ -51,6 +51,7 @@ struct Tuning {
     int sgemm_xcd = 0;                        // GQ_SGEMM_XCD: the same for the (single-matrix) streaming GEMM
     int sgemm_full = -1;                      // GQ_SGEMM_FULL: Q4_K 16/32-token tiles stream whole super-blocks:
                                               // 1 every streaming GEMM, 0 none, -1 single matrices (measured gain)
+    int rstream_wpc = 0;                      // GQ_RSTREAM_WPC: its workgroups per K chunk (0: CUs / chunks)
     int rstream = 0;                          // GQ_RSTREAM: Q4_K 1..16-token GEMMs on the row-stream kernel
     int sgemm_wring = 0;                      // GQ_SGEMM_WRING: Q4_K 16-token tiles on per-wave weight rings
     int sgemm_nt = 0;                         // GQ_SGEMM_NT: the streaming GEMM's weight DMAs non-temporal

@@ -117,6 +117,9 @@ bool parse_key(Tuning &t, const char *key, long long v)
         t.rgemm_spol = (int)v;
     } else if (k == "GQ_SGEMM_FULL") {
         t.sgemm_full = v < 0 ? -1 : (v != 0);
+    } else if (k == "GQ_RSTREAM_WPC") {
+        if (v < 0 || v > 4096) return false;
+        t.rstream_wpc = (int)v;
     } else if (k == "GQ_RSTREAM") {
         if (!in({0, 1, 2})) return false;
         t.rstream = (int)v;
@@ -146,7 +149,7 @@ void tuning_from_env(Tuning &t)
                                        "GQ_GEMM_NB", "GQ_GEMM_RG", "GQ_GEMM_LOADERS", "GQ_GEMM_SPLITS",
                                        "GQ_GEMM_PARTIAL", "GQ_GEMM_FUSED_REDUCE", "GQ_GEMV_CAP", "GQ_GEMV_R",
                                        "GQ_WGEMM", "GQ_WGEMM_RG", "GQ_WGEMM_NB", "GQ_WGEMM_SPLITS", "GQ_WGEMM_WD",
-                                       "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D", "GQ_RGEMM", "GQ_SGEMM", "GQ_SGEMM_SPLITS", "GQ_SGEMM_STREAMK", "GQ_RGEMM_NB", "GQ_ISKINNY", "GQ_ISKINNY_RG", "GQ_RGEMM_SPOL", "GQ_RGEMM_XCD", "GQ_SGEMM_XCD", "GQ_SGEMM_PAIR", "GQ_SGEMM_FULL", "GQ_SGEMM_WRING", "GQ_SGEMM_NT", "GQ_RSTREAM", "GQ_CUS", "GQ_ABLATE"};
+                                       "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D", "GQ_RGEMM", "GQ_SGEMM", "GQ_SGEMM_SPLITS", "GQ_SGEMM_STREAMK", "GQ_RGEMM_NB", "GQ_ISKINNY", "GQ_ISKINNY_RG", "GQ_RGEMM_SPOL", "GQ_RGEMM_XCD", "GQ_SGEMM_XCD", "GQ_SGEMM_PAIR", "GQ_SGEMM_FULL", "GQ_SGEMM_WRING", "GQ_SGEMM_NT", "GQ_RSTREAM", "GQ_RSTREAM_WPC", "GQ_CUS", "GQ_ABLATE"};
     for (const char *k : keys) {
         const char *e = getenv(k); // the only getenv of the library: once per process
         if (!e || !*e) continue;

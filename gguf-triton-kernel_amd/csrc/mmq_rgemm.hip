@@ -1264,7 +1264,7 @@ hipError_t launch_rstream(const uint8_t *A, const uint16_t *X, uint16_t *C, void
     if (N < 1 || N > 16 || K % 256 != 0 || M < 1) return hipErrorInvalidValue;
     const int ksb = rs_ksb(), chunks = (int)((K / 256 + ksb - 1) / ksb);
     const int64_t groups = (M + 31) / 32;
-    int64_t wpc = num_cus() / chunks;
+    int64_t wpc = tuning().rstream_wpc > 0 ? tuning().rstream_wpc : num_cus() / chunks; // (GQ_RSTREAM_WPC: A/B)
     if (wpc < 1) wpc = 1;
     if (wpc > groups) wpc = groups;
     if (ksb == 8) rstream_kernel<8><<<dim3((unsigned)(chunks * wpc)), dim3(64 * RW), 0, s>>>(A, X, (float *)partials, M, N, K, (int)wpc);
