@@ -121,7 +121,7 @@ bool parse_key(Tuning &t, const char *key, long long v)
         if (v < 0 || v > 4096) return false;
         t.rstream_wpc = (int)v;
     } else if (k == "GQ_RSTREAM") {
-        if (!in({0, 1, 2, 3})) return false;
+        if (!in({0, 1, 2})) return false;
         t.rstream = (int)v;
     } else if (k == "GQ_SGEMM_NT") {
         t.sgemm_nt = v != 0;

@@ -1131,21 +1131,18 @@ namespace {
 // KSB super-blocks per K chunk (x~ resident: KSB x 8 KiB), NS ring slots of 32 rows x KSB
 // super-blocks; KSB = 8: 1152-byte runs, 2 slots, wave w = super-block w of both 16-row halves;
 // KSB = 4: 576-byte runs, 4 slots, wave w = super-block w & 3 of half w >> 2
-template <int KSB, int ROWS_ = 32> struct RS {
-    static constexpr int ROWS = ROWS_, RB = KSB * 144, W = ROWS * RB, WI = W / 1024, NW = (WI + RW - 1) / RW;
-    static constexpr int X = KSB * 16 * 512, RED = RW * 512 * 4;
-    static constexpr int NSF = (LDS_CAP - X - RED - 1024) / W, NS = NSF > 4 ? 4 : NSF;
+template <int KSB> struct RS {
+    static constexpr int ROWS = 32, RB = KSB * 144, W = ROWS * RB, WI = W / 1024, NW = (WI + RW - 1) / RW;
+    static constexpr int NS = KSB == 8 ? 2 : 4, X = KSB * 16 * 512, RED = RW * 512 * 4;
     static constexpr int LDS = X + NS * W + RED + 1024;
-    // (super-block, 16-row half) pairs per wave
-    static constexpr int NH = KSB * (ROWS / 16) / RW;
-    static_assert(NS >= 2 && LDS <= LDS_CAP && W % 1024 == 0 && (NS - 2) * NW <= 63 && NH >= 1, "rstream LDS");
+    static_assert(LDS <= LDS_CAP && W % 1024 == 0 && (NS - 2) * NW <= 63, "rstream LDS");
 };
 
-template <int KSB, int ROWS_ = 32>
+template <int KSB>
 __global__ __launch_bounds__(64 * RW) void rstream_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
                                                          float *__restrict__ P, int64_t M, int64_t N, int64_t K, int wpc)
 {
-    using G = RS<KSB, ROWS_>;
+    using G = RS<KSB>;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[G::LDS];
     uint8_t *const xim = lds, *const ring = lds + G::X;
     float *const red = (float *)(lds + G::X + G::NS * G::W);
@@ -1190,8 +1187,8 @@ __global__ __launch_bounds__(64 * RW) void rstream_kernel(const uint8_t *__restr
     int issued = G::NS - 1 < nst ? G::NS - 1 : nst;
     for (int j = 0; j < issued; ++j) issue_w(j);
     // this wave's super-block and 16-row halves
-    constexpr int NH = G::NH;
-    const int mysb = wave % KSB, h0 = (wave / KSB) * NH;
+    constexpr int NH = KSB == 8 ? 2 : 1;
+    const int mysb = KSB == 8 ? wave : (wave & 3), h0 = KSB == 8 ? 0 : (wave >> 2);
     for (int j = 0; j < nst; ++j) {
         vm_wait<(G::NS - 2) * G::NW>((issued - 1 - j) * G::NW); // stage j (and, at j = 0, the x~)
         __builtin_amdgcn_s_barrier();
@@ -1226,13 +1223,15 @@ __global__ __launch_bounds__(64 * RW) void rstream_kernel(const uint8_t *__restr
 #pragma unroll
             for (int i = 0; i < 4; ++i) red[wave * 512 + (4 * h + i) * 64 + lane] = acc[h][i];
         __builtin_amdgcn_s_barrier();
-        if (tid < G::ROWS * 16) {
+        {
             const int t = tid, hh = t >> 8, i = (t >> 6) & 3, ln = t & 63;
             float v = 0.f;
+            if constexpr (KSB == 8) {
 #pragma unroll
-            for (int w = 0; w < RW; ++w) {
-                const int wh0 = (w / KSB) * NH;
-                if (hh >= wh0 && hh < wh0 + NH) v += red[w * 512 + (4 * (hh - wh0) + i) * 64 + ln];
+                for (int w = 0; w < RW; ++w) v += red[w * 512 + t];
+            } else {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) v += red[(4 * hh + w) * 512 + i * 64 + ln];
             }
             const int64_t row = (g0 + j) * G::ROWS + 16 * hh + 4 * (ln >> 4) + i, tok = ln & 15;
             if (row < M && tok < N) P[((int64_t)chunk * N + tok) * M + row] = v;
@@ -1251,7 +1250,6 @@ __global__ __launch_bounds__(256) void rstream_reduce_kernel(const float *__rest
     C[tok * ldc + row] = f2h_bits(v);
 }
 int rs_ksb() { return tuning().rstream == 2 ? 4 : 8; }
-int rs_rows() { return tuning().rstream == 3 ? 16 : 32; }
 } // namespace
 
 size_t rstream_partial_bytes(int64_t M, int64_t N, int64_t K)
@@ -1265,12 +1263,11 @@ hipError_t launch_rstream(const uint8_t *A, const uint16_t *X, uint16_t *C, void
 {
     if (N < 1 || N > 16 || K % 256 != 0 || M < 1) return hipErrorInvalidValue;
     const int ksb = rs_ksb(), chunks = (int)((K / 256 + ksb - 1) / ksb);
-    const int64_t groups = (M + rs_rows() - 1) / rs_rows();
+    const int64_t groups = (M + 31) / 32;
     int64_t wpc = tuning().rstream_wpc > 0 ? tuning().rstream_wpc : num_cus() / chunks; // (GQ_RSTREAM_WPC: A/B)
     if (wpc < 1) wpc = 1;
     if (wpc > groups) wpc = groups;
-    if (rs_rows() == 16) rstream_kernel<8, 16><<<dim3((unsigned)(chunks * wpc)), dim3(64 * RW), 0, s>>>(A, X, (float *)partials, M, N, K, (int)wpc);
-    else if (ksb == 8) rstream_kernel<8><<<dim3((unsigned)(chunks * wpc)), dim3(64 * RW), 0, s>>>(A, X, (float *)partials, M, N, K, (int)wpc);
+    if (ksb == 8) rstream_kernel<8><<<dim3((unsigned)(chunks * wpc)), dim3(64 * RW), 0, s>>>(A, X, (float *)partials, M, N, K, (int)wpc);
     else rstream_kernel<4><<<dim3((unsigned)(chunks * wpc)), dim3(64 * RW), 0, s>>>(A, X, (float *)partials, M, N, K, (int)wpc);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

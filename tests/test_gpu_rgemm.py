@@ -189,7 +189,7 @@ def test_xcd_order_same_bits(fmt, M, N, K, route, tune):
 
 @pytest.mark.parametrize("M,N,K", [(11008, 16, 4096), (4096, 8, 11008), (300, 5, 2816), (31, 6, 256), (1000, 16, 768),
                                    (97, 13, 2304)])
-@pytest.mark.parametrize("mode", [1, 2, 3])
+@pytest.mark.parametrize("mode", [1, 2])
 def test_rstream_parity(M, N, K, mode, tune):
     """The row-stream GEMM (GQ_RSTREAM=1, opt-in: Q4_K at 1..16 tokens, 32-row groups x 8 super-blocks
     per stage, chunk partials summed by rstream_reduce) against the oracle -- ragged rows and
@@ -200,7 +200,7 @@ def test_rstream_parity(M, N, K, mode, tune):
     B = random_activations(N, K, seed=N + 7 * K)
     A_t, B_t = _t(qA.view(np.int8)), _t(B)
     ref = _mmq("q4_k", A_t, B_t, M, N, K).cpu().numpy()
-    tune(GQ_RSTREAM=mode)  # (1: 8-super-block chunks, 32-row groups, 2 slots; 2: 4 super-blocks, 4 slots; 3: 16-row groups, 4 slots)
+    tune(GQ_RSTREAM=mode)  # (1: 8-super-block chunks, 2-slot ring; 2: 4-super-block chunks, 4 slots)
     assert kl.route_name(kl.GQ_Q4_K, M, N, K).startswith("rstream_kernel")
     assert kl.route_name(kl.GQ_Q4_K, M, N, K, prepared=True).startswith("rstream_kernel")
     got = _mmq("q4_k", A_t, B_t, M, N, K).cpu().numpy()
