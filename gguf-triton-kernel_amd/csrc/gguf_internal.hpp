@@ -147,7 +147,7 @@ hipError_t launch_gemm(int fmt, const uint8_t *A, const GemmAct &x, uint16_t *C,
 // The split-K sum of the fp16 partials gemm_kernel (and rgemm_kernel) write: tiles of 16*8*rg
 // rows x 16*nb tokens, S splits (mmq_gemm.hip gemm_reduce_f16_kernel).
 hipError_t launch_gemm_reduce_f16(int nb, int rg, const uint16_t *P, uint16_t *C, int64_t M, int64_t N, int64_t ldc,
-                                  int S, int tiles_x, int tiles_y, hipStream_t s = nullptr);
+                                  int S, int tiles_x, int tiles_y, hipStream_t s);
 
 // Resident-split GEMM (mmq_rgemm.hip): 256 rows x 16*nb tokens x one super-block per workgroup,
 // the split's weights and activations loaded once into LDS; split-K over every super-block

@@ -605,7 +605,7 @@ void gq_debug_reset_tuning(void) { gq::reset_tuning(); }
 
 int gq_block_elems(gq_type t) { return block_elems(t); }
 int gq_block_bytes(gq_type t) { return block_bytes(t); }
-int gq_version(void) { return 102; }
+int gq_version(void) { return 103; }
 const char *gq_last_error(void) { return g_err.c_str(); }
 
 size_t gq_mmq_call_workspace_size(gq_type t, gq_act act, int64_t M, int64_t N, int64_t K)

@@ -906,7 +906,7 @@ hipError_t launch_snb(const uint8_t *A, const uint16_t *X, uint16_t *C, void *P,
                                                         (tuning().sgemm_full != 0) | (tuning().sgemm_wring ? 2 : 0));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.splits == 1) return e;
-    return launch_gemm_reduce_f16(NB, RRG, (const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n);
+    return launch_gemm_reduce_f16(NB, RRG, (const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n, s);
 }
 
 template <int F, int NB, int AQ>
@@ -918,7 +918,7 @@ hipError_t launch_nb(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t 
                                                             tuning().rgemm_xcd);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.splits == 1) return e;
-    return launch_gemm_reduce_f16(NB, RRG, (const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n);
+    return launch_gemm_reduce_f16(NB, RRG, (const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n, s);
 }
 
 template <int F, int AQ>
@@ -1222,6 +1222,9 @@ __global__ __launch_bounds__(64 * RW) void rstream_kernel(const uint8_t *__restr
         for (int h = 0; h < NH; ++h)
 #pragma unroll
             for (int i = 0; i < 4; ++i) red[wave * 512 + (4 * h + i) * 64 + lane] = acc[h][i];
+        // the sums must have left the LDS queue before another wave reads them: gfx950's compiler
+        // puts no wait in front of a raw s_barrier (round 4's non-identical bits, mode 3)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         {
             const int t = tid, hh = t >> 8, i = (t >> 6) & 3, ln = t & 63;

@@ -102,17 +102,23 @@ def _bind_mmq_ex():
     entry bound to the ctypes-loaded library's gq_mmq_ex -- ~0.2 us per call instead of ctypes'
     ~1.5-2 us of argument conversion), or the ctypes function when that module was not built.
     Both reach the same gq_mmq_ex in the same loaded libgguf_mmq.so."""
-    import glob
+    import importlib.machinery
     import importlib.util
     fn = lib().gq_mmq_ex
-    paths = sorted(glob.glob(os.path.join(LIB_DIR, "_gqcall*.so")))
-    if not paths:
-        return fn
-    spec = importlib.util.spec_from_file_location("_gqcall", paths[0])
-    mod = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(mod)
-    mod.bind(ctypes.cast(fn, ctypes.c_void_p).value)
-    return mod.mmq_ex
+    # only a build for THIS interpreter's ABI (lib/ may hold builds for several Pythons)
+    for suffix in importlib.machinery.EXTENSION_SUFFIXES:
+        path = os.path.join(LIB_DIR, "_gqcall" + suffix)
+        if not os.path.exists(path):
+            continue
+        try:
+            spec = importlib.util.spec_from_file_location("_gqcall", path)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+        except ImportError:
+            continue
+        mod.bind(ctypes.cast(fn, ctypes.c_void_p).value)
+        return mod.mmq_ex
+    return fn
 
 
 def set_tuning(key: str, value: int):

@@ -238,7 +238,8 @@ int gq_mmq_grouped_prepared(gq_act act, const gq_gemm_item *items, int n, int64_
 /* Text of the last error on this thread ("" if none). */
 const char *gq_last_error(void);
 
-/* Library ABI version (major * 100 + minor). */
+/* Library ABI version (major * 100 + minor).  103: gq_gemm_item, gq_mmq_grouped_prepared[_workspace_size],
+ * gq_debug_route, and larger workspace sizes for the GEMM routes (round 4). */
 int gq_version(void);
 
 /*

@@ -213,3 +213,23 @@ def test_rstream_parity(M, N, K, mode, tune):
     sub = np.concatenate([qA[r * rb:(r + 1) * rb] for r in rows])
     assert O.max_rel_err(got[:, rows], O.mmq_from_fp16("q4_k", sub, B, len(rows), N, K, O.IDEAL)) <= TIGHT
     assert O.allclose(O.mmq_from_fp16("q4_k", sub, B, len(rows), N, K, O.EXACT), got[:, rows], 0.01)
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("M,N,K", [(4096, 8, 11008), (11008, 16, 4096)])
+def test_rstream_repeat_bit_identical(M, N, K, mode, tune):
+    """Round 4's 16-row mode returned different bits from two calls on the same input: its
+    per-wave sums were written to LDS and read by other waves after a raw s_barrier with no
+    `s_waitcnt lgkmcnt(0)` in front (gfx950's compiler inserts none; tools/check_barriers.py
+    lists such barriers from the ISA).  The surviving modes shared that epilogue; with the wait
+    every call must give the same bits -- twelve calls, prepared and not, at K = 11008."""
+    import kernels._lib as kl
+    qA = random_blocks("q4_k", M, K, seed=K + 1)
+    B = random_activations(N, K, seed=N + 2)
+    A_t, B_t = _t(qA.view(np.int8)), _t(B)
+    tune(GQ_RSTREAM=mode)
+    assert kl.route_name(kl.GQ_Q4_K, M, N, K).startswith("rstream_kernel")
+    first = _mmq("q4_k", A_t, B_t, M, N, K)
+    for i in range(12):
+        C = _prepared("q4_k", A_t, B_t, M, N, K) if i % 2 else _mmq("q4_k", A_t, B_t, M, N, K)
+        assert torch.equal(C.view(torch.int16), first.view(torch.int16)), i
