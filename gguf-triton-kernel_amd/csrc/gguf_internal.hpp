@@ -20,20 +20,13 @@ struct Tuning {
     int decode_early = -1;                    // GQ_DECODE_EARLY: ring refill vs quantization (-1: auto)
     int decode_q6_img = -1;                   // GQ_DECODE_Q6_IMG: Q6_K aligned ring image (-1: K <= 4096)
     int gemm_aq = 1;                          // GQ_GEMM_AQ: in-kernel quantization of 16/32-token tiles
-    int gemm_aq_nb4 = 0;                      // GQ_GEMM_AQ_NB4
     int gemm_nb = 0;                          // GQ_GEMM_NB: 16-token groups per tile, 1/2/4/8 (0: auto)
     int gemm_rg = 0;                          // GQ_GEMM_RG: 1 or 2 (0: auto)
     int gemm_loaders = -1;                    // GQ_GEMM_LOADERS: 0 or 4 (-1: auto)
     long long gemm_splits = 0;                // GQ_GEMM_SPLITS: split-K factor (0: auto)
     int gemm_partial_f32 = 0;                 // GQ_GEMM_PARTIAL=f32
-    int gemm_fused_reduce = 0;                // GQ_GEMM_FUSED_REDUCE
     long long gemv_cap = 0;                   // GQ_GEMV_CAP (0: auto)
     int gemv_r = 0;                           // GQ_GEMV_R: rows per wave, 1/2/4 (0: auto)
-    int wgemm = -1;                           // GQ_WGEMM: weight-register GEMM 0 off / 1 on (-1: auto)
-    int wgemm_rg = 0;                         // GQ_WGEMM_RG: 1 or 2 (0: auto)
-    int wgemm_nb = 0;                         // GQ_WGEMM_NB: 2/4/8 (0: auto)
-    int wgemm_splits = 0;                     // GQ_WGEMM_SPLITS (0: auto)
-    int wgemm_wd = 0;                         // GQ_WGEMM_WD: weight super-blocks in registers, 2/3/4 (0: auto)
     int skinny = -1;                          // GQ_SKINNY: 5..32-token kernel (-1 auto, 0 off, 1 every 1..32)
     int skinny_rg = 0;                        // GQ_SKINNY_RG: fragments per workgroup, 1..4 (0: auto)
     int skinny_d = 0;                         // GQ_SKINNY_D: super-blocks in the register ring, 2..4 (0: auto)
@@ -42,21 +35,10 @@ struct Tuning {
     int sgemm_splits = 0;                     // GQ_SGEMM_SPLITS (0: auto)
     int sgemm_streamk = -1;                   // GQ_SGEMM_STREAMK: stream-K unit split of the auto plan: 1 every
                                               // streaming GEMM, 0 none, -1 the grouped plans (the measured gain)
-    int iskinny = 0;                          // GQ_ISKINNY: integer-MFMA skinny kernel (Q4_K 5..16 tokens) 0 off / 1 on
-    int iskinny_rg = 0;                       // GQ_ISKINNY_RG: its 16-row fragments per unit, 1..4 (0: auto)
     int rgemm_nb = 0;                         // GQ_RGEMM_NB: the resident GEMM's token tile, 1/2/4/8 x 16 (0: auto)
     int rgemm_spol = 16;                      // GQ_RGEMM_SPOL: its partial stores' cache policy 0 / 2 (nt) / 16 (sc1)
-    int rgemm_xcd = 0;                        // GQ_RGEMM_XCD: workgroup -> tile order per XCD (mmq_rgemm.hip xcd_tile):
-                                              // 0 blockIdx as is, 1 a tile's splits consecutive, 2 a split's row tiles
-    int sgemm_xcd = 0;                        // GQ_SGEMM_XCD: the same for the (single-matrix) streaming GEMM
     int sgemm_full = -1;                      // GQ_SGEMM_FULL: Q4_K 16/32-token tiles stream whole super-blocks:
                                               // 1 every streaming GEMM, 0 none, -1 single matrices (measured gain)
-    int rstream_wpc = 0;                      // GQ_RSTREAM_WPC: its workgroups per K chunk (0: CUs / chunks)
-    int rstream = 0;                          // GQ_RSTREAM: Q4_K 1..16-token GEMMs on the row-stream kernel
-    int sgemm_wring = 0;                      // GQ_SGEMM_WRING: Q4_K 16-token tiles on per-wave weight rings
-    int sgemm_nt = 0;                         // GQ_SGEMM_NT: the streaming GEMM's weight DMAs non-temporal
-    int sgemm_pair = 0;                       // GQ_SGEMM_PAIR: issue a super-block's two half stages together
-                                              // (1: rings of 4+ slots, 2: 3+; mmq_rgemm.hip sgemm_body)
     int cus = 0;                              // GQ_CUS: compute units to plan for (0: the device's count)
     int ablate = 0;                           // GQ_ABLATE (GQ_ABLATION diagnostic builds only)
 };
@@ -121,8 +103,6 @@ struct GemmPlan {
     int loaders = 0;           // 4: four dedicated DMA-issuing waves beside the 8 multiplying ones
     int pf16 = 0;              // split-K partials stored as fp16 (else fp32)
     int aq = 0;                // activations quantized in-kernel from raw fp16 (GemmAct::xraw)
-    int fused_reduce = 0;      // fp16 split-K partials summed by each row group's last-arriving wave
-                               // (no reduce launch); 0: gemm_reduce_f16_kernel
     size_t partial_bytes = 0;  // fp32 partial slabs needed when splits > 1
 };
 // Activations as the GEMM reads them: fp16 x~ (act_quant DEQ) or, for the code forms, codes +
@@ -158,16 +138,8 @@ struct RGemmPlan {
     int nb = 8, tiles_m = 0, tiles_n = 0, splits = 1;
     size_t partial_bytes = 0;
 };
-// Integer-MFMA skinny kernel (mmq_iskinny.hip): Q4_K, 1..16 tokens, act_quant's I8 form
-// (codes [N][K], d and s block-major [K/32][ldd], s at Xs)
-int iskinny_rg(int64_t M);
-hipError_t launch_iskinny(int fmt, const uint8_t *A, const int8_t *Xq, const float *Xd, const float *Xs, int64_t ldd,
-                          uint16_t *C, int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
+
 RGemmPlan plan_rgemm(int64_t M, int64_t N, int64_t K);
-// Row-stream GEMM (mmq_rgemm.hip rstream_kernel, opt-in GQ_RSTREAM): Q4_K, 1..16 tokens, prepared x~
-size_t rstream_partial_bytes(int64_t M, int64_t N, int64_t K);
-hipError_t launch_rstream(const uint8_t *A, const uint16_t *X, uint16_t *C, void *partials, int64_t M, int64_t N,
-                          int64_t K, int64_t ldc, hipStream_t s);
 // resident workgroups one CU holds at once (LDS-bound: Q4_K at 16 tokens 3, at 32 two, else one)
 int rgemm_per_cu(int fmt, int nb);
 hipError_t launch_rgemm(int fmt, int aq, const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, void *partials,
@@ -203,21 +175,6 @@ struct SGroupPlan {
 SGroupPlan plan_sgemm_grouped(const SGroupItem *items, int n, int64_t N, int splits);
 hipError_t launch_sgemm_grouped(const SGroupItem *items, int n, int64_t N, const SGroupPlan &g, void *partials,
                                 hipStream_t s);
-
-// Weight-register GEMM (mmq_wgemm.hip): weights streamed into VGPRs a super-block ahead,
-// activations (fp16 x~, act_quant DEQ form) register-staged into a two-slot LDS ring; 128*rg
-// rows x 16*nb tokens per workgroup, split-K `splits` ways (fp16 partials + wreduce_kernel).
-struct WGemmPlan {
-    int rg = 2, nb = 8;
-    int wd = 2; // super-blocks of weights held in registers (wd - 1 in flight): 2, 3, 4 (4: rg 1 only)
-    int tiles_m = 0, tiles_n = 0;
-    int splits = 1, sb_per_split = 1;
-    size_t partial_bytes = 0;
-};
-// rg / nb: tile shape (rg in {1, 2}, nb in {2, 4, 8}); splits <= 0: as many as fill 256 CUs
-WGemmPlan plan_wgemm(int fmt, int64_t M, int64_t N, int64_t K, int rg, int nb, int splits);
-hipError_t launch_wgemm(int fmt, const uint8_t *A, const uint16_t *X, uint16_t *C, void *partials,
-                        const WGemmPlan &plan, int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
 
 // Grouped decode (mmq_decode.hip): several matrices -- each its own type, activations (N x K
 // fp16, row stride ldx) and output (N x M, stride ldc) -- in one launch per token tile, the

@@ -1,6 +1,5 @@
 // gguf_wfrag.hpp -- GGUF weight fragments straight from HBM into registers, dequantized to the
-// A operand of v_mfma_f32_16x16x32_f16 (shared by the batched GEMM, mmq_wgemm.hip, and the
-// skinny-token kernel, mmq_skinny.hip).
+// A operand of v_mfma_f32_16x16x32_f16 (the skinny-token kernel, mmq_skinny.hip).
 //
 // WB<F>: one super-block (256 K elements; Q8_0: 8 blocks) of one 16-row fragment -- lane
 // (row c = lane&15, group g = lane>>4) loads its bytes with 16-byte buffer loads and produces
@@ -41,17 +40,7 @@ __device__ __forceinline__ uint32_t bl4(__amdgpu_buffer_rsrc_t r, uint32_t v, ui
 {
     return __builtin_amdgcn_raw_buffer_load_b32(r, v, s, 0);
 }
-// Diagnostic ablations (GQ_WGEMM_ABL, a -D of a separate build; 0 in the product): 1 = no
-// weight loads after the prologue, 2 = no activation DMA after the prologue, 4 = no MFMA,
-// 8 = no dequantization (raw bits as fp16), 16 / 32 = weight loads at 4- / 16-byte aligned
-// addresses (wrong values: access-pattern probes).
-#ifndef GQ_WGEMM_ABL
-#define GQ_WGEMM_ABL 0
-#endif
-constexpr int ABL = GQ_WGEMM_ABL;
-// weight byte offset as loaded (the alignment probe rounds it down)
-constexpr uint32_t WMASK = ABL & 32 ? ~15u : (ABL & 16 ? ~3u : ~0u);
-__device__ __forceinline__ uint32_t wo(uint32_t v) { return v & WMASK; }
+__device__ __forceinline__ uint32_t wo(uint32_t v) { return v; } // (the weight byte offset as loaded)
 
 // ---------------------------------------------------------------------------------------
 // One super-block of one 16-row fragment: this lane's bytes (WB<F>::load: back-to-back 16-byte

@@ -40,11 +40,6 @@ bool parse_key(Tuning &t, const char *key, long long v)
     } else if (k == "GQ_DECODE_NT4_CACHE") t.decode_nt4_cache = v != 0;
     else if (k == "GQ_DECODE_F8_ITC") t.decode_f8_itc = v != 0;
     else if (k == "GQ_SGEMM_STREAMK") t.sgemm_streamk = v < 0 ? -1 : (v != 0);
-    else if (k == "GQ_ISKINNY") t.iskinny = v != 0;
-    else if (k == "GQ_ISKINNY_RG") {
-        if (v < 0 || v > 4) return false;
-        t.iskinny_rg = (int)v;
-    }
     else if (k == "GQ_RGEMM_NB") {
         if (!in({0, 1, 2, 4, 8})) return false;
         t.rgemm_nb = (int)v;
@@ -58,7 +53,6 @@ bool parse_key(Tuning &t, const char *key, long long v)
         t.decode_q6_img = (int)v;
     }
     else if (k == "GQ_GEMM_AQ") t.gemm_aq = v != 0;
-    else if (k == "GQ_GEMM_AQ_NB4") t.gemm_aq_nb4 = v != 0;
     else if (k == "GQ_GEMM_NB") {
         if (!in({0, 1, 2, 4, 8})) return false;
         t.gemm_nb = (int)v;
@@ -72,28 +66,12 @@ bool parse_key(Tuning &t, const char *key, long long v)
         if (v < 0) return false;
         t.gemm_splits = v;
     } else if (k == "GQ_GEMM_PARTIAL") t.gemm_partial_f32 = v != 0; // 1 = f32
-    else if (k == "GQ_GEMM_FUSED_REDUCE") t.gemm_fused_reduce = v != 0;
     else if (k == "GQ_GEMV_CAP") {
         if (v < 0) return false;
         t.gemv_cap = v;
     } else if (k == "GQ_GEMV_R") {
         if (!in({0, 1, 2, 4})) return false;
         t.gemv_r = (int)v;
-    } else if (k == "GQ_WGEMM") {
-        if (!in({-1, 0, 1})) return false;
-        t.wgemm = (int)v;
-    } else if (k == "GQ_WGEMM_RG") {
-        if (!in({0, 1, 2})) return false;
-        t.wgemm_rg = (int)v;
-    } else if (k == "GQ_WGEMM_NB") {
-        if (!in({0, 2, 4, 8})) return false;
-        t.wgemm_nb = (int)v;
-    } else if (k == "GQ_WGEMM_SPLITS") {
-        if (v < 0 || v > 4096) return false;
-        t.wgemm_splits = (int)v;
-    } else if (k == "GQ_WGEMM_WD") {
-        if (!in({0, 2, 3, 4})) return false;
-        t.wgemm_wd = (int)v;
     } else if (k == "GQ_SKINNY") {
         if (!in({-1, 0, 1})) return false;
         t.skinny = (int)v;
@@ -117,22 +95,6 @@ bool parse_key(Tuning &t, const char *key, long long v)
         t.rgemm_spol = (int)v;
     } else if (k == "GQ_SGEMM_FULL") {
         t.sgemm_full = v < 0 ? -1 : (v != 0);
-    } else if (k == "GQ_RSTREAM_WPC") {
-        if (v < 0 || v > 4096) return false;
-        t.rstream_wpc = (int)v;
-    } else if (k == "GQ_RSTREAM") {
-        if (!in({0, 1, 2})) return false;
-        t.rstream = (int)v;
-    } else if (k == "GQ_SGEMM_NT") {
-        t.sgemm_nt = v != 0;
-    } else if (k == "GQ_SGEMM_WRING") {
-        t.sgemm_wring = v != 0;
-    } else if (k == "GQ_SGEMM_PAIR") {
-        if (!in({0, 1, 2})) return false;
-        t.sgemm_pair = (int)v;
-    } else if (k == "GQ_RGEMM_XCD" || k == "GQ_SGEMM_XCD") {
-        if (!in({0, 1, 2})) return false;
-        (k == "GQ_RGEMM_XCD" ? t.rgemm_xcd : t.sgemm_xcd) = (int)v;
     } else if (k == "GQ_CUS") {
         if (v < 0 || v > 1024) return false;
         t.cus = (int)v;
@@ -144,12 +106,12 @@ bool parse_key(Tuning &t, const char *key, long long v)
 void tuning_from_env(Tuning &t)
 {
     t = Tuning{};
-    static const char *const keys[] = {"GQ_BLAS_MIN_TOKENS", "GQ_GEMM_MAX_BYTES", "GQ_GEMM_I8", "GQ_NO_FUSED_DECODE",
-                                       "GQ_DECODE_MAXNT", "GQ_DECODE_NT4_CACHE", "GQ_DECODE_Q6_IMG", "GQ_DECODE_F8_ITC", "GQ_DECODE_EARLY", "GQ_GEMM_AQ", "GQ_GEMM_AQ_NB4",
+    static const char *const keys[] = {"GQ_BLAS_MIN_TOKENS", "GQ_GEMM_MAX_BYTES", "GQ_GEMM_I8", "GQ_NO_FUSED_DECODE", "GQ_DECODE_MAXNT",
+                                       "GQ_DECODE_NT4_CACHE", "GQ_DECODE_Q6_IMG", "GQ_DECODE_F8_ITC", "GQ_DECODE_EARLY", "GQ_GEMM_AQ",
                                        "GQ_GEMM_NB", "GQ_GEMM_RG", "GQ_GEMM_LOADERS", "GQ_GEMM_SPLITS",
-                                       "GQ_GEMM_PARTIAL", "GQ_GEMM_FUSED_REDUCE", "GQ_GEMV_CAP", "GQ_GEMV_R",
-                                       "GQ_WGEMM", "GQ_WGEMM_RG", "GQ_WGEMM_NB", "GQ_WGEMM_SPLITS", "GQ_WGEMM_WD",
-                                       "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D", "GQ_RGEMM", "GQ_SGEMM", "GQ_SGEMM_SPLITS", "GQ_SGEMM_STREAMK", "GQ_RGEMM_NB", "GQ_ISKINNY", "GQ_ISKINNY_RG", "GQ_RGEMM_SPOL", "GQ_RGEMM_XCD", "GQ_SGEMM_XCD", "GQ_SGEMM_PAIR", "GQ_SGEMM_FULL", "GQ_SGEMM_WRING", "GQ_SGEMM_NT", "GQ_RSTREAM", "GQ_RSTREAM_WPC", "GQ_CUS", "GQ_ABLATE"};
+                                       "GQ_GEMM_PARTIAL", "GQ_GEMV_CAP", "GQ_GEMV_R", "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D",
+                                       "GQ_RGEMM", "GQ_SGEMM", "GQ_SGEMM_SPLITS", "GQ_SGEMM_STREAMK", "GQ_RGEMM_NB", "GQ_RGEMM_SPOL",
+                                       "GQ_SGEMM_FULL", "GQ_CUS", "GQ_ABLATE"};
     for (const char *k : keys) {
         const char *e = getenv(k); // the only getenv of the library: once per process
         if (!e || !*e) continue;
@@ -262,23 +224,7 @@ int64_t gemm_toks_per_launch(int64_t N, int64_t K)
     return n < 16 ? 16 : (n < N ? n : N);
 }
 
-// Weight-register GEMM (mmq_wgemm.hip) for the fp16 form (GQ_WGEMM forces it on / off).  The
-// choice depends on the type and the token count only -- never on the row count, so a row
-// subset (a shard) runs the same arithmetic as the whole matrix (bit-identical rows).  By
-// default Q4_K from 33 tokens on, where it measured level or faster than the LDS-DMA GEMM
-// (graph-timed, profiles/r03/wgemm_ab_final.log: 11008x4096 x128 30.6 vs 35.1 us, x512 86.2 vs
-// 93.9; 4096^2 x128 15.6 vs 15.4, x256 22.3 vs 22.5; 4096x11008 x128 28.8 vs 29.1).  Q8_0 and
-// Q6_K stay on the LDS-DMA GEMM (4096^2 x128 Q8_0 20.8 vs 17.3; Q6_K 28672x8192 x128 115.6 vs
-// 111.9).
-constexpr int64_t kWgemmMinTokens = 33;
 constexpr int64_t kRgemmMinTokens = 5, kRgemmMultiRoundTokens = 32, kRgemmMultiRoundTokensQ4 = 64;
-bool use_wgemm(int t, int form, int64_t N)
-{
-    const int w = gq::tuning().wgemm;
-    if (form != gq::AF_F16 || w == 0) return false;
-    if (w == 1) return true;
-    return t == GQ_Q4_K && N >= kWgemmMinTokens;
-}
 // Skinny-token kernel (mmq_skinny.hip).  By type and token count only (a row subset runs the
 // same arithmetic as the whole matrix): by default Q4_K and Q8_0 at 5..16 tokens, where it
 // measured faster than the LDS-DMA GEMM (profiles/r03/tails/route_sw.log, step incl. act_quant,
@@ -303,18 +249,6 @@ gq::SkinnyPlan skinny_plan(int t, int64_t M, int64_t N, int64_t K)
     return gq::plan_skinny(t, M, N, K, tu.skinny_rg, tu.skinny_d);
 }
 
-gq::WGemmPlan wgemm_plan(int t, int64_t M, int64_t N, int64_t K)
-{
-    const gq::Tuning &tu = gq::tuning();
-    const int nb = tu.wgemm_nb ? tu.wgemm_nb : (N > 64 ? 8 : (N > 32 ? 4 : 2));
-    const int rg = tu.wgemm_rg ? tu.wgemm_rg : 1;
-    gq::WGemmPlan p = gq::plan_wgemm(t, M, N, K, rg, nb, tu.wgemm_splits);
-    // weight super-blocks held in registers (wd - 1 in flight); launch_wgemm lowers 4 to 3 for
-    // the two-fragment waves, 3 to 2 where it would spill
-    p.wd = tu.wgemm_wd ? tu.wgemm_wd : (nb <= 4 ? 4 : 3);
-    return p;
-}
-
 // Resident-split GEMM (mmq_rgemm.hip: 256 rows x <= 128 tokens x one super-block per workgroup,
 // the split's operands loaded once; profiles/r04/).  By default where its grid is one round of
 // the chip and at least half of it (a 4096-row matrix at K = 4096: 16 x 16 workgroups) and the
@@ -322,14 +256,12 @@ gq::WGemmPlan wgemm_plan(int t, int64_t M, int64_t N, int64_t K)
 // prepared (gq_mmq_prepared).  With split-K over every super-block its partial sums differ from
 // gemm_kernel's (other splits), so a forced split factor (GQ_GEMM_SPLITS) keeps gemm_kernel.
 // GQ_RGEMM=1: wherever it applies (tests), 0: off.
-// A knob of the LDS-DMA or weight-register GEMM set (tests, A/B of those kernels): the automatic
+// A knob of the LDS-DMA GEMM set (tests, A/B of those kernels): the automatic
 // resident / streaming routes stand aside so the call reaches the kernel the knob is for.
 bool gemm_knob_pinned()
 {
     const gq::Tuning &u = gq::tuning();
-    return u.gemm_splits > 0 || u.gemm_nb || u.gemm_rg || u.gemm_loaders >= 0 || u.gemm_partial_f32 ||
-           u.gemm_fused_reduce || u.gemm_aq_nb4 || u.wgemm == 1 || u.wgemm_splits || u.wgemm_rg || u.wgemm_nb ||
-           u.wgemm_wd;
+    return u.gemm_splits > 0 || u.gemm_nb || u.gemm_rg || u.gemm_loaders >= 0 || u.gemm_partial_f32;
 }
 
 bool use_rgemm(int t, int form, int64_t M, int64_t N, int64_t K)
@@ -357,28 +289,10 @@ bool use_rgemm(int t, int form, int64_t M, int64_t N, int64_t K)
 // The resident GEMM where it applies, ahead of the skinny kernel (4096^2 x16 step: Q4_K 6.8 vs
 // 9.7 us, Q8_0 7.8 vs 11.2, Q6_K 8.1 vs 12.9; x8 Q4_K 6.8 vs 9.3 -- profiles/r04/rg_small.txt)
 // unless the skinny kernel is forced (GQ_SKINNY=1)
-// Row-stream GEMM (mmq_rgemm.hip rstream_kernel; GQ_RSTREAM=1, opt-in): Q4_K, 1..16 tokens on the
-// prepared fp16 x~ (so gq_mmq_ex prepares first), weight rows streamed in 1152-byte runs
-bool use_rstream(int t, int form, int64_t M, int64_t N, int64_t K, int act)
-{
-    if (gq::tuning().rstream == 0 || t != GQ_Q4_K || form != gq::AF_F16 || act != GQ_ACT_Q8_1) return false;
-    return N >= 1 && N <= 16 && K % 256 == 0 && M > 0 && M * (K / 256) * 144 < ((int64_t)1 << 31) &&
-           N * K < ((int64_t)1 << 30);
-}
-
 bool rgemm_route(int t, int form, int64_t M, int64_t N, int64_t K, int act)
 {
-    if (use_rstream(t, form, M, N, K, act)) return false;
     if (!use_rgemm(t, form, M, N, K)) return false;
     return gq::tuning().skinny != 1 || !use_skinny(t, form, N, act);
-}
-
-// Integer-MFMA skinny kernel (mmq_iskinny.hip): Q4_K, 5..16 tokens, gq_mmq_ex only (it quantizes
-// into the I8 form itself; the prepared calls keep the fp16 routes).  GQ_ISKINNY=1: on.
-bool use_iskinny(int t, int form, int64_t M, int64_t N, int64_t K, int act)
-{
-    if (gq::tuning().iskinny != 1 || t != GQ_Q4_K || form != gq::AF_F16 || act != GQ_ACT_Q8_1) return false;
-    return N >= 5 && N <= 16 && K % 256 == 0 && M > 0 && M * (K / 256) * 144 < ((int64_t)1 << 31) && N * K < ((int64_t)1 << 31);
 }
 
 // Streaming 256-row GEMM (mmq_rgemm.hip sgemm_kernel) on the prepared x~, where the resident
@@ -477,20 +391,14 @@ size_t ws_bytes(int t, int act, int64_t M, int64_t N, int64_t K)
     else if (!r.gemv && gq::gemm_supported(t, K) && M > 0 && N > 0) {
         // split-K partials of the largest need over the launch shapes (full and remainder chunks)
         // (the kernel is chosen by the call's token count, so every chunk runs the same arithmetic)
-        const bool sk = use_skinny(t, r.form, N, act), wg = use_wgemm(t, r.form, N);
+        const bool sk = use_skinny(t, r.form, N, act);
         const int64_t mr = gemm_rows_per_launch(t, M, K), nt = sk ? N : gemm_toks_per_launch(N, K);
         size_t p = use_rgemm(t, r.form, M, N, K) ? gq::plan_rgemm(M, N, K).partial_bytes
                    : use_sgemm(t, r.form, M, N, K) ? sgemm_partial_bytes(t, M, N, K) : 0;
-        if (use_rstream(t, r.form, M, N, K, act)) {
-            const size_t q = gq::rstream_partial_bytes(M, N, K);
-            p = q > p ? q : p;
-        }
         for (int64_t mc : {mr, M % mr})
             for (int64_t nc : {nt, N % nt})
                 if (mc > 0 && nc > 0) {
-                    const size_t q = sk   ? 0
-                                     : wg ? wgemm_plan(t, mc, nc, K).partial_bytes
-                                          : gq::plan_gemm(t, mc, nc, K, r.form).partial_bytes;
+                    const size_t q = sk ? 0 : gq::plan_gemm(t, mc, nc, K, r.form).partial_bytes;
                     p = q > p ? q : p;
                 }
         b += align_up(p);
@@ -720,11 +628,6 @@ static int compute(gq_type t, int act, const void *A, void *workspace, size_t wo
         // (the kernel is chosen by the call's token count: every chunk runs the same arithmetic)
         // (<= 32 skinny tokens are never cut: their x~ is far below the guard, and the token
         // count sets the kernel's K split)
-        if (use_rstream(t, r.form, M, N, K, act)) {
-            e = gq::launch_rstream((const uint8_t *)A, c.xdeq, (uint16_t *)C, c.partials, M, N, K, ldc, s);
-            if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (rstream): %s", hipGetErrorString(e));
-            return GQ_OK;
-        }
         if (rgemm_route(t, r.form, M, N, K, act)) {
             e = gq::launch_rgemm(t, 0, (const uint8_t *)A, c.xdeq, K, (uint16_t *)C, c.partials, gq::plan_rgemm(M, N, K),
                                  M, N, K, ldc, s);
@@ -747,7 +650,7 @@ static int compute(gq_type t, int act, const void *A, void *workspace, size_t wo
             if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (sgemm): %s", hipGetErrorString(e));
             return GQ_OK;
         }
-        const bool sk = use_skinny(t, r.form, N, act), wg = use_wgemm(t, r.form, N);
+        const bool sk = use_skinny(t, r.form, N, act);
         const int64_t mr = gemm_rows_per_launch(t, M, K), nt = sk ? N : gemm_toks_per_launch(N, K);
         e = hipSuccess;
         for (int64_t n0 = 0; n0 < N && e == hipSuccess; n0 += nt)
@@ -756,12 +659,6 @@ static int compute(gq_type t, int act, const void *A, void *workspace, size_t wo
                 if (sk) {
                     e = gq::launch_skinny(t, (const uint8_t *)A + m0 * row_bytes_of(t, K), c.xdeq + n0 * K,
                                           (uint16_t *)C + n0 * ldc + m0, skinny_plan(t, mc, nc, K), mc, nc, K, ldc, s);
-                    continue;
-                }
-                if (wg) {
-                    e = gq::launch_wgemm(t, (const uint8_t *)A + m0 * row_bytes_of(t, K), c.xdeq + n0 * K,
-                                         (uint16_t *)C + n0 * ldc + m0, c.partials, wgemm_plan(t, mc, nc, K), mc, nc,
-                                         K, ldc, s);
                     continue;
                 }
                 gq::GemmAct x;
@@ -800,15 +697,6 @@ int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int6
         if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (decode): %s", hipGetErrorString(e));
         return GQ_OK;
     }
-    if (use_iskinny(t, r.form, M, N, K, act)) {
-        rc = prepare(act, B, N, K, ldb, workspace, workspace_bytes, (hipStream_t)stream, 2 | 4);
-        if (rc != GQ_OK) return rc;
-        Carved c = carve(act, workspace, N, K);
-        hipError_t e = gq::launch_iskinny(t, (const uint8_t *)A, c.xq, c.xd, c.xs, scale_ld(N), (uint16_t *)C, M, N, K, ldc,
-                                          (hipStream_t)stream);
-        if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (iskinny): %s", hipGetErrorString(e));
-        return GQ_OK;
-    }
     if (rgemm_route(t, r.form, M, N, K, act) && ldb % 8 == 0 &&
         ((uintptr_t)B & 15) == 0) {
         // one launch (+ the split-K reduce): the activations quantized inside the GEMM (q8_1, or
@@ -820,8 +708,8 @@ int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int6
         if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (rgemm): %s", hipGetErrorString(e));
         return GQ_OK;
     }
-    if (!r.gemv && !r.blas && act == GQ_ACT_Q8_1 && r.form == gq::AF_F16 && !use_wgemm(t, r.form, N) && !use_skinny(t, r.form, N) &&
-        !use_sgemm(t, r.form, M, N, K) && !use_rstream(t, r.form, M, N, K, act) &&
+    if (!r.gemv && !r.blas && act == GQ_ACT_Q8_1 && r.form == gq::AF_F16 && !use_skinny(t, r.form, N) &&
+        !use_sgemm(t, r.form, M, N, K) &&
         gemm_rows_per_launch(t, M, K) >= M &&
         gemm_toks_per_launch(N, K) >= N) {
         // 16/32-token tiles whose split fits LDS: the GEMM quantizes the activations itself (no
@@ -1168,10 +1056,8 @@ const char *gq_debug_route(gq_type t, gq_act act, int64_t M, int64_t N, int64_t 
     g_err.clear();
     const Route r = route(t, act, N, K);
     if (!prepared && fused_decode_route(t, act, N, K)) return "stream_decode_kernel";
-    if (!prepared && use_iskinny(t, route(t, act, N, K).form, M, N, K, act)) return "iskinny_q4k_kernel";
     if (r.blas) return "dequant_kernel + hipBLASLt";
     if (r.gemv) return "gemv_kernel";
-    if (use_rstream(t, r.form, M, N, K, act)) return "rstream_kernel + rstream_reduce_kernel";
     if (rgemm_route(t, r.form, M, N, K, act)) return "rgemm_kernel + gemm_reduce_f16_kernel";
     if (use_skinny(t, r.form, N, act)) return "skinny_kernel";
     if (use_sgemm(t, r.form, M, N, K)) {
@@ -1180,6 +1066,5 @@ const char *gq_debug_route(gq_type t, gq_act act, int64_t M, int64_t N, int64_t 
         return sgemm_streamk(t, M, N, K, it, g) ? "sgemm_grouped_kernel + reduce_grouped_kernel (stream-K)"
                                                : "sgemm_kernel + gemm_reduce_f16_kernel";
     }
-    if (use_wgemm(t, r.form, N)) return "wgemm_kernel + wreduce_kernel";
     return "gemm_kernel + gemm_reduce_f16_kernel";
 }

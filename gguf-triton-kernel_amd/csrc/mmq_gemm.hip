@@ -58,31 +58,9 @@ namespace gq {
 __device__ unsigned long long g_gstamps[65536][8];
 #endif
 
-// Split-K arrival counters of the fused reduce: one per (tile, wave) of a launch, zero at module
-// load and put back to zero by the wave that reads S - 1 from it, so every launch finds its
-// counters at zero with no memset node.  Each launch takes the next range of the pool (a host
-// cursor): launches on different streams use distinct counters unless 1 << 18 counters'
-// worth of launches lie between them.  Limits of this opt-in (test / A-B only) form: the base is
-// taken at launch time, so a captured graph bakes it in -- two replays of one graph running at
-// the same time, or a graph replayed concurrently with eager launches that wrapped the ring onto
-// its range, would share counters.  Use it on one stream, one replay at a time; the default
-// (separate reduce launch) has no such state.
-constexpr int kSplitCounters = 1 << 18;
-__device__ unsigned g_split_cnt[kSplitCounters];
-
 namespace {
 
-int split_counters(int need)
-{
-    static std::atomic<uint32_t> cursor{0};
-    uint32_t base = cursor.fetch_add((uint32_t)need);
-    base %= (uint32_t)kSplitCounters;
-    if (base + (uint32_t)need > (uint32_t)kSplitCounters) base = 0; // need <= 256 * NWAVE << pool
-    return (int)base;
-}
-
 constexpr int LDS_MAX = 160 * 1024;
-constexpr int FR_GROUP = 8; // fused split-K reduce: splits whose partial loads are issued together
 
 
 // multiplying waves per workgroup: 8 = 512 threads, two waves per SIMD (4 waves x two row
@@ -186,8 +164,7 @@ template <int F, int NB, int RG, int ABL = 0, int AM = AF_F16, int NL = 0, int A
 __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *__restrict__ A, const void *__restrict__ X,
                                                    const float *__restrict__ XD, uint16_t *__restrict__ C,
                                                    float *__restrict__ P, int64_t M, int64_t N, int64_t K,
-                                                   int64_t ldc, int64_t ldd, int wstages_per_split, int pf16,
-                                                   int cbase)
+                                                   int64_t ldc, int64_t ldd, int wstages_per_split, int pf16)
 {
     using G = Cfg<F, NB, RG, AM, NL, AQ>;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[G::LDS_BYTES];
@@ -620,121 +597,19 @@ __global__ __launch_bounds__(64 * (NWAVE + NL)) void gemm_kernel(const uint8_t *
                 return (u32x2){(uint32_t)f2h_bits(v[0] * down) | ((uint32_t)f2h_bits(v[1] * down) << 16),
                                (uint32_t)f2h_bits(v[2] * down) | ((uint32_t)f2h_bits(v[3] * down) << 16)};
             };
-            // fused reduce (cbase >= 0): the partials and e's are written and read with
-            // agent-scope cache policy (sc1: coherent across the XCDs' L2s per access), so the
-            // hand-over needs no cache-wide write-back or invalidate -- those cost 3x the GEMM
-            const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
-                (void *)P, 0, (int)(uint32_t)(nblk * (G::BM * G::BN * 2 + NWAVE * 4)), 0x00020000);
-            const uint32_t es_off = (uint32_t)(nblk * (G::BM * G::BN * 2));
-            if (lane == 0) { // (its RG row groups share it)
-                if (cbase >= 0) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)e, prs, es_off + (uint32_t)(bidx * NWAVE + wave) * 4u, 0, 16);
-                else es[bidx * NWAVE + wave] = e;
-            }
+            if (lane == 0) es[bidx * NWAVE + wave] = e; // (its RG row groups share it)
 #pragma unroll
             for (int rg = 0; rg < RG; ++rg) {
                 if constexpr (NB == 1) {
                     const int q = (RG * wave + rg) * 64 + lane;
-                    if (cbase >= 0) __builtin_amdgcn_raw_buffer_store_b64(pk(acc[rg][0]), prs, (uint32_t)(bidx * (G::BM * G::BN * 2) + 8 * q), 0, 16);
-                    else ((u32x2 *)hb)[q] = pk(acc[rg][0]);
+                    ((u32x2 *)hb)[q] = pk(acc[rg][0]);
                 } else {
 #pragma unroll
                     for (int u = 0; u < NB / 2; ++u) {
                         const u32x2 lo = pk(acc[rg][2 * u]), hi = pk(acc[rg][2 * u + 1]);
                         const int q = ((RG * wave + rg) * (NB / 2) + u) * 64 + lane;
                         const u32x4 w = {lo.x, lo.y, hi.x, hi.y};
-                        if (cbase >= 0) __builtin_amdgcn_raw_buffer_store_b128(w, prs, (uint32_t)(bidx * (G::BM * G::BN * 2) + 16 * q), 0, 16);
-                        else ((u32x4 *)hb)[q] = w;
-                    }
-                }
-            }
-            if (RG == 1 && cbase >= 0) { // (128-row tiles only: the 256-row form's registers)
-                // fused reduce: the wave that arrives last at this (tile, wave) row group sums
-                // the row group's S partials in split order -- the arithmetic of
-                // gemm_reduce_f16_kernel, so the two forms give identical bits -- and writes C.
-                // The row groups of a tile are independent: no workgroup barrier, and the
-                // reduction of a tile is spread over its 8 row groups' last waves.
-                const int S = (int)gridDim.z;
-                unsigned *cnt = g_split_cnt + cbase + tile * NWAVE + wave;
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this wave's partials and e have landed
-                unsigned old = 0;
-                if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                old = __builtin_amdgcn_readfirstlane(old);
-                if (old != (unsigned)(S - 1)) {
-#ifdef GQ_GEMM_STAMPS
-                    stamp_out();
-#endif
-                    return;
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // no load moves above the arrival
-                if (lane == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); // next launch
-                constexpr int TPU = NB == 1 ? 1 : 2;      // token tiles per store unit
-                constexpr int UPR = NB == 1 ? 1 : NB / 2; // units per row group
-                constexpr int NU = RG * UPR;              // units this wave sums
-                constexpr int GS = RG == 2 ? 4 : FR_GROUP; // splits whose loads are in flight together
-                // every unit's loads of GS splits issued together (one round trip per GS splits);
-                // splits past S add nothing here, and one +0 at the end stands for the +0's the
-                // reduce kernel adds for them (S not a multiple of 8): x + 0 is x except -0 -> +0
-                f32x4 sum[NU][TPU];
-#pragma unroll
-                for (int n = 0; n < NU; ++n)
-#pragma unroll
-                    for (int j = 0; j < TPU; ++j) sum[n][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-                for (int s0 = 0; s0 < S; s0 += GS) {
-                    u32x2 v[GS][NU][TPU];
-                    float up[GS];
-#pragma unroll
-                    for (int i = 0; i < GS; ++i) {
-                        const int sp = s0 + i < S ? s0 + i : S - 1; // unconditional loads
-                        const uint32_t bo = (uint32_t)((tile * S + sp) * (G::BM * G::BN * 2));
-#pragma unroll
-                        for (int n = 0; n < NU; ++n) {
-                            const int q = (RG * wave * UPR + n) * 64 + lane; // unit index in a block
-                            if constexpr (TPU == 2) {
-                                const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(prs, bo + 16u * q, 0, 16);
-                                v[i][n][0] = (u32x2){w.x, w.y};
-                                v[i][n][1] = (u32x2){w.z, w.w};
-                            } else {
-                                v[i][n][0] = __builtin_amdgcn_raw_buffer_load_b64(prs, bo + 8u * q, 0, 16);
-                            }
-                        }
-                        const int ev = (int)__builtin_amdgcn_raw_buffer_load_b32(prs, es_off + (uint32_t)((tile * S + sp) * NWAVE + wave) * 4u, 0, 16);
-                        up[i] = __builtin_bit_cast(float, (uint32_t)(127 + ev) << 23);
-                    }
-#pragma unroll
-                    for (int i = 0; i < GS; ++i) {
-                        if (s0 + i >= S) break;
-#pragma unroll
-                        for (int n = 0; n < NU; ++n)
-#pragma unroll
-                            for (int j = 0; j < TPU; ++j) {
-                                sum[n][j][0] += h2f(v[i][n][j].x & 0xffffu) * up[i];
-                                sum[n][j][1] += h2f(v[i][n][j].x >> 16) * up[i];
-                                sum[n][j][2] += h2f(v[i][n][j].y & 0xffffu) * up[i];
-                                sum[n][j][3] += h2f(v[i][n][j].y >> 16) * up[i];
-                            }
-                    }
-                }
-                if (S % 8 != 0)
-#pragma unroll
-                    for (int n = 0; n < NU; ++n)
-#pragma unroll
-                        for (int j = 0; j < TPU; ++j) sum[n][j] += (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int n = 0; n < NU; ++n) {
-                    const int rg = n / UPR, u = n % UPR;
-                    const int64_t row = m0 + 16 * (RG * wave + rg) + 4 * g;
-                    if (row >= M) continue;
-#pragma unroll
-                    for (int j = 0; j < TPU; ++j) {
-                        const int64_t tok = n0 + 16 * (TPU * u + j) + l16;
-                        if (tok >= N) continue;
-                        uint16_t *dst = C + tok * ldc + row;
-                        if (row + 4 <= M) {
-                            *(u32x2 *)dst = (u32x2){(uint32_t)f2h_bits(sum[n][j][0]) | ((uint32_t)f2h_bits(sum[n][j][1]) << 16),
-                                                    (uint32_t)f2h_bits(sum[n][j][2]) | ((uint32_t)f2h_bits(sum[n][j][3]) << 16)};
-                        } else {
-                            for (int i = 0; i < 4 && row + i < M; ++i) dst[i] = f2h_bits(sum[n][j][i]);
-                        }
+                        ((u32x4 *)hb)[q] = w;
                     }
                 }
             }
@@ -911,23 +786,21 @@ hipError_t launch_cfg(const uint8_t *A, const GemmAct &x, uint16_t *C, float *P,
     const int cps = pl.chunks_per_split;
     const void *X = AQ ? (const void *)x.xraw : (G::CODES ? (const void *)x.xq : (const void *)x.xdeq);
     const int64_t ldd = AQ ? x.ldx : x.ldd;
-    const bool fused = pl.splits > 1 && pl.pf16 && pl.fused_reduce && RG == 1;
-    const int cb = fused ? split_counters((int)(grid.x * grid.y) * NWAVE) : -1;
 #ifdef GQ_ABLATION
     const int abl = tuning().ablate;
 #define GQ_ABL_CASE(v) \
-    case v: gemm_kernel<F, NB, RG, v, AM, NL, AQ><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, ldd, cps, pl.pf16, cb); break;
+    case v: gemm_kernel<F, NB, RG, v, AM, NL, AQ><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, ldd, cps, pl.pf16); break;
     switch (abl) {
     GQ_ABL_CASE(1) GQ_ABL_CASE(6) GQ_ABL_CASE(8) GQ_ABL_CASE(15) GQ_ABL_CASE(16) GQ_ABL_CASE(31) GQ_ABL_CASE(32)
     GQ_ABL_CASE(33) GQ_ABL_CASE(2) GQ_ABL_CASE(4) GQ_ABL_CASE(64) GQ_ABL_CASE(68) GQ_ABL_CASE(96) GQ_ABL_CASE(128) GQ_ABL_CASE(134)
-    default: gemm_kernel<F, NB, RG, 0, AM, NL, AQ><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, ldd, cps, pl.pf16, cb); break;
+    default: gemm_kernel<F, NB, RG, 0, AM, NL, AQ><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, ldd, cps, pl.pf16); break;
     }
 #undef GQ_ABL_CASE
 #else
-    gemm_kernel<F, NB, RG, 0, AM, NL, AQ><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, ldd, cps, pl.pf16, cb);
+    gemm_kernel<F, NB, RG, 0, AM, NL, AQ><<<grid, dim3(G::THREADS), 0, s>>>(A, X, x.xd, C, PP, M, N, K, ldc, ldd, cps, pl.pf16);
 #endif
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess || pl.splits == 1 || fused) return e;
+    if (e != hipSuccess || pl.splits == 1) return e;
     if (pl.pf16) {
         const int64_t nq = (int64_t)grid.x * grid.y * (NWAVE * RG * NB * 64);
         gemm_reduce_f16_kernel<NB, RG><<<dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s>>>(
@@ -998,9 +871,9 @@ bool gemm_aq_ok(const GemmPlan &p)
     // splits of at most two super-blocks: the quantization (a few passes of the loader waves)
     // then hides under the first weight stage; longer splits measured neutral to 2% slower
     // (Q4_K 4096x11008 x16), shorter ones 4-9% faster (profiles/r02/gemm_aq_ab.txt)
-    // 64-token tiles (GQ_GEMM_AQ_NB4=1) measured 11-14% slower: the loader waves' quantization
+    // 64-token tiles measured 11-14% slower: the loader waves' quantization
     // (32 blocks per lane) no longer hides under the first weight stage
-    const int max_nb = tuning().gemm_aq_nb4 ? 4 : 2;
+    constexpr int max_nb = 2;
     return p.act == AF_F16 && p.loaders == 4 && p.rg == R1 && p.nb <= max_nb && p.chunks_per_split <= 2 &&
            4 * p.chunks_per_split <= aq_sub_of(p.nb);
 }
@@ -1047,14 +920,6 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, int act)
     // (Q8_0 4096^2 x128 step 23.2 -> 22.1 us; profiles/r02/pf16_step.txt)
     p.pf16 = 1;
     if (tuning().gemm_partial_f32) p.pf16 = 0;
-    // GQ_GEMM_FUSED_REDUCE=1: fp16 partials summed inside the GEMM by the last wave to arrive
-    // at each (tile, wave) row group, no reduce launch.  Bit-identical, but slower on every
-    // shape measured (Q8_0 4096^2 x128 20.5 -> 24.9 us, Q4_K 11008x4096 x128 37.3 -> 41.6;
-    // profiles/r02/fused_reduce_ab_rejected.txt): the hand-over has to go through memory with
-    // agent-scope stores and loads (cache-wide write-back/invalidate fences instead: 3x slower),
-    // where the separate launch finds the partials in its XCD's L2.  Off by default.
-    p.fused_reduce = 0;
-    p.fused_reduce = p.pf16 && tuning().gemm_fused_reduce;
     // blocked partials: S x (tiles) x 128 rows x 16*nb tokens (padded tiles)
     p.partial_bytes = S > 1 ? (size_t)S * tiles * bm * 16 * p.nb * (p.pf16 ? 2 : sizeof(float)) : 0;
     if (S > 1 && p.pf16) p.partial_bytes += (size_t)S * tiles * NWAVE * sizeof(int); // the per-wave e's

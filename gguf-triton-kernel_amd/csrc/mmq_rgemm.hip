@@ -32,8 +32,7 @@ namespace {
 
 // diagnostic ablation builds only (make rabl RABL=n; never the product): 1 = no weight DMA,
 // 2 = no activation load, 4 = no multiply (fragments + MFMA; the streaming kernels too),
-// 8 = no epilogue stores, 16 = the streaming kernel's weight stages read as contiguous runs of
-// the tile's rows (same bytes per stage, wrong values: the access pattern's cost alone)
+// 8 = no epilogue stores
 #ifndef GQ_RGEMM_ABL
 #define GQ_RGEMM_ABL 0
 #endif
@@ -149,28 +148,6 @@ __device__ __forceinline__ TileId grid_tile()
 {
     return TileId{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y, (int)gridDim.z};
 }
-// XCD-aware order (GQ_RGEMM_XCD / GQ_SGEMM_XCD): the hardware deals workgroups out to the 8 XCDs
-// round-robin by linear id, each XCD with its own L2.  xpol 0 keeps blockIdx; otherwise the
-// workgroups one XCD receives take consecutive ids w of a bijective remap (blocks of ceil or floor
-// nwg/8), decomposed 1: split fastest -- a row tile's super-blocks on one XCD, so the 128-byte
-// lines two neighbouring super-blocks of a row share (144 / 210 / 272-byte rows are not
-// line-aligned) are fetched into one L2, not two; 2: row tile fastest -- one split's K range
-// on one XCD, so each XCD reads its slice of the activations instead of all of them.
-__device__ __forceinline__ TileId xcd_tile(int xpol)
-{
-    if (xpol == 0) return grid_tile();
-    const int gx = (int)gridDim.x, gy = (int)gridDim.y, gz = (int)gridDim.z, nwg = gx * gy * gz;
-    const int orig = (int)blockIdx.x + gx * ((int)blockIdx.y + gy * (int)blockIdx.z);
-    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
-    const int w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-    if (xpol == 1) {
-        const int t = w / gz;
-        return TileId{t % gx, t / gx, w - t * gz, gx, gy, gz};
-    }
-    const int t = w / gx;
-    return TileId{w - t * gx, t % gy, t / gy, gx, gy, gz};
-}
-
 template <int NB>
 __device__ __forceinline__ void store_tile(const f32x4 (&acc)[RRG][NB], uint16_t *__restrict__ C,
                                            uint16_t *__restrict__ P, int64_t M, int64_t N, int64_t ldc, int spol,
@@ -264,13 +241,13 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[RRG][NB], uint16_t
 template <int F, int NB, int AQ>
 __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
                                                        int64_t ldx, uint16_t *__restrict__ C, uint16_t *__restrict__ P,
-                                                       int64_t M, int64_t N, int64_t K, int64_t ldc, int spol, int xpol)
+                                                       int64_t M, int64_t N, int64_t K, int64_t ldc, int spol)
 {
     using G = RCfg<F, NB>;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[G::LDS];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const TileId tile = xcd_tile(xpol);
+    const TileId tile = grid_tile();
     const int64_t m0 = (int64_t)tile.x * RBM, n0 = (int64_t)tile.y * G::BN, sb = tile.z;
     const int64_t row_bytes = (K / Layout<F>::QK) * Layout<F>::BYTES;
     uint8_t *const ximg = lds + G::X_OFF;
@@ -414,8 +391,7 @@ struct SParts {
     int64_t N;
     int spol;
     int streamk, U, W; // stream-K: U units over W workgroups, workgroup w = units [wU/W, (w+1)U/W)
-    int pair;          // GQ_SGEMM_PAIR (sgemm_body)
-    int full;          // bit 0: GQ_SGEMM_FULL (Q4_K, NB <= 2: sgemm_full_body); bit 1: GQ_SGEMM_WRING (NB 1)
+    int full;          // GQ_SGEMM_FULL (Q4_K, NB <= 2: sgemm_full_body)
     SPart p[kMaxSParts];
 };
 struct RPart {
@@ -440,7 +416,7 @@ template <int F, int NB>
 __device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
                                            uint16_t *__restrict__ C, uint16_t *__restrict__ P, int64_t M, int64_t N,
                                            int64_t K, int64_t ldc, int spol, const TileId &id, int64_t sb0, int64_t sb1,
-                                           uint8_t *lds, int pair)
+                                           uint8_t *lds)
 {
     using G = SCfg<F, NB>;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -462,25 +438,8 @@ __device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const 
             const int k = wave + RW * i, p = 64 * k + lane, r = p / G::NPH, pc = p - r * G::NPH;
             const bool real = k < G::WH_INSTR;
             const int64_t row = m0 + r < M ? m0 + r : M - 1;
-            uint32_t vo = real ? (uint32_t)(row * row_bytes) + hsrc<F>(h, pc) : 0u, soff = (uint32_t)(G::SB * sb);
-            if constexpr ((ABL & 16) != 0) { // (ablation: the same bytes per stage, read as one contiguous run)
-#ifdef GQ_ABL_RUN // (... or as runs of GQ_ABL_RUN bytes from consecutive rows of the tile)
-                constexpr int64_t RUN = GQ_ABL_RUN;
-                const int64_t byte = 16 * (int64_t)p, c = byte / RUN, o = byte - c * RUN;
-                const int64_t rows_here = M - m0 < RBM ? M - m0 : RBM;
-                const int64_t col = (((2 * sb + h) * RUN) % (row_bytes - RUN + 16)) & ~(int64_t)15;
-                vo = (uint32_t)((m0 + c % rows_here) * row_bytes + col + o);
-#else
-                const int64_t span = (M - m0 < RBM ? M - m0 : RBM) * row_bytes - G::W_BYTES - 16;
-                const int64_t off = ((2 * sb + h) * (int64_t)G::W_BYTES) % (span > 16 ? span : 16);
-                vo = (uint32_t)(m0 * row_bytes + ((off + 16 * (int64_t)p) & ~(int64_t)15));
-#endif
-                soff = 0;
-            }
-            if (pair & 4) // (GQ_SGEMM_NT: the weights non-temporal, as the decode kernel's)
-                dma16<2>(wrs, real ? slot + 1024 * k : lds + G::SCRATCH, vo, soff);
-            else
-                dma16(wrs, real ? slot + 1024 * k : lds + G::SCRATCH, vo, soff); // (+16 lane)
+            const uint32_t vo = real ? (uint32_t)(row * row_bytes) + hsrc<F>(h, pc) : 0u;
+            dma16(wrs, real ? slot + 1024 * k : lds + G::SCRATCH, vo, (uint32_t)(G::SB * sb)); // (+16 lane)
         }
         // activation half image: piece P = 64k + lane: sub-stage ul = P / (BN*8), token r, slot qd
 #pragma unroll
@@ -499,30 +458,13 @@ __device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const 
     for (int rg = 0; rg < RRG; ++rg)
 #pragma unroll
         for (int t = 0; t < NB; ++t) acc[rg][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    // pair (GQ_SGEMM_PAIR, rings of 4+ slots; 2: 3+): a super-block's two half stages are issued
-    // together, so each row's bytes of the super-block are requested at once (one DRAM row
-    // activation, not two a step apart); stage s may be issued once s <= j + NS - 1 at step j
-    const int pm = pair & 3;
-    const bool pr = pm != 0 && G::NS >= (pm == 2 ? 3 : 4);
-    int issued = pr ? ((G::NS - 1) & ~1) : G::NS - 1;
-    issued = issued < nst ? issued : nst;
+    int issued = G::NS - 1 < nst ? G::NS - 1 : nst;
     for (int i = 0; i < issued; ++i) issue(i);
     for (int j = 0; j < nst; ++j) {
         // stage j landed: all but the (<= NS-2) younger stages this wave issued
-        const int younger = issued - 1 - j;
-        vm_wait<(G::NS - 2) * G::NPS>(younger * G::NPS);
+        vm_wait<(G::NS - 2) * G::NPS>((issued - 1 - j) * G::NPS);
         __builtin_amdgcn_s_barrier();
-        // into the slots the stages before j left (barrier passed)
-        if (pr) {
-            if (issued + 1 < nst && issued + 1 <= j + G::NS - 1) {
-                issue(issued);
-                issue(issued + 1);
-                issued += 2;
-            }
-        } else if (issued < nst) {
-            issue(issued);
-            ++issued;
-        }
+        if (issued < nst) issue(issued++); // into the slot stage j-1 left (barrier passed)
         const uint8_t *slot = lds + (j % G::NS) * G::SLOT;
         const int h = j & 1;
         if constexpr ((ABL & 4) != 0) continue; // (ablation builds: no multiply)
@@ -631,128 +573,28 @@ __device__ __forceinline__ void sgemm_full_body(const uint8_t *__restrict__ A, c
     store_tile<NB>(acc, C, P, M, N, ldc, spol, id);
 }
 
-// Q4_K at 16-token tiles with per-wave weight rings (GQ_SGEMM_WRING): the decode kernel's
-// structure with the MFMA multiply.  Each wave streams its own 32 rows' super-blocks (one 144-byte
-// image per row, 4.6 KB per super-block) through a private ring of WR_NS slots and waits only on
-// its own DMA counter -- no workgroup barrier per stage; the x~ of up to WR_XC super-blocks is
-// resident in LDS, reloaded (one barrier) per chunk.  Same fragments and MFMA order per
-// super-block as sgemm_body: the same bits.
-constexpr int WR_NS = 3, WR_XC = 4, WR_SLOT = 5120; // (32 rows x 144 B = 4608, the DMA pad to 5 KiB)
-struct WRing {
-    static constexpr int X_BYTES = WR_XC * 16 * 512, W_OFF = X_BYTES;
-    static constexpr int LDS = X_BYTES + RW * WR_NS * WR_SLOT;
-    static_assert(LDS <= LDS_CAP && (WR_NS - 1) * 5 <= 63, "WRing");
-};
-
-__device__ __forceinline__ void wring_body(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
-                                           uint16_t *__restrict__ C, uint16_t *__restrict__ P, int64_t M, int64_t N,
-                                           int64_t K, int64_t ldc, int spol, const TileId &id, int64_t sb0, int64_t sb1,
-                                           uint8_t *lds)
-{
-    constexpr int BN = 16;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int g = lane >> 4, l16 = lane & 15;
-    const int64_t m0 = (int64_t)id.x * RBM, n0 = (int64_t)id.y * BN;
-    const int64_t row_bytes = (K / 256) * 144;
-    const int nst = (int)(sb1 - sb0);
-    const __amdgpu_buffer_rsrc_t wrs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, (int)(uint32_t)((M * row_bytes + 15) & ~(int64_t)15), 0x00020000);
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, (int)(uint32_t)(N * K * 2), 0x00020000);
-    uint8_t *const ring = lds + WRing::W_OFF + wave * (WR_NS * WR_SLOT);
-    // this wave's 32 rows of super-block j: piece p = 64k + lane -> row p / 9, piece p % 9
-    auto issue_w = [&](int j) __attribute__((always_inline)) {
-        uint8_t *slot = ring + (j % WR_NS) * WR_SLOT;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            const int p = 64 * k + lane, r = p / 9, pc = p - 9 * r;
-            const bool real = p < 32 * 9;
-            const int64_t row = m0 + 32 * wave + r < M ? m0 + 32 * wave + r : M - 1;
-            const uint32_t vo = real ? (uint32_t)(row * row_bytes) + 16u * pc : 0u;
-            dma16(wrs, slot + 1024 * k, vo, (uint32_t)(144 * (sb0 + j))); // (pad lanes: the slot's last 512 B)
-        }
-    };
-    // the x~ of super-blocks [c0, c0 + cn): 8 KiB each, 8 DMA instructions, one per wave
-    auto issue_x = [&](int c0, int cn) __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < WR_XC; ++i) {
-            if (i >= cn) break;
-            const int pp = 64 * wave + lane; // piece of the super-block's 8 KiB image
-            const int u = pp / (BN * 8), r = (pp / 8) % BN, qd = pp & 7, q = qd ^ act_swz(r);
-            const int64_t tok = n0 + r < N ? n0 + r : N - 1;
-            const uint32_t vo = (uint32_t)(tok * K * 2) + 2u * (uint32_t)sub_elem<Q4_K>(u, q);
-            dma16(xrs, lds + i * (BN * 512) + 1024 * wave, vo, (uint32_t)(512 * (sb0 + c0 + i)));
-        }
-    };
-    f32x4 acc[RRG][1];
-#pragma unroll
-    for (int rg = 0; rg < RRG; ++rg) acc[rg][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    int issued = 0;
-    for (int c0 = 0; c0 < nst; c0 += WR_XC) {
-        const int cn = nst - c0 < WR_XC ? nst - c0 : WR_XC;
-        if (c0 > 0) __builtin_amdgcn_s_barrier(); // every wave is done with the previous chunk's x~
-        issue_x(c0, cn);
-        while (issued < nst && issued < c0 + WR_NS - 1) issue_w(issued++); // (the first chunk's prologue)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier(); // the chunk's x~ landed for every wave
-        for (int j = c0; j < c0 + cn; ++j) {
-            vm_wait<(WR_NS - 2) * 5>((issued - 1 - j) * 5); // super-block j of this wave landed
-            if (issued < nst) issue_w(issued++);             // into the slot super-block j-1 left
-            const uint8_t *slot = ring + (j % WR_NS) * WR_SLOT;
-            if constexpr ((ABL & 4) != 0) continue;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint8_t *xs = lds + (j - c0) * (BN * 512) + u * (BN * 128);
-                f16x8 af[RRG][2];
-#pragma unroll
-                for (int rg = 0; rg < RRG; ++rg) {
-                    const uint8_t *wr = slot + 144 * (16 * rg + l16);
-                    q4k_frags(wr, wr + 16 + 32 * u, g, u, af[rg]);
-                }
-#pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    const f16x8 bk = *(const f16x8 *)(xs + 128 * l16 + 16 * ((4 * s + g) ^ act_swz(l16)));
-#pragma unroll
-                    for (int rg = 0; rg < RRG; ++rg)
-                        acc[rg][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[rg][s], bk, acc[rg][0], 0, 0, 0);
-                }
-            }
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    store_tile<1>(acc, C, P, M, N, ldc, spol, id);
-}
-
 template <int F, int NB> constexpr int sgemm_lds()
 {
-    if constexpr (F == Q4_K && NB <= 2) {
-        constexpr int a = SCfg<F, NB>::LDS > SFull<NB>::LDS ? SCfg<F, NB>::LDS : SFull<NB>::LDS;
-        return NB == 1 && WRing::LDS > a ? WRing::LDS : a;
-    }
+    if constexpr (F == Q4_K && NB <= 2) return SCfg<F, NB>::LDS > SFull<NB>::LDS ? SCfg<F, NB>::LDS : SFull<NB>::LDS;
     return SCfg<F, NB>::LDS;
 }
 
 template <int F, int NB>
 __global__ __launch_bounds__(64 * RW) void sgemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
                                                        uint16_t *__restrict__ C, uint16_t *__restrict__ P, int64_t M,
-                                                       int64_t N, int64_t K, int64_t ldc, int spol, int xpol, int pair,
-                                                       int full)
+                                                       int64_t N, int64_t K, int64_t ldc, int spol, int full)
 {
     __shared__ __attribute__((aligned(1024))) uint8_t lds[sgemm_lds<F, NB>()];
     // split z: super-blocks [z*nsb/S, (z+1)*nsb/S) (split lengths differ by one when S does not divide)
-    const TileId id = xcd_tile(xpol);
+    const TileId id = grid_tile();
     const int64_t nsb = K / 256, s0 = id.z * nsb / id.gz, s1 = (id.z + 1) * nsb / id.gz;
     if constexpr (F == Q4_K && NB <= 2) {
-        if (NB == 1 && (full & 2)) {
-            wring_body(A, X, C, P, M, N, K, ldc, spol, id, s0, s1, lds);
-            return;
-        }
-        if (full & 1) {
+        if (full) {
             sgemm_full_body<NB>(A, X, C, P, M, N, K, ldc, spol, id, s0, s1, lds);
             return;
         }
     }
-    sgemm_body<F, NB>(A, X, C, P, M, N, K, ldc, spol, id, s0, s1, lds, pair);
+    sgemm_body<F, NB>(A, X, C, P, M, N, K, ldc, spol, id, s0, s1, lds);
 }
 
 // ---- several matrices in one launch (gq_mmq_grouped_prepared): part i = one matrix's
@@ -770,23 +612,17 @@ __global__ __launch_bounds__(64 * RW) void sgemm_grouped_kernel(const SParts a)
     const int b = (int)blockIdx.x;
     auto run = [&](const SPart &q, const TileId &id, int64_t sb0, int64_t sb1) __attribute__((always_inline)) {
         switch (q.fmt) {
-        case Q8_0: sgemm_body<Q8_0, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds, a.pair); return;
+        case Q8_0: sgemm_body<Q8_0, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds); return;
         case Q4_K:
-            if constexpr (NB == 1) {
-                if (a.full & 2) {
-                    wring_body(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds);
-                    return;
-                }
-            }
             if constexpr (NB <= 2) {
-                if (a.full & 1) {
+                if (a.full) {
                     sgemm_full_body<NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds);
                     return;
                 }
             }
-            sgemm_body<Q4_K, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds, a.pair);
+            sgemm_body<Q4_K, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds);
             return;
-        default: sgemm_body<Q6_K, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds, a.pair); return;
+        default: sgemm_body<Q6_K, NB>(q.A, q.X, q.C, q.P, q.M, a.N, q.K, q.ldc, a.spol, id, sb0, sb1, lds); return;
         }
     };
     if (!a.streamk) { // tile-granular splits: workgroup = (part, tile, split)
@@ -902,8 +738,7 @@ hipError_t launch_snb(const uint8_t *A, const uint16_t *X, uint16_t *C, void *P,
 {
     const dim3 grid((unsigned)p.tiles_m, (unsigned)p.tiles_n, (unsigned)p.splits);
     sgemm_kernel<F, NB><<<grid, dim3(64 * RW), 0, s>>>(A, X, C, (uint16_t *)P, M, N, K, ldc, tuning().rgemm_spol,
-                                                        tuning().sgemm_xcd, tuning().sgemm_pair | (tuning().sgemm_nt ? 4 : 0),
-                                                        (tuning().sgemm_full != 0) | (tuning().sgemm_wring ? 2 : 0));
+                                                        tuning().sgemm_full != 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.splits == 1) return e;
     return launch_gemm_reduce_f16(NB, RRG, (const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n, s);
@@ -914,8 +749,7 @@ hipError_t launch_nb(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t 
                      int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
     const dim3 grid((unsigned)p.tiles_m, (unsigned)p.tiles_n, (unsigned)p.splits);
-    rgemm_kernel<F, NB, AQ><<<grid, dim3(64 * RW), 0, s>>>(A, X, ldx, C, (uint16_t *)P, M, N, K, ldc, tuning().rgemm_spol,
-                                                            tuning().rgemm_xcd);
+    rgemm_kernel<F, NB, AQ><<<grid, dim3(64 * RW), 0, s>>>(A, X, ldx, C, (uint16_t *)P, M, N, K, ldc, tuning().rgemm_spol);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.splits == 1) return e;
     return launch_gemm_reduce_f16(NB, RRG, (const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n, s);
@@ -1092,8 +926,7 @@ hipError_t launch_sgemm_grouped(const SGroupItem *items, int n, int64_t N, const
     a.n = n;
     a.N = N;
     a.spol = tuning().rgemm_spol;
-    a.pair = tuning().sgemm_pair | (tuning().sgemm_nt ? 4 : 0);
-    a.full = (tuning().sgemm_full > 0) | (tuning().sgemm_wring ? 2 : 0);
+    a.full = tuning().sgemm_full > 0;
     a.streamk = r.streamk = g.streamk ? 1 : 0;
     a.U = r.U = g.U;
     a.W = r.W = g.blocks;
@@ -1117,166 +950,6 @@ hipError_t launch_sgemm_grouped(const SGroupItem *items, int n, int64_t N, const
     default: return hipErrorInvalidValue;
     }
 #undef GQ_SGG
-}
-
-// ---------------------------------------------------------------------------------------
-// Row-stream GEMM (GQ_RSTREAM, opt-in; Q4_K, 1..16 tokens, prepared x~): long weight runs.  The
-// run-length ablation (profiles/r04/ab19_runlength_layer.txt) streams weights at ~6.8 TB/s in
-// runs of >= 1 KB against ~3.2 in the tile GEMMs' one-super-block-per-row pieces.  A workgroup
-// owns one K chunk of 8 super-blocks (its x~ resident, 64 KB) and streams 32-row groups, each
-// stage 32 rows x 8 super-blocks (32 runs of 1152 bytes) through a 2-slot ring; wave w multiplies
-// super-block w of the group (q4k_frags + 16 MFMA), the waves' fp32 sums are added in LDS and the
-// group's chunk partial stored fp32 at P[chunk][token][row]; rstream_reduce sums the chunks.
-namespace {
-// KSB super-blocks per K chunk (x~ resident: KSB x 8 KiB), NS ring slots of 32 rows x KSB
-// super-blocks; KSB = 8: 1152-byte runs, 2 slots, wave w = super-block w of both 16-row halves;
-// KSB = 4: 576-byte runs, 4 slots, wave w = super-block w & 3 of half w >> 2
-template <int KSB> struct RS {
-    static constexpr int ROWS = 32, RB = KSB * 144, W = ROWS * RB, WI = W / 1024, NW = (WI + RW - 1) / RW;
-    static constexpr int NS = KSB == 8 ? 2 : 4, X = KSB * 16 * 512, RED = RW * 512 * 4;
-    static constexpr int LDS = X + NS * W + RED + 1024;
-    static_assert(LDS <= LDS_CAP && W % 1024 == 0 && (NS - 2) * NW <= 63, "rstream LDS");
-};
-
-template <int KSB>
-__global__ __launch_bounds__(64 * RW) void rstream_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
-                                                         float *__restrict__ P, int64_t M, int64_t N, int64_t K, int wpc)
-{
-    using G = RS<KSB>;
-    __shared__ __attribute__((aligned(1024))) uint8_t lds[G::LDS];
-    uint8_t *const xim = lds, *const ring = lds + G::X;
-    float *const red = (float *)(lds + G::X + G::NS * G::W);
-    uint8_t *const scratch = lds + G::X + G::NS * G::W + G::RED;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int g = lane >> 4, l16 = lane & 15;
-    const int nsb = (int)(K / 256), chunk = (int)blockIdx.x / wpc, part = (int)blockIdx.x % wpc;
-    const int sb0 = KSB * chunk, ksb = nsb - sb0 < KSB ? nsb - sb0 : KSB;
-    const int64_t groups = (M + G::ROWS - 1) / G::ROWS;
-    const int64_t g0 = groups * part / wpc, g1 = groups * (part + 1) / wpc;
-    const int nst = (int)(g1 - g0);
-    const int64_t row_bytes = (int64_t)nsb * 144;
-    const __amdgpu_buffer_rsrc_t wrs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, (int)(uint32_t)((M * row_bytes + 15) & ~(int64_t)15), 0x00020000);
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, (int)(uint32_t)(N * K * 2), 0x00020000);
-    // stage j: rows 32 (g0 + j) + r, image row r at RB r, super-block s at position s ^ (r % KSB)
-    auto issue_w = [&](int j) __attribute__((always_inline)) {
-        uint8_t *slot = ring + (j % G::NS) * G::W;
-#pragma unroll
-        for (int i = 0; i < G::NW; ++i) {
-            const int k = wave + RW * i, p = 64 * k + lane;
-            const bool real = k < G::WI;
-            const int r = p / (9 * KSB), q = p - 9 * KSB * r, sp = q / 9, pc = q - 9 * sp, sbi = sp ^ (r & (KSB - 1));
-            const int64_t row0 = (g0 + j) * G::ROWS + r, row = row0 < M ? row0 : M - 1;
-            const int sbs = sbi < ksb ? sbi : 0;
-            const uint32_t vo = real ? (uint32_t)(row * row_bytes + 144 * (int64_t)(sb0 + sbs)) + 16u * pc : 0u;
-            dma16(wrs, real ? slot + 1024 * k : scratch, vo, 0u);
-        }
-    };
-    if (nst <= 0) return;
-    // the chunk's x~ (8 DMA instructions per super-block; absent super-blocks skipped)
-#pragma unroll
-    for (int i = 0; i < KSB; ++i) {
-        const int k = wave + RW * i, s = k >> 3, pp = 64 * (k & 7) + lane;
-        if (s >= ksb) continue;
-        const int u = pp / 128, r = (pp / 8) % 16, qd = pp & 7, q = qd ^ act_swz(r);
-        const int64_t tok = r < N ? r : N - 1;
-        const uint32_t vo = (uint32_t)(tok * K * 2) + 2u * (uint32_t)(256 * (sb0 + s) + sub_elem<Q4_K>(u, q));
-        dma16(xrs, xim + 8192 * s + 16 * pp, vo, 0u);
-    }
-    int issued = G::NS - 1 < nst ? G::NS - 1 : nst;
-    for (int j = 0; j < issued; ++j) issue_w(j);
-    // this wave's super-block and 16-row halves
-    constexpr int NH = KSB == 8 ? 2 : 1;
-    const int mysb = KSB == 8 ? wave : (wave & 3), h0 = KSB == 8 ? 0 : (wave >> 2);
-    for (int j = 0; j < nst; ++j) {
-        vm_wait<(G::NS - 2) * G::NW>((issued - 1 - j) * G::NW); // stage j (and, at j = 0, the x~)
-        __builtin_amdgcn_s_barrier();
-        if (issued < nst) issue_w(issued++); // into the slot stage j-1 left
-        f32x4 acc[NH];
-#pragma unroll
-        for (int h = 0; h < NH; ++h) acc[h] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        if (mysb < ksb) {
-            const uint8_t *slot = ring + (j % G::NS) * G::W;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint8_t *xs = xim + 8192 * mysb + u * 2048;
-                f16x8 af[NH][2];
-#pragma unroll
-                for (int h = 0; h < NH; ++h) {
-                    const int r = 16 * (h0 + h) + l16;
-                    const uint8_t *wr = slot + G::RB * r + 144 * (mysb ^ (r & (KSB - 1)));
-                    q4k_frags(wr, wr + 16 + 32 * u, g, u, af[h]);
-                }
-#pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    const f16x8 bk = *(const f16x8 *)(xs + 128 * l16 + 16 * ((4 * s + g) ^ act_swz(l16)));
-#pragma unroll
-                    for (int h = 0; h < NH; ++h)
-                        acc[h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[h][s], bk, acc[h], 0, 0, 0);
-                }
-            }
-        }
-        // the waves' sums in LDS (output e = (half, i, lane)), then thread t adds its output's terms
-#pragma unroll
-        for (int h = 0; h < NH; ++h)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) red[wave * 512 + (4 * h + i) * 64 + lane] = acc[h][i];
-        // the sums must have left the LDS queue before another wave reads them: gfx950's compiler
-        // puts no wait in front of a raw s_barrier (round 4's non-identical bits, mode 3)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        {
-            const int t = tid, hh = t >> 8, i = (t >> 6) & 3, ln = t & 63;
-            float v = 0.f;
-            if constexpr (KSB == 8) {
-#pragma unroll
-                for (int w = 0; w < RW; ++w) v += red[w * 512 + t];
-            } else {
-#pragma unroll
-                for (int w = 0; w < 4; ++w) v += red[(4 * hh + w) * 512 + i * 64 + ln];
-            }
-            const int64_t row = (g0 + j) * G::ROWS + 16 * hh + 4 * (ln >> 4) + i, tok = ln & 15;
-            if (row < M && tok < N) P[((int64_t)chunk * N + tok) * M + row] = v;
-        }
-    }
-}
-
-__global__ __launch_bounds__(256) void rstream_reduce_kernel(const float *__restrict__ P, uint16_t *__restrict__ C,
-                                                             int64_t M, int64_t N, int64_t ldc, int chunks)
-{
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= M * N) return;
-    const int64_t tok = i / M, row = i - tok * M;
-    float v = 0.f;
-    for (int c = 0; c < chunks; ++c) v += P[((int64_t)c * N + tok) * M + row];
-    C[tok * ldc + row] = f2h_bits(v);
-}
-int rs_ksb() { return tuning().rstream == 2 ? 4 : 8; }
-} // namespace
-
-size_t rstream_partial_bytes(int64_t M, int64_t N, int64_t K)
-{
-    const int64_t chunks = (K / 256 + rs_ksb() - 1) / rs_ksb();
-    return (size_t)chunks * (size_t)N * (size_t)M * 4;
-}
-
-hipError_t launch_rstream(const uint8_t *A, const uint16_t *X, uint16_t *C, void *partials, int64_t M, int64_t N,
-                          int64_t K, int64_t ldc, hipStream_t s)
-{
-    if (N < 1 || N > 16 || K % 256 != 0 || M < 1) return hipErrorInvalidValue;
-    const int ksb = rs_ksb(), chunks = (int)((K / 256 + ksb - 1) / ksb);
-    const int64_t groups = (M + 31) / 32;
-    int64_t wpc = tuning().rstream_wpc > 0 ? tuning().rstream_wpc : num_cus() / chunks; // (GQ_RSTREAM_WPC: A/B)
-    if (wpc < 1) wpc = 1;
-    if (wpc > groups) wpc = groups;
-    if (ksb == 8) rstream_kernel<8><<<dim3((unsigned)(chunks * wpc)), dim3(64 * RW), 0, s>>>(A, X, (float *)partials, M, N, K, (int)wpc);
-    else rstream_kernel<4><<<dim3((unsigned)(chunks * wpc)), dim3(64 * RW), 0, s>>>(A, X, (float *)partials, M, N, K, (int)wpc);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    rstream_reduce_kernel<<<dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s>>>((const float *)partials, C, M, N,
-                                                                                      ldc, chunks);
-    return hipGetLastError();
 }
 
 hipError_t launch_rgemm(int fmt, int aq, const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, void *partials,

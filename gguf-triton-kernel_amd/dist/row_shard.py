@@ -126,7 +126,7 @@ class RowShardedMMQ:
         token count only); on the GEMM routes (LDS-DMA, weight-register, resident / streaming
         split-K) the split-K factor -- and the route itself -- follow the chunk's row count, so a
         chunk sums K in another order: equal within the GEMM tolerance, bit-identical only with
-        split-K pinned (GQ_GEMM_SPLITS=1 GQ_WGEMM_SPLITS=1 GQ_RGEMM=0, as the GPU tests do)."""
+        split-K pinned (GQ_GEMM_SPLITS=1 GQ_RGEMM=0, as the GPU tests do)."""
         if not dist.is_initialized() and self.world != 1:
             raise RuntimeError("pipelined() needs an initialised process group for world > 1")
         qk, nbytes = BLOCK[self.fmt]

@@ -140,7 +140,7 @@ def reset_tuning():
 
 
 class tuning:
-    """Context manager: `with tuning(GQ_GEMM_SPLITS=8, GQ_WGEMM=0): ...` (values reset on exit)."""
+    """Context manager: `with tuning(GQ_GEMM_SPLITS=8, GQ_RGEMM=0): ...` (values reset on exit)."""
 
     def __init__(self, **kw):
         self.kw = kw

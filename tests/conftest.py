@@ -36,7 +36,7 @@ def golden():
 
 @pytest.fixture
 def tune():
-    """tune(GQ_GEMM_SPLITS=8, GQ_WGEMM=0, ...): override the library's tuning defaults for this
+    """tune(GQ_GEMM_SPLITS=8, GQ_RGEMM=0, ...): override the library's tuning defaults for this
     test (gq_debug_set_tuning; the library reads GQ_* from the environment once, so setting
     os.environ in a test has no effect); everything is reset after the test."""
     import kernels._lib as kl

@@ -68,7 +68,7 @@ def test_grouped_gemm_bit_identical_to_per_matrix(N, splits, tune):
     assert outs is not None, kl.lib().gq_last_error()
     torch.cuda.synchronize()
     if splits == 1:
-        tune(GQ_SGEMM=0, GQ_RGEMM=0, GQ_WGEMM=0, GQ_SKINNY=0, GQ_GEMM_SPLITS=1)
+        tune(GQ_SGEMM=0, GQ_RGEMM=0, GQ_SKINNY=0, GQ_GEMM_SPLITS=1)
     else:
         tune(GQ_SGEMM=1, GQ_RGEMM=0, GQ_SKINNY=0, GQ_SGEMM_SPLITS=splits)
     for (t, A, _, M, K, _), n, C, B in zip(items, names, outs, inputs):
@@ -248,13 +248,11 @@ def test_single_matrix_stream_k(fmt, M, K, N, tune):
 
 
 @pytest.mark.parametrize("N", [8, 20, 40, 128])
-@pytest.mark.parametrize("knob,pair", [("GQ_SGEMM_PAIR", 1), ("GQ_SGEMM_PAIR", 2), ("GQ_SGEMM_FULL", 1),
-                                       ("GQ_SGEMM_WRING", 1)])
+@pytest.mark.parametrize("knob,pair", [("GQ_SGEMM_FULL", 1)])
 def test_stage_schedule_same_bits(N, knob, pair, tune):
-    """GQ_SGEMM_PAIR (a super-block's two half stages issued together) and GQ_SGEMM_FULL (Q4_K
-    16/32-token tiles streaming whole super-blocks as one 144-byte image per row) change when and
-    how bytes are requested, not what is computed: the grouped layer and a single streaming-GEMM
-    call give the bits of the one-half-stage-at-a-time schedule."""
+    """GQ_SGEMM_FULL (Q4_K 16/32-token tiles streaming whole super-blocks as one 144-byte image
+    per row) changes how bytes are requested, not what is computed: the grouped layer and a
+    single streaming-GEMM call give the bits of the half-stage schedule."""
     import kernels._lib as kl
     types, raw, x, h, items, names, inputs = _layer_items(kl, N, layer=0, seed=N + pair)
     ref = kl.mmq_grouped_prepared(items, N)
@@ -266,7 +264,7 @@ def test_stage_schedule_same_bits(N, knob, pair, tune):
     torch.cuda.synchronize()
     for n, a, b in zip(names, ref, got):
         assert torch.equal(a.view(torch.int16), b.view(torch.int16)), n
-    one = "ffn_down" if knob == "GQ_SGEMM_PAIR" else "ffn_up"  # (a Q6_K / a Q4_K projection)
+    one = "ffn_up"  # (a Q4_K projection)
     t, A, _, M, K, _ = items[names.index(one)]
     B = inputs[names.index(one)]
     outs = []

@@ -220,7 +220,7 @@ def test_baseline_configs_full_size(fmt, M, K, Ns):
         #     (split-K off for both: the split factor is chosen per shape and changes the fp32
         #     summation order of the MFMA path)
         import kernels._lib as kl
-        with kl.tuning(GQ_GEMM_SPLITS=1, GQ_WGEMM_SPLITS=1):
+        with kl.tuning(GQ_GEMM_SPLITS=1):
             Cf = _fn(fmt)(A_t, B_t, M, N, K)
             sub_t = torch.from_numpy(sub.view(np.int8)).to(dev)
             Cs = _fn(fmt)(sub_t, B_t, len(rows), N, K)
@@ -291,7 +291,7 @@ def test_gemm_256_row_tiles(fmt, tune):
     """Two 16-row groups per wave (256-row tiles) of the LDS-DMA GEMM, with and without split-K,
     ragged edges (Q6_K: the 224-B pair-swizzled row image, mmq_gemm.hip Cfg::Q6S); without
     split-K the same bits as 128-row tiles (a row's MFMA chain does not depend on the tile)."""
-    tune(GQ_GEMM_RG=2, GQ_WGEMM=0)
+    tune(GQ_GEMM_RG=2)
     for M, N, K, splits in ((600, 100, 1024, None), (300, 128, 2048, "4"), (8200, 128, 768, "3"), (530, 97, 1536, "1")):
         if splits:
             tune(GQ_GEMM_SPLITS=splits)

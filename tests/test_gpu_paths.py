@@ -44,7 +44,7 @@ def _run(fmt, qA, B, M, N, K):
                                           (64, 64, 1024, None), (300, 100, 2048, "3"), (256, 128, 4096, None),
                                           (96, 128, 4096, "8"), (1000, 77, 1280, None)])
 def test_q8_0_int8_mfma_gemm(M, N, K, splits, tune):
-    tune(GQ_GEMM_I8=1, GQ_WGEMM=0)  # (the int8 form lives in the LDS-DMA GEMM)
+    tune(GQ_GEMM_I8=1)  # (the int8 form lives in the LDS-DMA GEMM)
     if splits:
         tune(GQ_GEMM_SPLITS=splits)
     qA = random_blocks("q8_0", M, K, seed=M + 3 * N)
@@ -63,7 +63,7 @@ def test_q8_0_int8_mfma_full_size(M, N, K, tune):
     token, 48 sampled rows against the oracle (IDEAL at the tight int8 gate, EXACT at the
     reference's 1%)."""
     from kernels._lib import TYPES, mmq
-    tune(GQ_GEMM_I8=1, GQ_WGEMM=0)
+    tune(GQ_GEMM_I8=1)
     dev = _dev()
     qA = random_blocks("q8_0", M, K, seed=M + K)
     B = random_activations(N, K, seed=N + 11)
@@ -81,7 +81,7 @@ def test_q8_0_int8_mfma_full_size(M, N, K, tune):
 
 def test_q8_0_int8_mfma_golden(golden, tune):
     """Every golden case of the reference through the int8 form (cases with N >= 5 run it)."""
-    tune(GQ_GEMM_I8=1, GQ_WGEMM=0)
+    tune(GQ_GEMM_I8=1)
     for c in golden["q8_0"]:
         got = _run("q8_0", c["qA"], c["B"], c["M"], c["N"], c["K"])
         if c["kind"] != "tiny":
@@ -121,7 +121,7 @@ def test_row_sharded_q6_k_70b(M, K, G, N, tune):
     on sampled rows."""
     from dist.row_shard import RowShardedMMQ, shard_bytes
     from kernels._lib import TYPES, mmq
-    tune(GQ_GEMM_SPLITS=1, GQ_WGEMM_SPLITS=1)
+    tune(GQ_GEMM_SPLITS=1)
     dev = _dev()
     qA = random_blocks("q6_k", M, K, seed=M + G)
     B = random_activations(N, K, seed=N + K)
@@ -159,7 +159,7 @@ def test_gemm_chunked_launches_bit_exact(fmt, tune):
     B = random_activations(N, K, seed=10)
     A_t = torch.from_numpy(qA.view(np.int8)).to(dev)
     B_t = torch.from_numpy(B).to(dev)
-    tune(GQ_GEMM_SPLITS=1, GQ_WGEMM_SPLITS=1, GQ_BLAS_MIN_TOKENS=0)
+    tune(GQ_GEMM_SPLITS=1, GQ_BLAS_MIN_TOKENS=0)
     one = mmq(TYPES[fmt], A_t, B_t, M, N, K)
     tune(GQ_GEMM_MAX_BYTES=256 * 1024)  # 256 rows / 128 tokens per launch
     many = mmq(TYPES[fmt], A_t, B_t, M, N, K)
@@ -200,7 +200,7 @@ def test_split_k_partials_huge_cancelling_sums(partial, tune):
     of K repeats the first half's weights against negated activations.  fp16 partials carry a
     per-wave power-of-two scale, so neither form overflows (no inf/NaN) and both cancel."""
     from kernels._lib import TYPES, mmq
-    tune(GQ_GEMM_PARTIAL=int(partial == "f32"), GQ_GEMM_SPLITS=8, GQ_WGEMM=0)
+    tune(GQ_GEMM_PARTIAL=int(partial == "f32"), GQ_GEMM_SPLITS=8)
     dev = _dev()
     M, N, K = 256, 128, 4096
     half = random_blocks("q8_0", M, K // 2, seed=31).reshape(M, -1)
@@ -277,39 +277,6 @@ def test_gemm_in_kernel_quantization_bit_identical(fmt, M, N, K, tune):
     assert O.max_rel_err(fused.cpu().numpy(), ideal) <= TIGHT_GEMM
 
 
-@pytest.mark.parametrize("fmt", ("q8_0", "q4_k", "q6_k"))
-@pytest.mark.parametrize("M,N,K,splits", [(4096, 128, 4096, None), (300, 100, 2048, "3"), (1000, 77, 1280, "5"),
-                                          (8192, 128, 2048, "2"), (520, 17, 4096, "11"), (256, 5, 4096, "16"),
-                                          (384, 40, 3072, "12")])
-def test_fused_split_k_reduce_bit_identical(fmt, M, N, K, splits, tune):
-    """Split-K partials summed inside the GEMM by each row group's last-arriving wave
-    (GQ_GEMM_FUSED_REDUCE=1, mmq_gemm.hip GemmPlan::fused_reduce; measured slower, so opt-in)
-    give the same bits as the separate
-    gemm_reduce_f16_kernel launch, call after call (the arrival counters reset themselves),
-    and match the oracle.  Covers every tile width, 128- and 256-row tiles (Q4_K at 8192 rows),
-    split counts that are not multiples of 8, ragged M/N."""
-    from kernels._lib import TYPES, mmq
-    dev = _dev()
-    tune(GQ_WGEMM=0, GQ_RGEMM=0, GQ_SGEMM=0)  # (the fused reduce belongs to the LDS-DMA GEMM)
-    if splits:
-        tune(GQ_GEMM_SPLITS=splits)
-    qA = random_blocks(fmt, M, K, seed=M + 7 * N)
-    B = random_activations(N, K, seed=K + 5 * N)
-    A_t = torch.from_numpy(qA.view(np.int8)).to(dev)
-    B_t = torch.from_numpy(B).to(dev)
-    tune(GQ_GEMM_FUSED_REDUCE=1)
-    fused = [mmq(TYPES[fmt], A_t, B_t, M, N, K) for _ in range(3)]
-    tune(GQ_GEMM_FUSED_REDUCE=0)
-    staged = mmq(TYPES[fmt], A_t, B_t, M, N, K)
-    torch.cuda.synchronize()
-    for f in fused:
-        assert torch.equal(f.view(torch.int16), staged.view(torch.int16))
-    rows = np.arange(0, M, max(1, M // 256))
-    sub = qA.reshape(M, -1)[rows].reshape(-1)
-    ideal = O.mmq_from_fp16(fmt, sub, B, len(rows), N, K, O.IDEAL)
-    assert O.max_rel_err(fused[0].cpu().numpy()[:, rows], ideal) <= TIGHT_GEMM
-
-
 @pytest.mark.parametrize("W,N,R,M,pad", [(2, 5, 64, 100, 0), (8, 128, 3584, 28672, 0), (4, 3, 64, 250, 7),
                                          (3, 17, 128, 384, 0), (8, 1, 1024, 8192, 0)])
 def test_assemble_shards_kernel(W, N, R, M, pad):
@@ -333,7 +300,7 @@ def test_row_sharded_pipelined_world1(fmt, M, N, K, chunks, tune):
     does not change the arithmetic then)."""
     from dist.row_shard import RowShardedMMQ
     from kernels._lib import TYPES, mmq
-    tune(GQ_GEMM_SPLITS=1, GQ_WGEMM_SPLITS=1)
+    tune(GQ_GEMM_SPLITS=1)
     dev = _dev()
     qA = random_blocks(fmt, M, K, seed=M + 3)
     A_t = torch.from_numpy(qA.view(np.int8)).to(dev)

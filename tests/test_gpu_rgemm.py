@@ -94,7 +94,7 @@ def test_rgemm_one_superblock_bit_identical_to_gemm(fmt, N, tune):
     A_t, B_t = _t(qA.view(np.int8)), _t(B)
     tune(GQ_RGEMM=1, GQ_SKINNY=0)  # (Q4_K / Q8_0 at 16 tokens would take the skinny kernel)
     C1 = _prepared(fmt, A_t, B_t, M, N, K)
-    tune(GQ_RGEMM=0, GQ_WGEMM=0, GQ_GEMM_SPLITS=1)
+    tune(GQ_RGEMM=0, GQ_GEMM_SPLITS=1)
     C0 = _prepared(fmt, A_t, B_t, M, N, K)
     assert torch.equal(C0.view(torch.int16), C1.view(torch.int16))
 
@@ -153,83 +153,6 @@ def test_sgemm_bit_identities(fmt, tune):
     assert torch.equal(Cr.view(torch.int16), Cs.view(torch.int16))
     tune(GQ_SGEMM_SPLITS=1)
     C1 = _prepared(fmt, A_t, B_t, M, N, K)
-    tune(GQ_SGEMM=0, GQ_WGEMM=0, GQ_GEMM_SPLITS=1)
+    tune(GQ_SGEMM=0, GQ_GEMM_SPLITS=1)
     C0 = _prepared(fmt, A_t, B_t, M, N, K)
     assert torch.equal(C0.view(torch.int16), C1.view(torch.int16))
-
-
-@pytest.mark.parametrize("fmt", FMTS)
-@pytest.mark.parametrize("M,N,K,route", [(11008, 16, 4096, "rgemm"), (300, 70, 2816, "rgemm"), (4096, 128, 11008, "sgemm"),
-                                         (777, 20, 3072, "sgemm"), (100, 5, 256, "rgemm")])
-def test_xcd_order_same_bits(fmt, M, N, K, route, tune):
-    """The XCD-aware workgroup orders (GQ_RGEMM_XCD / GQ_SGEMM_XCD = 1: a tile's splits on one XCD,
-    2: a split's row tiles) move work between XCDs only: every (tile, split) is computed once,
-    with the same partial slot and reduce order, so the bits equal blockIdx order's -- odd grid
-    sizes included (the remap's uneven blocks)."""
-    import kernels._lib as kl
-    qA = random_blocks(fmt, M, K, seed=M + K)
-    B = random_activations(N, K, seed=N + K)
-    A_t, B_t = _t(qA.view(np.int8)), _t(B)
-    knob = "GQ_RGEMM_XCD" if route == "rgemm" else "GQ_SGEMM_XCD"
-    pin = dict(GQ_RGEMM=1, GQ_SKINNY=0) if route == "rgemm" else dict(GQ_RGEMM=0, GQ_SKINNY=0, GQ_SGEMM=1)
-    outs = []
-    for pol in (0, 1, 2):
-        tune(**pin, **{knob: pol})
-        name = kl.route_name(kl.TYPES[fmt], M, N, K)
-        assert name.startswith(route + "_kernel"), name
-        outs.append(_mmq(fmt, A_t, B_t, M, N, K))
-    assert torch.equal(outs[1].view(torch.int16), outs[0].view(torch.int16))
-    assert torch.equal(outs[2].view(torch.int16), outs[0].view(torch.int16))
-    rows = np.sort(np.random.default_rng(M).choice(M, size=min(M, 16), replace=False))
-    rb = qA.size // M
-    sub = np.concatenate([qA[r * rb:(r + 1) * rb] for r in rows])
-    got = outs[1].cpu().numpy()[:, rows]
-    assert O.max_rel_err(got, O.mmq_from_fp16(fmt, sub, B, len(rows), N, K, O.IDEAL)) <= TIGHT
-
-
-@pytest.mark.parametrize("M,N,K", [(11008, 16, 4096), (4096, 8, 11008), (300, 5, 2816), (31, 6, 256), (1000, 16, 768),
-                                   (97, 13, 2304)])
-@pytest.mark.parametrize("mode", [1, 2])
-def test_rstream_parity(M, N, K, mode, tune):
-    """The row-stream GEMM (GQ_RSTREAM=1, opt-in: Q4_K at 1..16 tokens, 32-row groups x 8 super-blocks
-    per stage, chunk partials summed by rstream_reduce) against the oracle -- ragged rows and
-    tokens, a short last K chunk (K = 11008: 43 super-blocks), fewer rows than one group -- and
-    within the GEMM tolerance of the default route, through gq_mmq_ex and the prepared call."""
-    import kernels._lib as kl
-    qA = random_blocks("q4_k", M, K, seed=M + K + N)
-    B = random_activations(N, K, seed=N + 7 * K)
-    A_t, B_t = _t(qA.view(np.int8)), _t(B)
-    ref = _mmq("q4_k", A_t, B_t, M, N, K).cpu().numpy()
-    tune(GQ_RSTREAM=mode)  # (1: 8-super-block chunks, 2-slot ring; 2: 4-super-block chunks, 4 slots)
-    assert kl.route_name(kl.GQ_Q4_K, M, N, K).startswith("rstream_kernel")
-    assert kl.route_name(kl.GQ_Q4_K, M, N, K, prepared=True).startswith("rstream_kernel")
-    got = _mmq("q4_k", A_t, B_t, M, N, K).cpu().numpy()
-    gotp = _prepared("q4_k", A_t, B_t, M, N, K).cpu().numpy()
-    assert np.isfinite(got.astype(np.float32)).all()
-    assert np.array_equal(got.view(np.int16), gotp.view(np.int16))
-    assert O.max_rel_err(got, ref) <= TIGHT
-    rows = np.sort(np.random.default_rng(M).choice(M, size=min(M, 24), replace=False))
-    rb = qA.size // M
-    sub = np.concatenate([qA[r * rb:(r + 1) * rb] for r in rows])
-    assert O.max_rel_err(got[:, rows], O.mmq_from_fp16("q4_k", sub, B, len(rows), N, K, O.IDEAL)) <= TIGHT
-    assert O.allclose(O.mmq_from_fp16("q4_k", sub, B, len(rows), N, K, O.EXACT), got[:, rows], 0.01)
-
-
-@pytest.mark.parametrize("mode", [1, 2])
-@pytest.mark.parametrize("M,N,K", [(4096, 8, 11008), (11008, 16, 4096)])
-def test_rstream_repeat_bit_identical(M, N, K, mode, tune):
-    """Round 4's 16-row mode returned different bits from two calls on the same input: its
-    per-wave sums were written to LDS and read by other waves after a raw s_barrier with no
-    `s_waitcnt lgkmcnt(0)` in front (gfx950's compiler inserts none; tools/check_barriers.py
-    lists such barriers from the ISA).  The surviving modes shared that epilogue; with the wait
-    every call must give the same bits -- twelve calls, prepared and not, at K = 11008."""
-    import kernels._lib as kl
-    qA = random_blocks("q4_k", M, K, seed=K + 1)
-    B = random_activations(N, K, seed=N + 2)
-    A_t, B_t = _t(qA.view(np.int8)), _t(B)
-    tune(GQ_RSTREAM=mode)
-    assert kl.route_name(kl.GQ_Q4_K, M, N, K).startswith("rstream_kernel")
-    first = _mmq("q4_k", A_t, B_t, M, N, K)
-    for i in range(12):
-        C = _prepared("q4_k", A_t, B_t, M, N, K) if i % 2 else _mmq("q4_k", A_t, B_t, M, N, K)
-        assert torch.equal(C.view(torch.int16), first.view(torch.int16)), i

@@ -7,8 +7,7 @@
 #   bash tools/gpu.sh pmc CFG...            PMC passes (one rocprofv3 run per counter group, --kernel-trace
 #                                           beside --pmc only) of bench.py --config CFG -> gpurun_out/pmc
 #   bash tools/gpu.sh traffic CFG...        HBM bytes per launch from FETCH_SIZE (tools/pmc_traffic.py)
-#   bash tools/gpu.sh wgemm                 weight-register GEMM: quick parity + A/B timings
-#                                           (VARIANTS / CONFIGS: names in tools/wgemm_check.py)
+#   bash tools/gpu.sh ab ARGS...            tools/ab.py: graph-timed A/B of tuning variants / builds
 #   bash tools/gpu.sh ab SPEC...            interleaved A/B of tools/gemm_tune.py specs (AB_R rounds)
 #   bash tools/gpu.sh dist                  bench.py's N > 1 path at world 1 over RCCL (BENCH_FORCE_DIST)
 #   bash tools/gpu.sh round                 round-end measurements: FETCH_SIZE traffic per config (read by
@@ -52,10 +51,6 @@ pmc)
   python3 "$ROOT/tools/pmc_summary.py" "$OUT" > "$OUT/summary.txt" 2>&1; cat "$OUT/summary.txt" ;;
 traffic)
   timeout -k 10 900 python3 tools/pmc_traffic.py "$@" ;;
-wgemm)
-  timeout -k 10 200 python -u tools/wgemm_check.py --quick --no-time || exit $?
-  timeout -k 10 400 python -u tools/wgemm_check.py --only-time --variants ${VARIANTS:-old,w_rg1_nb8_wd3,w_rg2_nb8} \
-    --configs ${CONFIGS:-q8_0_4096x4096_m128,q4_k_4096x4096_m128,q4_k_11008x4096_m128,q4_k_4096x11008_m128,q6_k_28672x8192_m128} ;;
 ab)
   A=""
   for r in $(seq ${AB_R:-3}); do for s in "$@"; do A="$A $s"; done; done
