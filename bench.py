@@ -338,7 +338,9 @@ def cpu_baseline(fmt, M, K, N, target_s=6.0):
 # (BENCH_REHEARSAL=1: no GPU, gloo, the product's CPU MMQ) runs the same code on a small shape
 STRONG_SHAPE, STRONG_TOKENS = ("q6_k", 28672, 8192), (1, 128)
 WEAK_SHAPE = ("q8_0", 4096, 4096, 128)
-REHEARSAL_STRONG, REHEARSAL_TOKENS, REHEARSAL_WEAK = ("q6_k", 2048, 512), (1, 8), ("q8_0", 256, 512, 8)
+# (the rehearsal keeps the 28672-row geometry -- 14336 / 7168 / 3584-row shards at 2 / 4 / 8 ranks,
+# each cut into 1 / 2 / 4 chunks of whole 64-row tiles -- with one super-block of K)
+REHEARSAL_STRONG, REHEARSAL_TOKENS, REHEARSAL_WEAK = ("q6_k", 28672, 256), (1, 8), ("q8_0", 256, 512, 8)
 
 
 def free_port() -> int:

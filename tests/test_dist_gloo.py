@@ -200,6 +200,31 @@ def test_bench_capture_failure_is_agreed_by_every_rank():
     assert "injected capture failure" in r.stderr
 
 
+def test_bench_gpus8_rehearsal_with_rank5_capture_failure():
+    """The 8-rank path the driver's 8-GPU node will run, rehearsed on the CPU (gloo): `bench.py
+    --gpus 8 --strong` over the Q6_K 28672-row geometry (3584-row shards; K scaled down to one
+    super-block), the 8-way agree_all with a capture failure injected on rank 5 only -- every rank
+    and the 1-GPU reference switch to eager timing -- and the 1 / 2 / 4-chunk dependent-chain
+    pipelines, each with its 8 all_gathers."""
+    r = _run_bench(["--gpus", "8", "--strong", "--steps", "2", "--warmup", "1"],
+                   {"BENCH_REHEARSAL": "1", "BENCH_INJECT_CAPTURE_FAIL": "5", "OMP_NUM_THREADS": "1"}, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["scaling"] == "strong"
+    assert d["config"]["N_out"] == 28672 and d["config"]["rows_per_rank"] == 3584
+    for p in d["strong"]:
+        assert p["ranks"] == 8 and p["rows_per_rank"] == 3584
+        assert set(p["e2e_chain_ms_by_chunks"]) == {"1", "2", "4"}
+        assert all(v > 0 for v in p["e2e_chain_ms_by_chunks"].values())
+        assert "capture failed on some rank" in p["timing"], p["timing"]
+        assert set(p["speedup_vs_1gpu"]) == {"compute", "e2e_overlap", "e2e_chain"}
+    assert "capture failed on some rank" in d["weak"]["timing"]
+    assert d["weak"]["N_out_global"] == 8 * 256
+    assert "injected capture failure (BENCH_INJECT_CAPTURE_FAIL) on rank 5" in r.stderr
+
+
 def test_bench_rotation_touches_a_gib_at_driver_steps():
     """The driver runs `bench.py --steps 20`: every single-GPU config, the Q4_K_M layer and the
     row-sharded shards still cycle over >= 1 GiB of distinct weights (bench.rotation_plan: several
