@@ -199,7 +199,7 @@ hipError_t launch_fmt(const uint8_t *A, const uint16_t *X, uint16_t *C, const FG
 FGemmPlan plan_fgemm(int fmt, int64_t M, int64_t N, int64_t K)
 {
     FGemmPlan p;
-    if (fmt == Q6_K || M < 1 || N < 1 || K < 256 || K % 256 != 0) return p;
+    if (M < 1 || N < 1 || K < 256 || K % 256 != 0) return p;
     // the tile whose grid is closest to whole rounds of the chip, smaller tiles first
     static const int cand[][2] = {{2, 2}, {4, 2}, {4, 4}, {8, 4}};
     const int64_t cus = num_cus();
@@ -228,6 +228,7 @@ hipError_t launch_fgemm(int fmt, const uint8_t *A, const uint16_t *X, uint16_t *
     switch (fmt) {
     case Q8_0: return launch_fmt<Q8_0>(A, X, C, p, M, N, K, ldc, s);
     case Q4_K: return launch_fmt<Q4_K>(A, X, C, p, M, N, K, ldc, s);
+    case Q6_K: return launch_fmt<Q6_K>(A, X, C, p, M, N, K, ldc, s);
     default: return hipErrorInvalidValue;
     }
 }

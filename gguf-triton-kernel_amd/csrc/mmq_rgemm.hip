@@ -66,16 +66,15 @@ template <int F> __device__ __forceinline__ uint32_t hsrc(int h, int pc)
 template <int F, int NB> struct RCfg {
     static constexpr int BN = 16 * NB;
     static constexpr int NPH = HImg<F>::NPH, HRB = 16 * NPH, SB = Layout<F>::BYTES * (256 / Layout<F>::QK);
-    static constexpr int WH_INSTR = (RBM * NPH + 63) / 64; // DMA instructions per half image
-    static constexpr int NWH = (WH_INSTR + RW - 1) / RW;   // per wave and half
-    static constexpr int W1_OFF = RBM * HRB;                // the second half image
-    static constexpr int X_OFF = 2 * RBM * HRB;             // then the activation image
+    // each wave's own 32 rows: [half 0 (32 x HRB)][half 1], moved by its own WWI DMA instructions
+    // (H0I of them hold half 0 -- the last of those may carry the head of half 1)
+    static constexpr int WW = 2 * 32 * HRB, WWI = WW / 1024, H0I = (32 * NPH + 63) / 64;
+    static constexpr int X_OFF = RW * WW;                   // then the activation image
     static constexpr int X_BYTES = BN * 512;                // 4 sub-stages x BN tokens x 128 B
     static constexpr int X_INSTR = X_BYTES / 1024;          // prepared form: DMA instructions
-    static constexpr int NX = (X_INSTR + RW - 1) / RW;
-    static constexpr bool PAD = WH_INSTR % RW != 0 || X_INSTR % RW != 0 || RBM * NPH % 64 != 0;
-    static constexpr int SCRATCH = X_OFF + X_BYTES;         // padding DMAs land here
-    static constexpr int LDS = SCRATCH + (PAD ? 1024 : 0);
+    static constexpr int NX = X_INSTR / RW;
+    static constexpr int LDS = X_OFF + X_BYTES;
+    static_assert(WW % 1024 == 0 && X_INSTR % RW == 0, "whole DMA instructions per wave");
     static_assert(LDS <= LDS_CAP, "LDS budget");
 };
 
@@ -116,15 +115,17 @@ template <int F> __device__ __forceinline__ void half_frags(const uint8_t *img, 
 // order, each wave's values scaled by 2^-e, the e's after all blocks; spol = store cache policy.
 // One sub-stage u (64 K elements) of this wave's 32 rows x every token: the A fragments from the
 // half image wimg (half u >> 1), the B fragments from the sub-stage's activation image xs
+// (rbase: the wave's first row in the image -- 32 * wave in a tile-wide image, 0 in a wave's own)
 template <int F, int NB>
-__device__ __forceinline__ void mul_substage(const uint8_t *wimg, const uint8_t *xs, int u, f32x4 (&acc)[RRG][NB])
+__device__ __forceinline__ void mul_substage(const uint8_t *wimg, const uint8_t *xs, int u, f32x4 (&acc)[RRG][NB],
+                                             int rbase)
 {
-    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
     const int g = lane >> 4, l16 = lane & 15;
     f16x8 af[RRG][2];
 #pragma unroll
     for (int rg = 0; rg < RRG; ++rg)
-        half_frags<F>(wimg + (16 * HImg<F>::NPH) * (16 * (RRG * wave + rg) + l16), g, u, af[rg]);
+        half_frags<F>(wimg + (16 * HImg<F>::NPH) * (rbase + 16 * rg + l16), g, u, af[rg]);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
         f16x8 bk[NB];
@@ -268,21 +269,23 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
         }
     }
 
-    // 2. the weights: half image h, instruction k = wave + 8i moves pieces p = 64k + lane (row p / NPH)
+    // 2. the weights: this wave's own 32 rows, both half images, instruction i moving pieces
+    //    p = 64i + lane of its region (half p / (32 NPH), row, piece) -- only this wave reads them,
+    //    so only its own vmcnt orders them: no workgroup barrier on the weights
     const __amdgpu_buffer_rsrc_t wrs =
         __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, (int)(uint32_t)((M * row_bytes + 15) & ~(int64_t)15), 0x00020000);
-    auto issue_half = [&](int h) __attribute__((always_inline)) {
+    uint8_t *const wimg = lds + wave * G::WW;
+    auto issue_w = [&]() __attribute__((always_inline)) {
         if constexpr (ABL & 1) return;
 #pragma unroll
-        for (int i = 0; i < G::NWH; ++i) {
-            const int k = wave + RW * i, p = 64 * k + lane, r = p / G::NPH, pc = p - r * G::NPH;
-            const bool real = k < G::WH_INSTR && r < RBM;
-            const int64_t row = m0 + r < M ? m0 + r : M - 1;
-            const uint32_t vo = real ? (uint32_t)(row * row_bytes) + hsrc<F>(h, pc) : 0u;
-            dma16(wrs, real ? lds + h * G::W1_OFF + 1024 * k : lds + G::SCRATCH, vo, (uint32_t)(G::SB * sb)); // (+16 lane)
+        for (int i = 0; i < G::WWI; ++i) {
+            const int p = 64 * i + lane, h = p / (32 * G::NPH), rem = p - h * (32 * G::NPH);
+            const int r = rem / G::NPH, pc = rem - r * G::NPH;
+            const int64_t row = m0 + 32 * wave + r < M ? m0 + 32 * wave + r : M - 1;
+            dma16(wrs, wimg + 1024 * i, (uint32_t)(row * row_bytes) + hsrc<F>(h, pc), (uint32_t)(G::SB * sb)); // (+16 lane)
         }
     };
-    // 3. (prepared) the activation image by LDS-DMA between the halves: image piece P = 64k + lane:
+    // 3. (prepared) the activation image by LDS-DMA, ahead of the weights: image piece P = 64k + lane:
     //    sub-stage u = P / (BN*8), token r, slot qd (source-swizzled)
     auto issue_x = [&]() __attribute__((always_inline)) {
         if constexpr (AQ != 0 || (ABL & 2)) return;
@@ -294,12 +297,11 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
             const int u = pp / (G::BN * 8), r = (pp / 8) % G::BN, qd = pp & 7, q = qd ^ act_swz(r);
             const int64_t tok = n0 + r < N ? n0 + r : N - 1;
             const uint32_t vo = (uint32_t)(tok * K * 2) + 2u * (uint32_t)sub_elem<F>(u, q);
-            dma16(xrs, k < G::X_INSTR ? lds + G::X_OFF + 1024 * k : lds + G::SCRATCH, vo, (uint32_t)(512 * sb));
+            dma16(xrs, lds + G::X_OFF + 1024 * k, vo, (uint32_t)(512 * sb));
         }
     };
-    issue_half(0);
     issue_x();
-    issue_half(1);
+    issue_w();
 
     // 4. (AQ) quantize into the image: x~ = fp16(d*q) in act_quant's DEQ order (deq_quad), or the
     //    fp8 variant's F8DEQ x~ (f8_quad) -- the compiler's vmcnt for xv leaves the DMAs in flight
@@ -319,24 +321,25 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
             *(u32x4 *)(ximg + u * (G::BN * 128) + 128 * r + 16 * (q ^ act_swz(r))) = o;
         }
     }
-    // first half (+ the prepared activations) landed: all but this wave's second-half DMAs
-    constexpr int W1N = (ABL & 1) ? 0 : G::NWH;
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(W1N) : "memory");
+    // the activation image complete (every wave's DMAs, or every wave's quantized pieces): this
+    // wave's x loads are older than its weight DMAs, so all but those are awaited
+    constexpr int WN = (ABL & 1) ? 0 : G::WWI;
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(WN) : "memory");
     __builtin_amdgcn_s_barrier();
 
-    // 5. the multiply: rows 16*(2*wave + rg) + [0, 16), every token, 4 sub-stages x 2 k-steps
+    // 5. the multiply: the wave's rows 16*rg + [0, 16), every token, 4 sub-stages x 2 k-steps; the
+    //    first half as soon as this wave's own half-0 DMAs landed
     f32x4 acc[RRG][NB];
 #pragma unroll
     for (int rg = 0; rg < RRG; ++rg)
 #pragma unroll
         for (int t = 0; t < NB; ++t) acc[rg][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    constexpr int H1N = (ABL & 1) ? 0 : G::WWI - G::H0I;
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(H1N) : "memory");
 #pragma unroll
     for (int u = 0; u < 4 && !(ABL & 4); ++u) {
-        if (u == 2) { // the second half
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-        }
-        mul_substage<F, NB>(lds + (u >> 1) * G::W1_OFF, ximg + u * (G::BN * 128), u, acc);
+        if (u == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the second half
+        mul_substage<F, NB>(wimg + (u >> 1) * (32 * G::HRB), ximg + u * (G::BN * 128), u, acc, 0);
     }
     if constexpr ((ABL & 4) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
@@ -470,7 +473,7 @@ __device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const 
         if constexpr ((ABL & 4) != 0) continue; // (ablation builds: no multiply)
 #pragma unroll
         for (int ul = 0; ul < 2; ++ul)
-            mul_substage<F, NB>(slot, slot + G::W_BYTES + ul * (G::BN * 128), 2 * h + ul, acc);
+            mul_substage<F, NB>(slot, slot + G::W_BYTES + ul * (G::BN * 128), 2 * h + ul, acc, 32 * wave);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // (nothing is in flight here; no DMA outlives the workgroup)
     store_tile<NB>(acc, C, P, M, N, ldc, spol, id);

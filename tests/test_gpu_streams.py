@@ -19,7 +19,7 @@ CASES = [
     ("q8_0", 4096, 128, 4096, "rgemm_kernel"),    # the headline: 16 splits + reduce
     ("q4_k", 4096, 16, 4096, "rgemm_kernel"),
     ("q6_k", 11008, 128, 4096, "sgemm_kernel"),   # streaming GEMM, split-K + reduce
-    ("q8_0", 22016, 16, 4096, "skinny_kernel"),
+    ("q4_k", 28672, 16, 8192, "skinny_kernel"),
     ("q6_k", 4096, 1, 4096, "stream_decode_kernel"),
     ("q4_k", 4096, 4, 11008, "gemv_kernel"),
     ("q8_0", 1024, 800, 1024, "dequant_kernel"),  # hipBLASLt (warmed before capture)
