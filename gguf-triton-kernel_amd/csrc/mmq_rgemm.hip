@@ -28,6 +28,18 @@
 #include "gguf_q8_1.hpp"
 
 namespace gq {
+
+#ifdef GQ_RGEMM_STAMPS // diagnostic build: per-wave timeline of rgemm_kernel (never the product)
+// [0] s_memrealtime at entry (100 MHz, chip-wide), [1] s_memtime at entry, then s_memtime at:
+// [2] loads issued, [3] x~ written (AQ), [4] past the activation barrier, [5] own half 0 landed,
+// [6] half 0 multiplied, [7] half 1 landed, [8] multiply done, [9] partial stores issued,
+// [10] stores complete, [11] s_memrealtime at the end; [12] workgroup id, [13] XCC id
+__device__ unsigned long long g_rstamps[65536][14];
+#define GQ_RST(i) (st[i] = __builtin_amdgcn_s_memtime())
+#else
+#define GQ_RST(i) ((void)0)
+#endif
+
 namespace {
 
 // diagnostic ablation builds only (make rabl RABL=n; never the product): 1 = no weight DMA,
@@ -252,6 +264,11 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
     const int64_t m0 = (int64_t)tile.x * RBM, n0 = (int64_t)tile.y * G::BN, sb = tile.z;
     const int64_t row_bytes = (K / Layout<F>::QK) * Layout<F>::BYTES;
     uint8_t *const ximg = lds + G::X_OFF;
+#ifdef GQ_RGEMM_STAMPS
+    unsigned long long st[14] = {};
+    st[0] = __builtin_amdgcn_s_memrealtime();
+    GQ_RST(1);
+#endif
 
     // 1. (AQ) the raw activations into registers first: their loads return ahead of the weight
     //    DMAs in this wave's in-order memory queue, so the quantization overlaps the weights' flight
@@ -302,6 +319,7 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
     };
     issue_x();
     issue_w();
+    GQ_RST(2);
 
     // 4. (AQ) quantize into the image: x~ = fp16(d*q) in act_quant's DEQ order (deq_quad), or the
     //    fp8 variant's F8DEQ x~ (f8_quad) -- the compiler's vmcnt for xv leaves the DMAs in flight
@@ -325,7 +343,9 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
     // wave's x loads are older than its weight DMAs, so all but those are awaited
     constexpr int WN = (ABL & 1) ? 0 : G::WWI;
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(WN) : "memory");
+    GQ_RST(3);
     __builtin_amdgcn_s_barrier();
+    GQ_RST(4);
 
     // 5. the multiply: the wave's rows 16*rg + [0, 16), every token, 4 sub-stages x 2 k-steps; the
     //    first half as soon as this wave's own half-0 DMAs landed
@@ -336,11 +356,26 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
         for (int t = 0; t < NB; ++t) acc[rg][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
     constexpr int H1N = (ABL & 1) ? 0 : G::WWI - G::H0I;
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(H1N) : "memory");
+    GQ_RST(5);
 #pragma unroll
     for (int u = 0; u < 4 && !(ABL & 4); ++u) {
-        if (u == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the second half
+        if (u == 2) { // the second half
+#ifdef GQ_RGEMM_STAMPS
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            for (int rg = 0; rg < RRG; ++rg)
+                for (int t = 0; t < NB; ++t) asm volatile("" ::"v"(acc[rg][t]));
+#endif
+            GQ_RST(6);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            GQ_RST(7);
+        }
         mul_substage<F, NB>(wimg + (u >> 1) * (32 * G::HRB), ximg + u * (G::BN * 128), u, acc, 0);
     }
+#ifdef GQ_RGEMM_STAMPS
+    for (int rg = 0; rg < RRG; ++rg)
+        for (int t = 0; t < NB; ++t) asm volatile("" ::"v"(acc[rg][t]));
+#endif
+    GQ_RST(8);
     if constexpr ((ABL & 4) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     // 6. epilogue
@@ -349,6 +384,20 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
         return;
     }
     store_tile<NB>(acc, C, P, M, N, ldc, spol, tile);
+#ifdef GQ_RGEMM_STAMPS
+    GQ_RST(9);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    GQ_RST(10);
+    st[11] = __builtin_amdgcn_s_memrealtime();
+    const int wg = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+    st[12] = (unsigned long long)wg;
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    st[13] = xcc & 0xfu;
+    const int id = wg * RW + wave;
+    if (lane == 0 && id < 65536)
+        for (int i = 0; i < 14; ++i) g_rstamps[id][i] = st[i];
+#endif
 }
 
 // ---------------------------------------------------------------------------------------
@@ -975,3 +1024,11 @@ hipError_t launch_rgemm(int fmt, int aq, const uint8_t *A, const uint16_t *X, in
 }
 
 } // namespace gq
+
+#ifdef GQ_RGEMM_STAMPS
+extern "C" int gq_debug_rgemm_stamps(void *host, size_t bytes)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(gq::g_rstamps), bytes < sizeof(gq::g_rstamps) ? bytes : sizeof(gq::g_rstamps)) ==
+                   hipSuccess ? 0 : 1;
+}
+#endif
