@@ -40,6 +40,7 @@ struct Tuning {
     int sgemm_full = -1;                      // GQ_SGEMM_FULL: Q4_K 16/32-token tiles stream whole super-blocks:
                                               // 1 every streaming GEMM, 0 none, -1 single matrices (measured gain)
     int fgemm = 0;                            // GQ_FGEMM: full-K tile GEMM 0 off / 1 wherever it applies
+    int kstream = -1;                         // GQ_KSTREAM: K-chunked streaming MMQ -1 auto / 0 off / 1 wherever it applies
     int fgemm_rw = 0;                         // GQ_FGEMM_RW: its row groups of 32 (2/4/8, 0: auto)
     int fgemm_nb = 0;                         // GQ_FGEMM_NB: its 16-token tiles (2/4, 0: auto)
     int cus = 0;                              // GQ_CUS: compute units to plan for (0: the device's count)
@@ -205,6 +206,27 @@ struct DecodeItem {
 };
 bool decode_grouped_ok(const DecodeItem *items, int n, int64_t N, bool fp8 = false);
 hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipStream_t s, bool fp8 = false);
+
+// K-chunked streaming MMQ (mmq_kstream.hip, 5..32 tokens): x~ in VGPRs (each of a workgroup's
+// 8 waves one K chunk), weights streamed per wave through private LDS rings, the waves' tiles
+// summed in LDS: one launch, no partials.  Up to kKMaxParts matrices (own type, activations,
+// output; the same N) in one launch, workgroups apportioned by weight bytes; a matrix's bits do
+// not depend on the launch it is in.  aq: 0 prepared x~ (X = [N][K], ldx = K, act_quant DEQ /
+// F8DEQ), 1 raw fp16 q8_1-quantized in-kernel, 2 raw fp16 with the fp8 variant's quantization.
+// kstream_ok: K % 256 == 0 and short enough for the waves' registers (K <= 4096), M % 16 == 0,
+// < 2 GiB of weights.
+constexpr int kKMaxParts = 16;
+struct KItem {
+    int fmt;
+    const uint8_t *A;
+    const uint16_t *X;
+    int64_t ldx;
+    uint16_t *C;
+    int64_t ldc, M, K;
+};
+int kstream_cw(int64_t N, int64_t K);
+bool kstream_ok(int fmt, int64_t M, int64_t N, int64_t K);
+hipError_t launch_kstream(const KItem *items, int n, int64_t N, int aq, hipStream_t s);
 
 // Skinny-token MMQ (mmq_skinny.hip, 1..32 tokens, K % 256 == 0): 16*rg rows x 16*nb tokens per
 // workgroup, K split over its 8 waves (8/nb ranges x nb token tiles), weights and activations

@@ -107,6 +107,9 @@ bool parse_key(Tuning &t, const char *key, long long v)
     } else if (k == "GQ_FGEMM_NB") {
         if (!in({0, 2, 4})) return false;
         t.fgemm_nb = (int)v;
+    } else if (k == "GQ_KSTREAM") {
+        if (!in({-1, 0, 1})) return false;
+        t.kstream = (int)v;
     } else if (k == "GQ_ABLATE") t.ablate = (int)v;
     else return false;
     return true;
@@ -120,7 +123,7 @@ void tuning_from_env(Tuning &t)
                                        "GQ_GEMM_NB", "GQ_GEMM_RG", "GQ_GEMM_LOADERS", "GQ_GEMM_SPLITS",
                                        "GQ_GEMM_PARTIAL", "GQ_GEMV_CAP", "GQ_GEMV_R", "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D",
                                        "GQ_RGEMM", "GQ_SGEMM", "GQ_SGEMM_SPLITS", "GQ_SGEMM_STREAMK", "GQ_RGEMM_NB", "GQ_RGEMM_SPOL",
-                                       "GQ_SGEMM_FULL", "GQ_FGEMM", "GQ_FGEMM_RW", "GQ_FGEMM_NB", "GQ_CUS",
+                                       "GQ_SGEMM_FULL", "GQ_FGEMM", "GQ_FGEMM_RW", "GQ_FGEMM_NB", "GQ_CUS", "GQ_KSTREAM",
                                        "GQ_ABLATE"};
     for (const char *k : keys) {
         const char *e = getenv(k); // the only getenv of the library: once per process
@@ -313,6 +316,24 @@ bool rgemm_route(int t, int form, int64_t M, int64_t N, int64_t K, int act)
     if (use_fgemm(t, form, M, N, K)) return false;
     if (!use_rgemm(t, form, M, N, K)) return false;
     return gq::tuning().skinny != 1 || !use_skinny(t, form, N, act);
+}
+
+// K-chunked streaming MMQ (mmq_kstream.hip): 5..32 tokens (the fp8 variant from 3: its decode
+// form covers 1..2), K % 256 == 0 within the waves' x~ registers (K <= 8192 at <= 16 tokens,
+// 4096 at 17..32), M % 16 == 0; one launch, no workspace (x~ quantized in-kernel from the raw
+// activations, or read prepared).  GQ_KSTREAM=1: wherever it applies, 0: off.
+bool use_kstream(int t, int form, int64_t M, int64_t N, int64_t K, int act)
+{
+    const int ks = gq::tuning().kstream;
+    if (ks == 0 || form != gq::AF_F16 || use_blas(N, K) || !gq::kstream_ok(t, M, N, K)) return false;
+    if (N < (act == GQ_ACT_FP8_E4M3 ? 3 : 5)) return false;
+    if (ks == 1) return true;
+    return false; // (auto: not yet measured)
+}
+// its 32-bit buffer offsets over the activations (rows ldx apart) and the output (rows ldc apart)
+bool kstream_fits(int64_t M, int64_t N, int64_t K, int64_t ldx, int64_t ldc)
+{
+    return ((N - 1) * ldx + K) * 2 < ((int64_t)1 << 31) && ((N - 1) * ldc + M) * 2 < ((int64_t)1 << 31);
 }
 
 // Streaming 256-row GEMM (mmq_rgemm.hip sgemm_kernel) on the prepared x~, where the resident
@@ -533,7 +554,7 @@ void gq_debug_reset_tuning(void) { gq::reset_tuning(); }
 
 int gq_block_elems(gq_type t) { return block_elems(t); }
 int gq_block_bytes(gq_type t) { return block_bytes(t); }
-int gq_version(void) { return 103; }
+int gq_version(void) { return 104; }
 const char *gq_last_error(void) { return g_err.c_str(); }
 
 size_t gq_mmq_call_workspace_size(gq_type t, gq_act act, int64_t M, int64_t N, int64_t K)
@@ -648,6 +669,12 @@ static int compute(gq_type t, int act, const void *A, void *workspace, size_t wo
         // (the kernel is chosen by the call's token count: every chunk runs the same arithmetic)
         // (<= 32 skinny tokens are never cut: their x~ is far below the guard, and the token
         // count sets the kernel's K split)
+        if (use_kstream(t, r.form, M, N, K, act) && kstream_fits(M, N, K, K, ldc)) {
+            const gq::KItem it{t, (const uint8_t *)A, c.xdeq, K, (uint16_t *)C, ldc, M, K};
+            e = gq::launch_kstream(&it, 1, N, 0, s);
+            if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (kstream): %s", hipGetErrorString(e));
+            return GQ_OK;
+        }
         if (use_fgemm(t, r.form, M, N, K)) {
             e = gq::launch_fgemm(t, (const uint8_t *)A, c.xdeq, (uint16_t *)C, gq::plan_fgemm(t, M, N, K), M, N, K, ldc, s);
             if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (fgemm): %s", hipGetErrorString(e));
@@ -720,6 +747,15 @@ int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int6
         hipError_t e = gq::launch_decode_fused(t, (const uint8_t *)A, (const uint16_t *)B, ldb, (uint16_t *)C, M, N,
                                                K, ldc, (hipStream_t)stream, act == GQ_ACT_FP8_E4M3);
         if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (decode): %s", hipGetErrorString(e));
+        return GQ_OK;
+    }
+    if (use_kstream(t, r.form, M, N, K, act) && ldb % 8 == 0 && ((uintptr_t)B & 15) == 0 &&
+        kstream_fits(M, N, K, ldb, ldc)) {
+        // one launch, no workspace: the activations quantized inside (q8_1, or the fp8 variant's
+        // e4m3), bit-identical to the act_quant forms the prepared call reads
+        const gq::KItem it{t, (const uint8_t *)A, (const uint16_t *)B, ldb, (uint16_t *)C, ldc, M, K};
+        hipError_t e = gq::launch_kstream(&it, 1, N, act == GQ_ACT_FP8_E4M3 ? 2 : 1, (hipStream_t)stream);
+        if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (kstream): %s", hipGetErrorString(e));
         return GQ_OK;
     }
     if (rgemm_route(t, r.form, M, N, K, act) && ldb % 8 == 0 &&
@@ -965,6 +1001,21 @@ int gq_mmq_grouped_ex(gq_act act, const gq_group_item *items, int n, int64_t N, 
                                  it.ldc, it.M, it.K};
     }
     if (m == 0) return GQ_OK;
+    if (N >= (fp8 ? 3 : 5)) {
+        // 5..32 tokens (fp8: 3..32): the K-chunked streaming MMQ, every item in one launch
+        gq::KItem ki[16];
+        for (int i = 0; i < m; ++i) {
+            const gq::DecodeItem &d = di[i];
+            if (!use_kstream(d.fmt, gq::AF_F16, d.M, N, d.K, act) || d.ldx % 8 != 0 || ((uintptr_t)d.X & 15) != 0 ||
+                !kstream_fits(d.M, N, d.K, d.ldx, d.ldc))
+                return fail(GQ_EUNSUPPORTED, "item %d: not a grouped K-chunked-stream shape (N=%lld, M=%lld, K=%lld)", i,
+                            (long long)N, (long long)d.M, (long long)d.K);
+            ki[i] = gq::KItem{d.fmt, d.A, d.X, d.ldx, d.C, d.ldc, d.M, d.K};
+        }
+        hipError_t e = gq::launch_kstream(ki, m, N, fp8 ? 2 : 1, (hipStream_t)stream);
+        if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (grouped kstream): %s", hipGetErrorString(e));
+        return GQ_OK;
+    }
     if (!gq::decode_grouped_ok(di, m, N, fp8))
         return fail(GQ_EUNSUPPORTED, "not a grouped-decode shape (N=%lld; N <= %d and every item a one-launch decode)",
                     (long long)N, fp8 ? 2 : 4);
@@ -1083,6 +1134,7 @@ const char *gq_debug_route(gq_type t, gq_act act, int64_t M, int64_t N, int64_t 
     if (!prepared && fused_decode_route(t, act, N, K)) return "stream_decode_kernel";
     if (r.blas) return "dequant_kernel + hipBLASLt";
     if (r.gemv) return "gemv_kernel";
+    if (use_kstream(t, r.form, M, N, K, act)) return "kstream_kernel";
     if (use_fgemm(t, r.form, M, N, K)) return "fgemm_kernel";
     if (rgemm_route(t, r.form, M, N, K, act)) return "rgemm_kernel + gemm_reduce_f16_kernel";
     if (use_skinny(t, r.form, N, act)) return "skinny_kernel";

@@ -182,17 +182,19 @@ int gq_mmq_sharded(gq_type t, const void *A_shard, const void *B, void *C, int64
                    size_t workspace_bytes, void *stream);
 
 /*
- * Grouped decode: several MMQs of the same token count N (1..4) in one launch, e.g. the
- * projections of one transformer block at decode time.  The reference has no counterpart (its
- * kernels/mmq_*.py take one matrix per call); this is the launch the layer dispatcher
- * (kernels/layer_mix.py) makes at 1..4 tokens.  Item i: weights A (M x K of
- * `type`), fp16 activations B (N x K, row stride ldb, q8_1-quantized in the kernel as gq_mmq
- * does), fp16 output C (N x M, row stride ldc); items may share B.  Every item's output is
- * bit-identical to its own gq_mmq call.  The chip's waves are split over the items by weight
- * bytes.  No workspace, no host sync.  GQ_EUNSUPPORTED (nothing launched) when N > 4, or when an
- * item is not a decode shape for the one-launch kernel (its activations do not fit LDS, or
- * >= 2 GiB of weights), or when the items need more than 16 parts (item x token group):
- * call gq_mmq per item then.
+ * Grouped MMQ: several MMQs of the same token count N (1..32) in one launch, e.g. the
+ * projections of one transformer block at decode / small-batch time.  The reference has no
+ * counterpart (its kernels/mmq_*.py take one matrix per call); this is the launch the layer
+ * dispatcher (kernels/layer_mix.py) makes.  Item i: weights A (M x K of `type`),
+ * fp16 activations B (N x K, row stride ldb, q8_1-quantized in the kernel as gq_mmq does), fp16
+ * output C (N x M, row stride ldc); items may share B.  N = 1..4: the streaming decode kernel,
+ * every item's output bit-identical to its own gq_mmq call; N = 5..32: the K-chunked streaming
+ * MMQ (every item bit-identical to its own gq_mmq_ex on that kernel, GQ_KSTREAM=1), which needs
+ * K % 256 == 0, K <= 8192 (N <= 16) / 4096 (N <= 32), M % 16 == 0, B 16-byte aligned and ldb % 8
+ * == 0.  The chip's workgroups are split over the items by weight bytes.  No workspace, no host
+ * sync.  GQ_EUNSUPPORTED (nothing launched) when N > 32, or an item is not a shape of that
+ * launch (decode: activations that do not fit LDS, >= 2 GiB of weights, more than 16 parts =
+ * item x token group; 5..32: the conditions above, more than 16 items): call gq_mmq per item then.
  */
 typedef struct gq_group_item {
     gq_type type;
@@ -205,8 +207,8 @@ typedef struct gq_group_item {
 } gq_group_item;
 int gq_mmq_grouped(const gq_group_item *items, int n, int64_t N, void *stream);
 /* The same with an activation format: GQ_ACT_Q8_1 is gq_mmq_grouped; GQ_ACT_FP8_E4M3 (the fp8
- * variant, its decode form at N <= 2) gives every item gq_mmq_ex(..., GQ_ACT_FP8_E4M3, ...)'s
- * bits and is GQ_EUNSUPPORTED (nothing launched) from N = 3. */
+ * variant: its decode form at N <= 2, the K-chunked stream at 3..32) gives every item
+ * gq_mmq_ex(..., GQ_ACT_FP8_E4M3, ...)'s bits on that kernel. */
 int gq_mmq_grouped_ex(gq_act act, const gq_group_item *items, int n, int64_t N, void *stream);
 
 /*
@@ -239,7 +241,8 @@ int gq_mmq_grouped_prepared(gq_act act, const gq_gemm_item *items, int n, int64_
 const char *gq_last_error(void);
 
 /* Library ABI version (major * 100 + minor).  103: gq_gemm_item, gq_mmq_grouped_prepared[_workspace_size],
- * gq_debug_route, and larger workspace sizes for the GEMM routes (round 4). */
+ * gq_debug_route, and larger workspace sizes for the GEMM routes (round 4).  104: gq_mmq_grouped[_ex]
+ * takes 5..32 tokens (the K-chunked streaming MMQ; round 5). */
 int gq_version(void);
 
 /*
