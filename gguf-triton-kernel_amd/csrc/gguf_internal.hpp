@@ -209,13 +209,14 @@ hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipS
 
 // K-chunked streaming MMQ (mmq_kstream.hip, 5..32 tokens): x~ in VGPRs (each of a workgroup's
 // 8 waves one K chunk), weights streamed per wave through private LDS rings, the waves' tiles
-// summed in LDS: one launch, no partials.  Up to kKMaxParts matrices (own type, activations,
-// output; the same N) in one launch, workgroups apportioned by weight bytes; a matrix's bits do
-// not depend on the launch it is in.  aq: 0 prepared x~ (X = [N][K], ldx = K, act_quant DEQ /
-// F8DEQ), 1 raw fp16 q8_1-quantized in-kernel, 2 raw fp16 with the fp8 variant's quantization.
-// kstream_ok: K % 256 == 0 and short enough for the waves' registers (K <= 4096), M % 16 == 0,
-// < 2 GiB of weights.
-constexpr int kKMaxParts = 16;
+// summed in LDS: one launch, no partials for K <= 4096.  A longer K is cut into ranges of 16
+// super-blocks whose fp32 partial tiles (kstream_partial_bytes of workspace) one small launch
+// sums in range order.  Up to kKMaxParts matrices x ranges (own type, activations, output; the
+// same N) in one launch, workgroups apportioned by weight bytes; a matrix's bits do not depend on
+// the launch it is in.  aq: 0 prepared x~ (X = [N][K], ldx = K, act_quant DEQ / F8DEQ), 1 raw fp16
+// q8_1-quantized in-kernel, 2 raw fp16 with the fp8 variant's quantization.
+// kstream_ok: K % 256 == 0, M % 16 == 0, < 2 GiB of weights.
+constexpr int kKMaxParts = 24;
 struct KItem {
     int fmt;
     const uint8_t *A;
@@ -224,9 +225,11 @@ struct KItem {
     uint16_t *C;
     int64_t ldc, M, K;
 };
+int kstream_splits(int64_t K);
 int kstream_cw(int64_t N, int64_t K);
 bool kstream_ok(int fmt, int64_t M, int64_t N, int64_t K);
-hipError_t launch_kstream(const KItem *items, int n, int64_t N, int aq, hipStream_t s);
+size_t kstream_partial_bytes(const KItem *items, int n, int64_t N);
+hipError_t launch_kstream(const KItem *items, int n, int64_t N, int aq, void *partials, hipStream_t s);
 
 // Skinny-token MMQ (mmq_skinny.hip, 1..32 tokens, K % 256 == 0): 16*rg rows x 16*nb tokens per
 // workgroup, K split over its 8 waves (8/nb ranges x nb token tiles), weights and activations

@@ -319,21 +319,36 @@ bool rgemm_route(int t, int form, int64_t M, int64_t N, int64_t K, int act)
 }
 
 // K-chunked streaming MMQ (mmq_kstream.hip): 5..32 tokens (the fp8 variant from 3: its decode
-// form covers 1..2), K % 256 == 0 within the waves' x~ registers (K <= 8192 at <= 16 tokens,
-// 4096 at 17..32), M % 16 == 0; one launch, no workspace (x~ quantized in-kernel from the raw
-// activations, or read prepared).  GQ_KSTREAM=1: wherever it applies, 0: off.
-bool use_kstream(int t, int form, int64_t M, int64_t N, int64_t K, int act)
+// form covers 1..2), K % 256 == 0, M % 16 == 0; one launch for K <= 4096 (x~ quantized in-kernel
+// from the raw activations, or read prepared).  GQ_KSTREAM=1: wherever it applies, 0: off.
+// By default on the prepared calls (x~ read as act_quant wrote it; single and grouped): 5..32
+// tokens measured 7-12% under the routes before it (MMQ us, default -> kstream, round 5
+// profiles/r05/ks_ab.txt: Q4_K 4096^2 x16 9.25 -> 7.96, 11008x4096 x16 15.31 -> 13.65,
+// 22016x4096 x16 24.23 -> 22.12, x32 30.52 -> 27.72, x8 24.02 -> 21.69; Q6_K 4096^2 x16 10.55 ->
+// 9.32; Q8_0 11008x4096 x16 18.05 -> 16.90).  Quantizing in-kernel (gq_mmq_ex) it is slower on the
+// small matrices (every workgroup quantizes its whole K of x), so the raw call keeps its routes.
+// A K longer than 4096 is cut into ranges summed by a second launch (fp32 partials in the
+// workspace): by default only inside a grouped launch (the layer's ffn_down beside the K = 4096
+// projections); split = false asks for the one-launch form.
+bool use_kstream(int t, int form, int64_t M, int64_t N, int64_t K, int act, bool prepared = false,
+                 bool split = false)
 {
     const int ks = gq::tuning().kstream;
     if (ks == 0 || form != gq::AF_F16 || use_blas(N, K) || !gq::kstream_ok(t, M, N, K)) return false;
     if (N < (act == GQ_ACT_FP8_E4M3 ? 3 : 5)) return false;
+    if (gq::kstream_splits(K) > 1 && !split && ks != 1) return false;
     if (ks == 1) return true;
-    return false; // (auto: not yet measured)
+    return prepared;
+}
+size_t kstream_ws(int t, int64_t M, int64_t N, int64_t K)
+{
+    const gq::KItem it{t, nullptr, nullptr, K, nullptr, M, M, K};
+    return gq::kstream_ok(t, M, N, K) && N <= 32 ? gq::kstream_partial_bytes(&it, 1, N) : 0;
 }
 // its 32-bit buffer offsets over the activations (rows ldx apart) and the output (rows ldc apart)
 bool kstream_fits(int64_t M, int64_t N, int64_t K, int64_t ldx, int64_t ldc)
 {
-    return ((N - 1) * ldx + K) * 2 < ((int64_t)1 << 31) && ((N - 1) * ldc + M) * 2 < ((int64_t)1 << 31);
+    return ((N - 1) * ldx + K) * 2 < ((int64_t)1 << 31) && ((N - 1) * ldc + M) * 4 < ((int64_t)1 << 31) && ldc % 4 == 0;
 }
 
 // Streaming 256-row GEMM (mmq_rgemm.hip sgemm_kernel) on the prepared x~, where the resident
@@ -436,6 +451,7 @@ size_t ws_bytes(int t, int act, int64_t M, int64_t N, int64_t K)
         const int64_t mr = gemm_rows_per_launch(t, M, K), nt = sk ? N : gemm_toks_per_launch(N, K);
         size_t p = use_rgemm(t, r.form, M, N, K) ? gq::plan_rgemm(M, N, K).partial_bytes
                    : use_sgemm(t, r.form, M, N, K) ? sgemm_partial_bytes(t, M, N, K) : 0;
+        if (gq::tuning().kstream == 1) p = p > kstream_ws(t, M, N, K) ? p : kstream_ws(t, M, N, K); // (its K ranges)
         for (int64_t mc : {mr, M % mr})
             for (int64_t nc : {nt, N % nt})
                 if (mc > 0 && nc > 0) {
@@ -669,9 +685,9 @@ static int compute(gq_type t, int act, const void *A, void *workspace, size_t wo
         // (the kernel is chosen by the call's token count: every chunk runs the same arithmetic)
         // (<= 32 skinny tokens are never cut: their x~ is far below the guard, and the token
         // count sets the kernel's K split)
-        if (use_kstream(t, r.form, M, N, K, act) && kstream_fits(M, N, K, K, ldc)) {
+        if (use_kstream(t, r.form, M, N, K, act, true) && kstream_fits(M, N, K, K, ldc)) {
             const gq::KItem it{t, (const uint8_t *)A, c.xdeq, K, (uint16_t *)C, ldc, M, K};
-            e = gq::launch_kstream(&it, 1, N, 0, s);
+            e = gq::launch_kstream(&it, 1, N, 0, c.partials, s);
             if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (kstream): %s", hipGetErrorString(e));
             return GQ_OK;
         }
@@ -754,7 +770,8 @@ int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int6
         // one launch, no workspace: the activations quantized inside (q8_1, or the fp8 variant's
         // e4m3), bit-identical to the act_quant forms the prepared call reads
         const gq::KItem it{t, (const uint8_t *)A, (const uint16_t *)B, ldb, (uint16_t *)C, ldc, M, K};
-        hipError_t e = gq::launch_kstream(&it, 1, N, act == GQ_ACT_FP8_E4M3 ? 2 : 1, (hipStream_t)stream);
+        hipError_t e = gq::launch_kstream(&it, 1, N, act == GQ_ACT_FP8_E4M3 ? 2 : 1,
+                                          carve(act, workspace, N, K).partials, (hipStream_t)stream);
         if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (kstream): %s", hipGetErrorString(e));
         return GQ_OK;
     }
@@ -1006,13 +1023,13 @@ int gq_mmq_grouped_ex(gq_act act, const gq_group_item *items, int n, int64_t N, 
         gq::KItem ki[16];
         for (int i = 0; i < m; ++i) {
             const gq::DecodeItem &d = di[i];
-            if (!use_kstream(d.fmt, gq::AF_F16, d.M, N, d.K, act) || d.ldx % 8 != 0 || ((uintptr_t)d.X & 15) != 0 ||
-                !kstream_fits(d.M, N, d.K, d.ldx, d.ldc))
+            if (!use_kstream(d.fmt, gq::AF_F16, d.M, N, d.K, act) || gq::kstream_splits(d.K) > 1 || d.ldx % 8 != 0 ||
+                ((uintptr_t)d.X & 15) != 0 || !kstream_fits(d.M, N, d.K, d.ldx, d.ldc))
                 return fail(GQ_EUNSUPPORTED, "item %d: not a grouped K-chunked-stream shape (N=%lld, M=%lld, K=%lld)", i,
                             (long long)N, (long long)d.M, (long long)d.K);
             ki[i] = gq::KItem{d.fmt, d.A, d.X, d.ldx, d.C, d.ldc, d.M, d.K};
         }
-        hipError_t e = gq::launch_kstream(ki, m, N, fp8 ? 2 : 1, (hipStream_t)stream);
+        hipError_t e = gq::launch_kstream(ki, m, N, fp8 ? 2 : 1, nullptr, (hipStream_t)stream); // (no K ranges)
         if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (grouped kstream): %s", hipGetErrorString(e));
         return GQ_OK;
     }
@@ -1047,35 +1064,61 @@ static int grouped_gemm_items(gq_act act, const gq_gemm_item *items, int n, int6
     return GQ_OK;
 }
 
+// gq_mmq_grouped_prepared's split of the items: those the K-chunked streaming MMQ takes (one
+// launch, no workspace) and the rest (the grouped streaming GEMM: one launch + its reduce)
+static void grouped_split(gq_act act, gq::SGroupItem *g, int n, int64_t N, gq::KItem *ks, int &nk, gq::SGroupItem *rest,
+                          int &nr)
+{
+    nk = nr = 0;
+    for (int i = 0; i < n; ++i) {
+        if (g[i].M <= 0) continue;
+        if (use_kstream(g[i].fmt, gq::AF_F16, g[i].M, N, g[i].K, act, true, true) &&
+            kstream_fits(g[i].M, N, g[i].K, g[i].K, g[i].ldc))
+            ks[nk++] = gq::KItem{g[i].fmt, g[i].A, g[i].X, g[i].K, g[i].C, g[i].ldc, g[i].M, g[i].K};
+        else
+            rest[nr++] = g[i];
+    }
+}
+
 size_t gq_mmq_grouped_prepared_workspace_size(gq_act act, const gq_gemm_item *items, int n, int64_t N)
 {
-    gq::SGroupItem g[16];
+    gq::SGroupItem g[16], rest[16];
+    gq::KItem ks[16];
+    int nk, nr;
     if (n < 1 || grouped_gemm_items(act, items, n, N, g) != GQ_OK) return 0;
-    int m = 0; // items with rows (as gq_mmq_grouped_prepared plans them)
-    for (int i = 0; i < n; ++i)
-        if (g[i].M > 0) g[m++] = g[i];
-    if (m == 0) return 0;
-    const gq::SGroupPlan p = gq::plan_sgemm_grouped(g, m, N, gq::tuning().sgemm_splits);
-    return p.ok ? p.partial_bytes : 0;
+    grouped_split(act, g, n, N, ks, nk, rest, nr);
+    // [the K-chunked stream's K-range partials][the streaming GEMM's split-K partials]
+    const size_t kb = align_up(gq::kstream_partial_bytes(ks, nk, N));
+    if (nr == 0) return kb;
+    const gq::SGroupPlan p = gq::plan_sgemm_grouped(rest, nr, N, gq::tuning().sgemm_splits);
+    return kb + (p.ok ? p.partial_bytes : 0);
 }
 
 int gq_mmq_grouped_prepared(gq_act act, const gq_gemm_item *items, int n, int64_t N, void *workspace,
                             size_t workspace_bytes, void *stream)
 {
     g_err.clear();
-    gq::SGroupItem g[16];
+    gq::SGroupItem g[16], rest[16];
+    gq::KItem ks[16];
+    int nk, nr;
     int rc = grouped_gemm_items(act, items, n, N, g);
     if (rc != GQ_OK) return rc;
-    int m = 0; // items with rows
-    for (int i = 0; i < n; ++i)
-        if (g[i].M > 0) g[m++] = g[i];
-    if (m == 0) return GQ_OK;
-    const gq::SGroupPlan p = gq::plan_sgemm_grouped(g, m, N, gq::tuning().sgemm_splits);
-    if (!p.ok) return fail(GQ_EUNSUPPORTED, "not a grouped GEMM shape");
-    if (p.partial_bytes && (!workspace || workspace_bytes < p.partial_bytes))
-        return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace ? workspace_bytes : (size_t)0, p.partial_bytes);
-    const hipError_t e = gq::launch_sgemm_grouped(g, m, N, p, workspace, (hipStream_t)stream);
-    if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (grouped GEMM): %s", hipGetErrorString(e));
+    grouped_split(act, g, n, N, ks, nk, rest, nr);
+    // [the K-chunked stream's K-range partials][the streaming GEMM's split-K partials]
+    const size_t kb = align_up(gq::kstream_partial_bytes(ks, nk, N));
+    gq::SGroupPlan p;
+    const size_t need = kb + (nr > 0 ? (p = gq::plan_sgemm_grouped(rest, nr, N, gq::tuning().sgemm_splits)).partial_bytes : 0);
+    if (nr > 0 && !p.ok) return fail(GQ_EUNSUPPORTED, "not a grouped GEMM shape");
+    if (need && (!workspace || workspace_bytes < need))
+        return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace ? workspace_bytes : (size_t)0, need);
+    if (nk > 0) {
+        const hipError_t e = gq::launch_kstream(ks, nk, N, 0, workspace, (hipStream_t)stream);
+        if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (grouped kstream): %s", hipGetErrorString(e));
+    }
+    if (nr > 0) {
+        const hipError_t e = gq::launch_sgemm_grouped(rest, nr, N, p, (uint8_t *)workspace + kb, (hipStream_t)stream);
+        if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (grouped GEMM): %s", hipGetErrorString(e));
+    }
     return GQ_OK;
 }
 
@@ -1134,7 +1177,8 @@ const char *gq_debug_route(gq_type t, gq_act act, int64_t M, int64_t N, int64_t 
     if (!prepared && fused_decode_route(t, act, N, K)) return "stream_decode_kernel";
     if (r.blas) return "dequant_kernel + hipBLASLt";
     if (r.gemv) return "gemv_kernel";
-    if (use_kstream(t, r.form, M, N, K, act)) return "kstream_kernel";
+    if (use_kstream(t, r.form, M, N, K, act, prepared != 0))
+        return gq::kstream_splits(K) > 1 ? "kstream_kernel + kstream_reduce_kernel" : "kstream_kernel";
     if (use_fgemm(t, r.form, M, N, K)) return "fgemm_kernel";
     if (rgemm_route(t, r.form, M, N, K, act)) return "rgemm_kernel + gemm_reduce_f16_kernel";
     if (use_skinny(t, r.form, N, act)) return "skinny_kernel";

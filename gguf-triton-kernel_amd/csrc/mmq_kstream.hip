@@ -53,7 +53,11 @@ namespace {
 #endif
 constexpr int KABL = GQ_KSTREAM_ABL;
 
-constexpr int KW = 8;        // waves per workgroup (two per SIMD)
+constexpr int KW = 8;        // waves per workgroup
+#ifndef GQ_KSTREAM_WPC
+#define GQ_KSTREAM_WPC 1
+#endif
+constexpr int KWPC = GQ_KSTREAM_WPC; // workgroups per CU (2: four waves per SIMD at <= 128 VGPRs -- spills 36-78 VGPRs today, diagnostic builds only)
 
 // LDS image of one super-block of a row: RBW bytes = PPS 16-byte pieces, piece q read from
 // super-block byte ksrc<F>(q).  Q6_K: 240-byte aligned image (d at 222), rgemm's / gemm's.
@@ -70,7 +74,7 @@ template <int F> __device__ __forceinline__ uint32_t ksrc(int q)
 // 4.25 KiB), as 16 image rows PPR pieces apart (odd strides spread a fragment's 16 rows over the
 // banks).  Small tasks, so that a ring of 3-4 slots per wave keeps ~100 KiB per CU in flight.
 template <int F> struct KTask {
-    static constexpr int TSB = F == Q4_K ? 2 : 1;      // super-blocks per task
+    static constexpr int TSB = F == Q4_K && KWPC == 1 ? 2 : 1; // super-blocks per task
     static constexpr int PPR0 = TSB * KImg<F>::PPS;    // pieces of a row's task bytes (18 / 15 / 17)
     static constexpr int PPR = PPR0 | 1;               // image row stride in pieces (odd)
     static constexpr int IRS = 16 * PPR;               // image row stride
@@ -78,8 +82,11 @@ template <int F> struct KTask {
     static constexpr int SLOT = 16 * IRS;              // ring slot bytes (4864 / 3840 / 4352)
 };
 constexpr int KNSMAX = 4;      // ring slots per wave at most
-constexpr int KRGN = 16384;    // LDS per wave: its weight ring, and the activation staging before it
-template <int NB> constexpr int KIP = NB == 1 ? 2 : 1; // items per LDS reduce (scratch: 16 KiB)
+constexpr int KCWMAX = 2;      // x~ super-blocks per wave at most (a K range: 16 super-blocks)
+// LDS per wave: its weight ring, and the activation staging before it (passes of KSPB super-blocks)
+constexpr int KRGN = KWPC == 1 ? 16384 : 9200;
+constexpr int KSPB = KWPC == 1 ? 2 : 1;
+template <int NB> constexpr int KIP = NB == 1 && KWPC == 1 ? 2 : 1; // items per LDS reduce
 template <int F> constexpr uint32_t sb_bytes() { return Layout<F>::BYTES * (256 / Layout<F>::QK); }
 
 // s_waitcnt vmcnt(n) for a wave-uniform n in [LO, HI] (the immediate is an encoding field): a
@@ -99,9 +106,11 @@ template <int LO, int HI> __device__ __attribute__((always_inline)) inline void 
 struct KPart {
     const uint8_t *A;
     const uint16_t *X;
-    uint16_t *C;
+    uint16_t *C;       // fp16 output (a whole-K part), or
+    float *P;          // fp32 partial tile of one K range (a split part; rows ldc apart)
     int64_t ldx, ldc;
     int M, K, fmt, cw; // cw: super-blocks per wave
+    int kofs, nsbp;    // the part's K range: super-blocks kofs .. kofs + nsbp - 1
     int64_t wcum;      // weight bytes of the parts before it
     int w;             // weight bytes per item (16 rows)
 };
@@ -316,8 +325,8 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l16 = lane & 15, gl = lane >> 4;
     const int M = P.M, nsb = P.K >> 8, cw = P.cw;
-    const int sb0 = wave * cw;
-    int mysb = nsb - sb0;
+    const int sb0 = P.kofs + wave * cw;
+    int mysb = P.kofs + P.nsbp - sb0;
     mysb = mysb < 0 ? 0 : (mysb > cw ? cw : mysb);
     const int ntg = (mysb + TSB - 1) / TSB;  // this wave's tasks per row group (0..NTG)
     const int ntask = (j1 - j0) * ntg;
@@ -374,20 +383,23 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
 #pragma unroll
         for (int t = 0; t < NB; ++t)
 #pragma unroll
-            for (int c0 = 0; c0 < CWM; c0 += 2) {
+            for (int c0 = 0; c0 < CWM; c0 += KSPB) {
                 if (c0 >= mysb) break; // (wave-uniform)
+                // a pass: 16 token rows of KSPB super-blocks (RP = 32 * KSPB pieces each)
+                constexpr int RP = 32 * KSPB;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) { // token row r: source piece l ^ bitrev4(r) at position l
+                for (int i = 0; i < 16 * RP / 64; ++i) {
+                    const int r = (64 * i + lane) / RP, pos = (64 * i + lane) % RP;
                     const int tok = 16 * t + r < N ? 16 * t + r : N - 1;
-                    const int q = lane ^ (((r & 1) << 3) | ((r & 2) << 1) | ((r & 4) >> 1) | ((r & 8) >> 3));
+                    const int q = pos ^ (((r & 1) << 3) | ((r & 2) << 1) | ((r & 4) >> 1) | ((r & 8) >> 3));
                     const int sb = sb0 + c0 + (q >> 5);
                     const uint32_t off = 2u * ((uint32_t)tok * (uint32_t)P.ldx +
                                                256u * (uint32_t)(sb < sb0 + mysb ? sb : sb0 + c0) + 8u * (uint32_t)(q & 31));
-                    dma16(xrs, ring + 1024 * r, off, 0);
+                    dma16(xrs, ring + 1024 * i, off, 0);
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-                for (int cs = 0; cs < 2 && c0 + cs < CWM; ++cs) {
+                for (int cs = 0; cs < KSPB && c0 + cs < CWM; ++cs) {
                     const int c = c0 + cs;
                     u32x4 xr[2][4];
 #pragma unroll
@@ -395,7 +407,7 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
 #pragma unroll
                         for (int i = 0; i < 4; ++i) {
                             const int qp = 32 * cs + (elem_a<F>(gl) + h * elem_b_off<F>()) / 8 + i;
-                            xr[h][i] = *(const u32x4 *)(ring + 1024 * l16 + 16 * (qp ^ frow));
+                            xr[h][i] = *(const u32x4 *)(ring + 16 * RP * l16 + 16 * (qp ^ frow));
                         }
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
@@ -423,8 +435,10 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
     // ---- IP items' tiles summed over the 8 waves (the last to arrive, in wave order) and stored ----
     // The summing wave issues exactly IP*NB buffer stores (tokens past N: an offset past the
     // buffer's range, dropped), so the ring's waits can count them (stores share vmcnt).
-    const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)P.C, 0, (int)(uint32_t)(((int64_t)(N - 1) * P.ldc + M) * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t crs =
+        P.P ? __builtin_amdgcn_make_buffer_rsrc((void *)P.P, 0, (int)(uint32_t)(((int64_t)(N - 1) * P.ldc + M) * 4), 0x00020000)
+            : __builtin_amdgcn_make_buffer_rsrc((void *)P.C, 0, (int)(uint32_t)(((int64_t)(N - 1) * P.ldc + M) * 2),
+                                                0x00020000);
     auto reduce_store = [&](int grp, int np, const f32x4 (&acc)[IP][NB]) __attribute__((always_inline)) -> bool {
         // the scratch is free once the previous hand-off has been summed (a wave is a whole round
         // of items ahead of the summing wave before it waits here)
@@ -451,12 +465,17 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
 #pragma unroll
                 for (int w = 1; w < KW; ++w) v += *(const f32x4 *)(scr + ((w * IP + ip) * NB + t) * 256 + 4 * lane);
                 const int tok = 16 * t + l16, row = 16 * (grp + ip) + 4 * gl; // (M % 16 == 0: 4 rows exist)
-                const uint32_t off =
-                    tok < N && ip < np ? 2u * ((uint32_t)tok * (uint32_t)P.ldc + (uint32_t)row) : 0x80000000u;
-                __builtin_amdgcn_raw_buffer_store_b64(
-                    (u32x2){(uint32_t)f2h_bits(v[0]) | ((uint32_t)f2h_bits(v[1]) << 16),
-                            (uint32_t)f2h_bits(v[2]) | ((uint32_t)f2h_bits(v[3]) << 16)},
-                    crs, off, 0, 0);
+                const bool real = tok < N && ip < np;
+                if (P.P) { // a split part: its fp32 partial
+                    const uint32_t off = real ? 4u * ((uint32_t)tok * (uint32_t)P.ldc + (uint32_t)row) : 0x80000000u;
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), crs, off, 0, 0);
+                } else {
+                    const uint32_t off = real ? 2u * ((uint32_t)tok * (uint32_t)P.ldc + (uint32_t)row) : 0x80000000u;
+                    __builtin_amdgcn_raw_buffer_store_b64(
+                        (u32x2){(uint32_t)f2h_bits(v[0]) | ((uint32_t)f2h_bits(v[1]) << 16),
+                                (uint32_t)f2h_bits(v[2]) | ((uint32_t)f2h_bits(v[3]) << 16)},
+                        crs, off, 0, 0);
+                }
             }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the scratch reads are done
         if (lane == 0) __hip_atomic_store(&sync[1], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -559,7 +578,7 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
 }
 
 template <int NB, int CWM>
-__global__ __launch_bounds__(64 * KW) void kstream_kernel(const KArgs a)
+__global__ __launch_bounds__(64 * KW, KWPC * KW / 4) void kstream_kernel(const KArgs a)
 {
     extern __shared__ __attribute__((aligned(1024))) uint8_t smem[]; // the waves' rings (KRGN each)
     __shared__ __attribute__((aligned(16))) float scr[KW * KIP<NB> * NB * 256]; // the waves' item tiles
@@ -591,7 +610,7 @@ template <int NB, int CWM> hipError_t run(const KArgs &a, unsigned grid, hipStre
         hipFuncAttributes fa;
         hipError_t e = hipFuncGetAttributes(&fa, (const void *)kstream_kernel<NB, CWM>);
         if (e != hipSuccess) return e;
-        if (fa.sharedSizeBytes + (size_t)KW * KRGN > 160 * 1024) return hipErrorInvalidValue;
+        if (KWPC * (fa.sharedSizeBytes + (size_t)KW * KRGN) > 160 * 1024) return hipErrorInvalidValue;
         e = hipFuncSetAttribute((const void *)kstream_kernel<NB, CWM>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 KW * KRGN);
         if (e != hipSuccess) return e;
@@ -605,11 +624,14 @@ template <int NB, int CWM> hipError_t run(const KArgs &a, unsigned grid, hipStre
 
 // K split over the 8 waves: cw super-blocks each (the fewest that cover K), or 0 when K is
 // longer than the waves' x~ registers hold (2 super-blocks each: K <= 4096)
+// K ranges (split parts) of a matrix: as few as keep each within the 8 waves' x~ registers
+// (2 super-blocks per wave: 16 per range); cw = super-blocks per wave of a range
+int kstream_splits(int64_t K) { return (int)((K / 256 + 8 * KCWMAX - 1) / (8 * KCWMAX)); }
 int kstream_cw(int64_t N, int64_t K)
 {
     if (K % 256 != 0 || N < 1 || N > 32) return 0;
-    const int64_t cw = (K / 256 + KW - 1) / KW;
-    return cw <= 2 ? (int)cw : 0;
+    const int64_t S = kstream_splits(K), per = (K / 256 + S - 1) / S;
+    return (int)((per + KW - 1) / KW);
 }
 
 bool kstream_ok(int fmt, int64_t M, int64_t N, int64_t K)
@@ -620,50 +642,110 @@ bool kstream_ok(int fmt, int64_t M, int64_t N, int64_t K)
     return M * (K / 256) * (int64_t)(fmt == Q8_0 ? 272 : (fmt == Q4_K ? 144 : 210)) < ((int64_t)1 << 31);
 }
 
-hipError_t launch_kstream(const KItem *items, int n, int64_t N, int aq, hipStream_t s)
+size_t kstream_partial_bytes(const KItem *items, int n, int64_t N)
+{
+    size_t b = 0;
+    for (int i = 0; i < n; ++i) {
+        const int S = kstream_splits(items[i].K);
+        if (S > 1) b += ((size_t)S * N * items[i].M * 4 + 255) & ~(size_t)255;
+    }
+    return b;
+}
+
+namespace {
+// C[t][m] = fp16(sum over the splits, in order, of the fp32 partials P[z][t][m]); four outputs per
+// thread, every split part of a launch in one grid
+struct KRed {
+    const float *P[kKMaxParts];
+    uint16_t *C[kKMaxParts];
+    int64_t ldc[kKMaxParts];
+    int M[kKMaxParts], S[kKMaxParts], blk0[kKMaxParts + 1];
+    int n, N;
+};
+__global__ __launch_bounds__(256) void kstream_reduce_kernel(const KRed r)
+{
+    int i = 0;
+    while (i + 1 < r.n && (int)blockIdx.x >= r.blk0[i + 1]) ++i;
+    const int64_t q = (int64_t)(blockIdx.x - r.blk0[i]) * 256 + threadIdx.x; // 4-output unit
+    const int M = r.M[i], m4 = M / 4;
+    if (q >= (int64_t)r.N * m4) return;
+    const int t = (int)(q / m4), m = 4 * (int)(q % m4);
+    const size_t zs = (size_t)r.N * M;
+    f32x4 v = *(const f32x4 *)(r.P[i] + (size_t)t * M + m);
+    for (int z = 1; z < r.S[i]; ++z) v += *(const f32x4 *)(r.P[i] + z * zs + (size_t)t * M + m);
+    *(u32x2 *)(r.C[i] + t * r.ldc[i] + m) = (u32x2){(uint32_t)f2h_bits(v[0]) | ((uint32_t)f2h_bits(v[1]) << 16),
+                                                    (uint32_t)f2h_bits(v[2]) | ((uint32_t)f2h_bits(v[3]) << 16)};
+}
+} // namespace
+
+hipError_t launch_kstream(const KItem *items, int n, int64_t N, int aq, void *partials, hipStream_t s)
 {
     if (n < 1 || n > kKMaxParts || N < 1 || N > 32) return hipErrorInvalidValue;
     KArgs a{};
-    a.n = n;
+    KRed rd{};
     a.N = (int)N;
     a.aq = aq;
-    int kb = 0;
-    int64_t wcum = 0, items_total = 0;
+    rd.N = (int)N;
+    int kb = 0, np = 0, cwm = 1;
+    int64_t wcum = 0, items_total = 0, rblk = 0;
+    uint8_t *pw = (uint8_t *)partials;
     for (int i = 0; i < n; ++i) {
         const KItem &it = items[i];
         if (!kstream_ok(it.fmt, it.M, N, it.K)) return hipErrorInvalidValue;
-        KPart &p = a.p[i];
-        p.A = it.A;
-        p.X = it.X;
-        p.C = it.C;
-        p.ldx = it.ldx;
-        p.ldc = it.ldc;
-        p.M = (int)it.M;
-        p.K = (int)it.K;
-        p.fmt = it.fmt;
-        p.cw = kstream_cw(N, it.K);
-        const int64_t rb = (it.K / 256) * (it.fmt == Q8_0 ? 272 : (it.fmt == Q4_K ? 144 : 210));
-        p.w = (int)(16 * rb);
-        p.wcum = wcum;
-        const int64_t ng = (it.M + 15) / 16;
-        wcum += ng * p.w;
-        items_total += ng;
+        const int S = kstream_splits(it.K), nsb = (int)(it.K / 256), per = (nsb + S - 1) / S;
+        float *P = nullptr;
+        if (S > 1) {
+            if (!partials || rd.n == kKMaxParts) return hipErrorInvalidValue;
+            P = (float *)pw;
+            pw += ((size_t)S * N * it.M * 4 + 255) & ~(size_t)255;
+            rd.P[rd.n] = P;
+            rd.C[rd.n] = it.C;
+            rd.ldc[rd.n] = it.ldc;
+            rd.M[rd.n] = (int)it.M;
+            rd.S[rd.n] = S;
+            rd.blk0[rd.n] = (int)rblk;
+            rblk += (N * (it.M / 4) + 255) / 256;
+            ++rd.n;
+        }
+        for (int z = 0; z < S; ++z) {
+            if (np == kKMaxParts) return hipErrorInvalidValue;
+            KPart &p = a.p[np++];
+            p.A = it.A;
+            p.X = it.X;
+            p.C = it.C;
+            p.P = P ? P + (size_t)z * N * it.M : nullptr;
+            p.ldx = it.ldx;
+            p.ldc = P ? it.M : it.ldc;
+            p.M = (int)it.M;
+            p.K = (int)it.K;
+            p.fmt = it.fmt;
+            p.kofs = z * per;
+            p.nsbp = nsb - p.kofs < per ? nsb - p.kofs : per;
+            p.cw = (p.nsbp + KW - 1) / KW;
+            const int64_t sbb = it.fmt == Q8_0 ? 272 : (it.fmt == Q4_K ? 144 : 210);
+            p.w = (int)(16 * p.nsbp * sbb);
+            p.wcum = wcum;
+            const int64_t ng = it.M / 16;
+            wcum += ng * p.w;
+            items_total += ng;
+            cwm = p.cw > cwm ? p.cw : cwm;
+        }
         const int k = it.fmt == Q4_K ? KTask<Q4_K>::SLOT : (it.fmt == Q6_K ? KTask<Q6_K>::SLOT : KTask<Q8_0>::SLOT);
         kb = k > kb ? k : kb;
     }
+    a.n = np;
     a.wtot = wcum;
     a.slot = kb;
     a.ns = KRGN / kb > KNSMAX ? KNSMAX : KRGN / kb; // ring slots per wave (3 or 4)
-    int cwm = 1;
-    for (int i = 0; i < n; ++i) cwm = a.p[i].cw > cwm ? a.p[i].cw : cwm;
-    const int64_t cus = num_cus();
-    const unsigned grid = (unsigned)(items_total < cus ? items_total : cus);
-    if (N <= 16) {
-        if (cwm <= 1) return run<1, 1>(a, grid, s);
-        return run<1, 2>(a, grid, s);
-    }
-    if (cwm <= 1) return run<2, 1>(a, grid, s);
-    return run<2, 2>(a, grid, s);
+    const int64_t wgs = num_cus() * KWPC;
+    const unsigned grid = (unsigned)(items_total < wgs ? items_total : wgs);
+    hipError_t e;
+    if (N <= 16) e = cwm <= 1 ? run<1, 1>(a, grid, s) : run<1, 2>(a, grid, s);
+    else e = cwm <= 1 ? run<2, 1>(a, grid, s) : run<2, 2>(a, grid, s);
+    if (e != hipSuccess || rd.n == 0) return e;
+    rd.blk0[rd.n] = (int)rblk;
+    kstream_reduce_kernel<<<dim3((unsigned)rblk), dim3(256), 0, s>>>(rd);
+    return hipGetLastError();
 }
 
 } // namespace gq

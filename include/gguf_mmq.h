@@ -86,8 +86,12 @@ int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int6
  * can serve several weight matrices that share an input (Q/K/V, gate/up).
  * Same result as gq_mmq within the stated tolerances, not always the same kernels: for
  * N <= 4 gq_mmq runs the one-launch fused decode kernel (quantizer in LDS) while the split
- * form quantizes to the workspace and runs the decode-shaped GEMV; for Q8_0 with the int8
- * GEMM form enabled (GQ_GEMM_I8=1) gq_act_prepare writes both activation forms.
+ * form quantizes to the workspace and runs the decode-shaped GEMV; at N = 5..32 (K <= 4096,
+ * M % 16 == 0) the split form runs the K-chunked streaming MMQ while gq_mmq keeps the resident
+ * GEMM (the same x~ and products, summed over K in another fp32 order: within 4e-3, not bit for
+ * bit; GQ_KSTREAM=1 puts both on the stream, GQ_KSTREAM=0 both off it, and then the bits match);
+ * for Q8_0 with the int8 GEMM form enabled (GQ_GEMM_I8=1) gq_act_prepare writes both activation
+ * forms.
  */
 int gq_act_prepare(const void *B, int64_t N, int64_t K, int64_t ldb, void *workspace, size_t workspace_bytes,
                    void *stream);
@@ -190,8 +194,7 @@ int gq_mmq_sharded(gq_type t, const void *A_shard, const void *B, void *C, int64
  * output C (N x M, row stride ldc); items may share B.  N = 1..4: the streaming decode kernel,
  * every item's output bit-identical to its own gq_mmq call; N = 5..32: the K-chunked streaming
  * MMQ (every item bit-identical to its own gq_mmq_ex on that kernel, GQ_KSTREAM=1), which needs
- * K % 256 == 0, K <= 8192 (N <= 16) / 4096 (N <= 32), M % 16 == 0, B 16-byte aligned and ldb % 8
- * == 0.  The chip's workgroups are split over the items by weight bytes.  No workspace, no host
+ * K % 256 == 0, K <= 4096, M % 16 == 0, B 16-byte aligned and ldb % 8 == 0.  The chip's workgroups are split over the items by weight bytes.  No workspace, no host
  * sync.  GQ_EUNSUPPORTED (nothing launched) when N > 32, or an item is not a shape of that
  * launch (decode: activations that do not fit LDS, >= 2 GiB of weights, more than 16 parts =
  * item x token group; 5..32: the conditions above, more than 16 items): call gq_mmq per item then.
@@ -220,7 +223,11 @@ int gq_mmq_grouped_ex(gq_act act, const gq_group_item *items, int n, int64_t N, 
  * (items may share one), output C (N x M, row stride ldc).  The chip's workgroups are spread
  * over the items' row tiles x super-blocks (each item split along K so that the whole launch is
  * one round of the chip); with the split factor pinned (GQ_SGEMM_SPLITS) every item's output is
- * bit-identical to its own gq_mmq_prepared_ex call on that kernel (GQ_SGEMM=1).  workspace: the
+ * bit-identical to its own gq_mmq_prepared_ex call on that kernel (GQ_SGEMM=1).  At N = 5..32
+ * the items with M % 16 == 0 go instead to one launch of the K-chunked streaming MMQ (a K over
+ * 4096 in ranges of 4096 whose fp32 partials a second launch sums), each item bit-identical to
+ * its own gq_mmq_prepared_ex (which takes the same kernel for K <= 4096; GQ_KSTREAM=1 for
+ * longer K); GQ_KSTREAM=0 keeps every item on the streaming GEMM.  workspace: the K-range and
  * split-K partials, >= gq_mmq_grouped_prepared_workspace_size() bytes (0 when nothing splits:
  * NULL allowed).  GQ_EUNSUPPORTED (nothing launched) for N < 5, more than 16 items, K % 256 != 0
  * or >= 2 GiB in one item: call gq_mmq_prepared_ex per item then.  No host sync.

@@ -62,7 +62,7 @@ def test_grouped_gemm_bit_identical_to_per_matrix(N, splits, tune):
     gemm_kernel's per-row MFMA sequence (GQ_SGEMM=0 GQ_GEMM_SPLITS=1); four the per-matrix
     streaming kernel's (GQ_SGEMM=1 GQ_SGEMM_SPLITS=4), the grouped reduce = gemm_reduce_f16."""
     import kernels._lib as kl
-    tune(GQ_SGEMM_SPLITS=splits)
+    tune(GQ_SGEMM_SPLITS=splits, GQ_KSTREAM=0)  # (the streaming GEMM's grouped form)
     types, raw, x, h, items, names, inputs = _layer_items(kl, N, layer=0, seed=N)
     outs = kl.mmq_grouped_prepared(items, N)
     assert outs is not None, kl.lib().gq_last_error()
@@ -164,7 +164,8 @@ def test_grouped_gemm_refuses():
     qB = torch.from_numpy(random_blocks("q8_0", M, K, seed=4).view(np.int8)).to(dev)
     ws = _prepare(kl, torch.from_numpy(random_activations(N, K, seed=5)).to(dev), N, K)
     out = torch.full((N, M), 3.0, dtype=torch.float16, device=dev)
-    with kl.tuning(GQ_CUS=256):
+    # (the streaming GEMM's limit: the K-chunked stream, which takes such items by default, off)
+    with kl.tuning(GQ_CUS=256, GQ_KSTREAM=0):
         assert kl.mmq_grouped_prepared([(kl.GQ_Q8_0, qB, ws, M, K, out)], N) is None
     torch.cuda.synchronize()
     assert torch.all(out == 3.0)
@@ -200,7 +201,7 @@ def test_grouped_gemm_stream_k(cus, tune):
     and the same bits call after call."""
     import kernels._lib as kl
     dev = _dev()
-    tune(GQ_CUS=cus, GQ_SGEMM_STREAMK=1)
+    tune(GQ_CUS=cus, GQ_SGEMM_STREAMK=1, GQ_KSTREAM=0)
     N = 40
     specs = [("q4_k", 1000, 4096), ("q6_k", 300, 2816), ("q8_0", 2048, 1024), ("q4_k", 256, 11008), ("q6_k", 64, 256)]
     X = {K: random_activations(N, K, seed=K) for K in {s[2] for s in specs}}
@@ -234,7 +235,7 @@ def test_single_matrix_stream_k(fmt, M, K, N, tune):
     raw = random_blocks(fmt, M, K, seed=M)
     B = random_activations(N, K, seed=K)
     A_t, B_t = torch.from_numpy(raw.view(np.int8)).to(dev), torch.from_numpy(B).to(dev)
-    tune(GQ_RGEMM=0, GQ_SKINNY=0, GQ_SGEMM=1, GQ_SGEMM_STREAMK=1, GQ_CUS=61)
+    tune(GQ_RGEMM=0, GQ_SKINNY=0, GQ_SGEMM=1, GQ_SGEMM_STREAMK=1, GQ_CUS=61, GQ_KSTREAM=0)
     ws = _prepare(kl, B_t, N, K, need=kl.workspace_size(kl.TYPES[fmt], M, N, K))
     C = kl.mmq_prepared(kl.TYPES[fmt], A_t, ws, M, N, K).cpu().numpy()
     tune(GQ_SGEMM_STREAMK=0)
@@ -255,6 +256,7 @@ def test_stage_schedule_same_bits(N, knob, pair, tune):
     single streaming-GEMM call give the bits of the half-stage schedule."""
     import kernels._lib as kl
     types, raw, x, h, items, names, inputs = _layer_items(kl, N, layer=0, seed=N + pair)
+    tune(GQ_KSTREAM=0)  # both sides on the streaming GEMM
     ref = kl.mmq_grouped_prepared(items, N)
     assert ref is not None, kl.lib().gq_last_error()
     torch.cuda.synchronize()

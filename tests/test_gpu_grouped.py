@@ -177,13 +177,16 @@ def test_act_prepare_grouped_matches_individual(act):
 
 @pytest.mark.parametrize("N,act", [(5, "q8_1"), (8, "q8_1"), (16, "q8_1"), (64, "q8_1"), (128, "q8_1"),
                                    (1, "fp8"), (2, "fp8"), (3, "fp8"), (8, "fp8"), (128, "fp8")])
-def test_layer_mix_prepared_matches_per_call(N, act):
+def test_layer_mix_prepared_matches_per_call(N, act, tune):
     """LayerMix from 5 tokens (the four inputs quantized in one gq_act_prepare_grouped launch, every
     projection prepared; grouped=False: one launch per projection, not the grouped GEMM of
     tests/test_gpu_gemm_grouped.py): unfused, every projection bit-identical to its own mmq(); fused (q+k and
     gate+up as one taller matrix, whose split-K plan may differ from the parts') within the GEMM
-    tolerance of the unfused result."""
+    tolerance of the unfused result.  GQ_KSTREAM=1: at 5..32 tokens the default routes a prepared call
+    to the K-chunked stream but a raw one to the resident GEMM (a different fp32 order over K; see
+    test_layer_mix_default_routes_within_tolerance), so both sides are pinned to the stream here."""
     import kernels._lib as kl
+    tune(GQ_KSTREAM=1)
     from gguf import LLAMA_LAYER_SHAPES, q4_k_m_layer_types
     from kernels.layer_mix import GGUFLinear, LayerMix
     dev = _dev()
@@ -203,6 +206,28 @@ def test_layer_mix_prepared_matches_per_call(N, act):
         torch.cuda.synchronize()
         assert torch.equal(res[n].view(torch.int16), solo.view(torch.int16)), n
         assert O.max_rel_err(fused[n].cpu().numpy(), solo.cpu().numpy()) <= 4e-3, n
+
+
+@pytest.mark.parametrize("N", [8, 16])
+def test_layer_mix_default_routes_within_tolerance(N):
+    """Default routes at 16 tokens: LayerMix's prepared projections (K-chunked stream) against each
+    projection's raw mmq() (resident GEMM) -- the same products summed in another fp32 order, so
+    within the GEMM tolerance (4e-3 relative), not bit for bit."""
+    import kernels._lib as kl
+    from gguf import LLAMA_LAYER_SHAPES, q4_k_m_layer_types
+    from kernels.layer_mix import GGUFLinear, LayerMix
+    dev = _dev()
+    types = q4_k_m_layer_types(0, 32)
+    _, A = _layer(types, seed=19)
+    lins = {n: GGUFLinear(types[n], A[n], M, K) for n, (M, K) in LLAMA_LAYER_SHAPES.items()}
+    x, a, y = (torch.from_numpy(random_activations(N, 4096, seed=s)).to(dev) for s in (25, 26, 27))
+    h = torch.from_numpy(random_activations(N, 11008, seed=28)).to(dev)
+    res = LayerMix(lins, fuse=False, grouped=False).forward(x, h, attn=a, x_ffn=y)
+    inp = {"attn_q": x, "attn_k": x, "attn_v": x, "attn_output": a, "ffn_gate": y, "ffn_up": y, "ffn_down": h}
+    for n, (M, K) in LLAMA_LAYER_SHAPES.items():
+        solo = kl.mmq(kl.TYPES[types[n]], A[n], inp[n], M, N, K)
+        torch.cuda.synchronize()
+        assert O.max_rel_err(res[n].cpu().numpy(), solo.cpu().numpy()) <= 4e-3, n
 
 
 @pytest.mark.parametrize("N", [1, 2, 3])

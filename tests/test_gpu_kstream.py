@@ -3,8 +3,10 @@ each of a workgroup's 8 waves one K chunk, weights streamed per wave through pri
 the waves' tiles summed in LDS by the last arriver; one launch, no split-K partials).
 
 Checked: every format at 5..32 tokens (one and two 16-token tiles, ragged N), K from one
-super-block to the longest the registers hold (K = 4096) including K
-that leaves waves idle or short (K = 768, 1280, 2816); the in-kernel quantization (gq_mmq_ex) and
+super-block to the longest one launch holds (K = 4096) including K that leaves waves idle or short
+(K = 768, 1280, 2816), and longer K in ranges of 16 super-blocks whose fp32 partials a second
+launch sums (K = 4352: a one-super-block range; 8192, 11008, 28672); the in-kernel quantization
+(gq_mmq_ex) and
 the prepared call (act_quant DEQ + the kernel) agree bit for bit; a grouped launch
 (gq_mmq_grouped_ex, mixed formats and K) gives every item's own bits; repeated calls give the
 same bits.  Tolerance: TIGHT (fp16 W x fp16 x~, fp32 MFMA accumulation) against the oracle's IDEAL
@@ -42,7 +44,9 @@ def _check_rows(fmt, qA, B, got, M, N, K, nrows=48, seed=0):
 
 
 CASES = [(4096, 16, 4096), (256, 5, 4096), (1024, 13, 3072), (512, 8, 256), (768, 16, 768), (4096, 32, 4096),
-         (512, 17, 1280), (2048, 24, 2816), (11008, 16, 4096), (64, 9, 1024)]
+         (512, 17, 1280), (2048, 24, 2816), (11008, 16, 4096), (64, 9, 1024),
+         # K ranges (16 super-blocks each) summed by the second launch
+         (1024, 16, 8192), (512, 7, 11008), (256, 32, 4352), (128, 20, 28672)]
 
 
 @pytest.mark.parametrize("fmt", ["q8_0", "q4_k", "q6_k"])
@@ -51,14 +55,14 @@ def test_kstream_parity(fmt, M, N, K, tune):
     import kernels._lib as kl
     tune(GQ_KSTREAM=1)
     t = kl.TYPES[fmt]
-    assert kl.route_name(t, M, N, K) == "kstream_kernel", kl.route_name(t, M, N, K)
+    assert kl.route_name(t, M, N, K).startswith("kstream_kernel"), kl.route_name(t, M, N, K)
     qA = random_blocks(fmt, M, K, seed=M + N + K)
     B = random_activations(N, K, seed=2 * K + N)
     A_t, B_t = _t(qA.view(np.int8)), _t(B)
     C = kl.mmq(t, A_t, B_t, M, N, K)
     ws = torch.empty(kl.workspace_size(t, M, N, K), dtype=torch.uint8, device=_dev())
     kl.act_prepare(B_t, N, K, ws)
-    assert kl.route_name(t, M, N, K, prepared=True) == "kstream_kernel"
+    assert kl.route_name(t, M, N, K, prepared=True).startswith("kstream_kernel")
     Cp = kl.mmq_prepared(t, A_t, ws, M, N, K)
     C2 = kl.mmq(t, A_t, B_t, M, N, K)
     torch.cuda.synchronize()
@@ -67,6 +71,33 @@ def test_kstream_parity(fmt, M, N, K, tune):
     got = C.cpu().numpy()
     assert np.isfinite(got.astype(np.float32)).all()
     _check_rows(fmt, qA, B, got, M, N, K, seed=M)
+
+
+def test_kstream_grouped_prepared_layer(tune):
+    """The 7B Q4_K_M layer's projections at 16 tokens through gq_mmq_grouped_prepared: the K = 4096
+    items and ffn_down (K = 11008, three K ranges) in one K-chunked stream launch + its range sum;
+    every output equals the item's own prepared call, and the oracle within TIGHT on sampled rows."""
+    import kernels._lib as kl
+    N = 16
+    spec = [("q4_k", 4096, 4096), ("q4_k", 1024, 4096), ("q6_k", 2048, 4096), ("q6_k", 4096, 11008)]
+    items, wss, Bs, qAs = [], [], [], []
+    for i, (fmt, M, K) in enumerate(spec):
+        qA = random_blocks(fmt, M, K, seed=300 + i)
+        B = random_activations(N, K, seed=400 + K)
+        ws = torch.empty(kl.workspace_size(kl.TYPES[fmt], M, N, K), dtype=torch.uint8, device=_dev())
+        kl.act_prepare(_t(B), N, K, ws)
+        A_t = _t(qA.view(np.int8))
+        items.append((kl.TYPES[fmt], A_t, ws, M, K, None))
+        qAs.append(qA)
+        Bs.append(B)
+    outs = kl.mmq_grouped_prepared(items, N)
+    assert outs is not None
+    tune(GQ_KSTREAM=1)
+    for i, (fmt, M, K) in enumerate(spec):
+        single = kl.mmq_prepared(kl.TYPES[fmt], items[i][1], items[i][2], M, N, K)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[i].view(torch.int16), single.view(torch.int16)), f"item {i}"
+        _check_rows(fmt, qAs[i], Bs[i], outs[i].cpu().numpy(), M, N, K, nrows=24, seed=i)
 
 
 def test_kstream_grouped_bit_identical(tune):

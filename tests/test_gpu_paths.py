@@ -300,7 +300,7 @@ def test_row_sharded_pipelined_world1(fmt, M, N, K, chunks, tune):
     does not change the arithmetic then)."""
     from dist.row_shard import RowShardedMMQ
     from kernels._lib import TYPES, mmq
-    tune(GQ_GEMM_SPLITS=1)
+    tune(GQ_GEMM_SPLITS=1, GQ_KSTREAM=0)  # (chunks run prepared: keep them off the K-chunked stream too)
     dev = _dev()
     qA = random_blocks(fmt, M, K, seed=M + 3)
     A_t = torch.from_numpy(qA.view(np.int8)).to(dev)

@@ -49,7 +49,7 @@ def _prepared(fmt, qA, B, M, N, K, act="q8_1"):
 @pytest.mark.parametrize("M,N,K", [(256, 128, 256), (300, 100, 1024), (1000, 40, 512), (513, 20, 768),
                                    (64, 16, 4096), (256, 128, 4096), (700, 33, 2048)])
 def test_rgemm_parity(fmt, M, N, K, tune):
-    tune(GQ_RGEMM=1, GQ_SKINNY=0)
+    tune(GQ_RGEMM=1, GQ_SKINNY=0, GQ_KSTREAM=0)
     qA = random_blocks(fmt, M, K, seed=M + N + K)
     B = random_activations(N, K, seed=3 * K + N)
     A_t, B_t = _t(qA.view(np.int8)), _t(B)

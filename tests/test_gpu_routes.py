@@ -14,7 +14,8 @@ pytestmark = pytest.mark.gpu
     ("q4_k", 4096, 16, 4096, False, "rgemm_kernel"),         # ahead of the skinny kernel
     ("q4_k", 11008, 16, 4096, False, "rgemm_kernel"),        # three resident workgroups per CU
     ("q8_0", 11008, 16, 4096, False, "rgemm_kernel"),        # up to four rounds at <= 32 tokens
-    ("q6_k", 11008, 16, 4096, True, "rgemm_kernel"),
+    ("q6_k", 11008, 16, 4096, True, "kstream_kernel"),      # prepared 5..32 tokens, K <= 4096 (round 5)
+    ("q4_k", 4096, 16, 4096, True, "kstream_kernel"),
     ("q4_k", 22016, 16, 4096, False, "rgemm_kernel"),
     ("q8_0", 28672, 16, 8192, False, "skinny_kernel"),        # (more than four rounds)
     ("q6_k", 28672, 16, 8192, True, "sgemm_kernel"),

@@ -17,7 +17,8 @@ pytestmark = pytest.mark.gpu
 CASES = [
     # fmt, M, N, K, the route's first kernel (gq_debug_route)
     ("q8_0", 4096, 128, 4096, "rgemm_kernel"),    # the headline: 16 splits + reduce
-    ("q4_k", 4096, 16, 4096, "rgemm_kernel"),
+    ("q4_k", 4096, 16, 4096, "rgemm_kernel"),     # (prepared: the K-chunked stream)
+    ("q6_k", 8192, 16, 4096, "rgemm_kernel"),
     ("q6_k", 11008, 128, 4096, "sgemm_kernel"),   # streaming GEMM, split-K + reduce
     ("q4_k", 28672, 16, 8192, "skinny_kernel"),
     ("q6_k", 4096, 1, 4096, "stream_decode_kernel"),
@@ -40,6 +41,8 @@ def test_side_stream_and_graph_replay(fmt, M, N, K, first, prepared):
     route = kl.route_name(t, M, N, K, prepared=prepared)
     if prepared and first == "stream_decode_kernel":
         first = "gemv_kernel"  # (the prepared call of a decode shape reads the SOA activations)
+    if prepared and N <= 32 and first == "rgemm_kernel":
+        first = "kstream_kernel"  # (prepared 5..32 tokens: the K-chunked stream, one launch)
     assert route.startswith(first), route
     A = torch.from_numpy(random_blocks(fmt, M, K, seed=M + N).view(np.int8)).to(dev)
     B = torch.from_numpy(random_activations(N, K, seed=K + N)).to(dev)
