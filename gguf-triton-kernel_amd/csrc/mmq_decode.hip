@@ -38,7 +38,7 @@
 namespace gq {
 
 #ifdef GQ_DECODE_STAMPS // diagnostic build: per-wave s_memtime breakdown (never the product)
-__device__ unsigned long long g_dstamps[65536][12];
+__device__ unsigned long long g_dstamps[65536][13];
 #endif
 
 namespace {
@@ -653,6 +653,9 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
         g_dstamps[gw_id][9] = t_c0 ? t_c0 : t_end;
         g_dstamps[gw_id][10] = t_pro;
         g_dstamps[gw_id][11] = (unsigned long long)bx;
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        g_dstamps[gw_id][12] = xcc & 0xfu;
     }
 #endif
 }

@@ -23,7 +23,7 @@ for cfg in sys.argv[1:] or ["q6_k_28672x8192_m1"]:
     for i in range(8):
         r.step(i, i % r.ncopies)
     torch.cuda.synchronize()
-    buf = np.zeros((65536, 12), np.uint64)
+    buf = np.zeros((65536, 13), np.uint64)
     assert kl.lib().gq_debug_decode_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes) == 0
     used = buf[buf[:, 3] > 0].astype(np.float64)
     pro, wait, loop, nt = used[:, 0], used[:, 1], used[:, 2], used[:, 3]
@@ -40,6 +40,15 @@ for cfg in sys.argv[1:] or ["q6_k_28672x8192_m1"]:
     print(f"   kernel span={t1.max() - T0:.0f}  wave starts: med={np.median(t0 - T0):.0f} max={(t0 - T0).max():.0f}  "
           f"ends: med={np.median(t1 - T0):.0f}  first DMA landed after barrier: med={np.median(w0 - tp):.0f}  "
           f"first task compute: med={np.median(c0 - w0):.0f}")
+    # where the spread of wave durations lies: inside a workgroup (one CU) or between workgroups
+    bx, xcc = used[:, 11].astype(np.int64), used[:, 12].astype(np.int64)
+    wmax = np.array([tot[bx == b].max() for b in np.unique(bx)])
+    wmin = np.array([tot[bx == b].min() for b in np.unique(bx)])
+    print(f"   per workgroup: max-min med={np.median(wmax - wmin):.0f} p90={np.percentile(wmax - wmin, 90):.0f};  "
+          f"workgroup max p10/p50/p90/max={np.percentile(wmax, 10):.0f}/{np.median(wmax):.0f}/"
+          f"{np.percentile(wmax, 90):.0f}/{wmax.max():.0f};  workgroup mean med={np.median([tot[bx == b].mean() for b in np.unique(bx)]):.0f}")
+    print("   per XCC: med/max duration " + "  ".join(
+        f"{x}:{np.median(tot[xcc == x]):.0f}/{tot[xcc == x].max():.0f}" for x in np.unique(xcc)))
     for q in (10, 50, 90):
         print(f"   p{q}: start={np.percentile(t0 - T0, q):.0f} barrier={np.percentile(tp - T0, q):.0f} "
               f"dma0={np.percentile(w0 - T0, q):.0f} end={np.percentile(t1 - T0, q):.0f}")
