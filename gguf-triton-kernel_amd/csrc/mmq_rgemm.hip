@@ -22,6 +22,8 @@
 // same x~, v_mfma_f32_16x16x32_f16 in the same (sub-stage, k-step) order into fp32 accumulators;
 // with one split per super-block the split-K partials are written in gemm_kernel's fp16 form and
 // summed by its reduce kernel (launch_gemm_reduce_f16).
+#include <type_traits>
+
 #include "gguf_blocks.hpp"
 #include "gguf_internal.hpp"
 #include "gguf_mfma.hpp"
@@ -292,10 +294,11 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
     const __amdgpu_buffer_rsrc_t wrs =
         __builtin_amdgcn_make_buffer_rsrc((void *)A, 0, (int)(uint32_t)((M * row_bytes + 15) & ~(int64_t)15), 0x00020000);
     uint8_t *const wimg = lds + wave * G::WW;
-    auto issue_w = [&]() __attribute__((always_inline)) {
+    auto issue_w = [&](auto i0c, auto i1c) __attribute__((always_inline)) {
+        constexpr int I0 = decltype(i0c)::value, I1 = decltype(i1c)::value;
         if constexpr (ABL & 1) return;
 #pragma unroll
-        for (int i = 0; i < G::WWI; ++i) {
+        for (int i = I0; i < I1; ++i) {
             const int p = 64 * i + lane, h = p / (32 * G::NPH), rem = p - h * (32 * G::NPH);
             const int r = rem / G::NPH, pc = rem - r * G::NPH;
             const int64_t row = m0 + 32 * wave + r < M ? m0 + 32 * wave + r : M - 1;
@@ -317,8 +320,18 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
             dma16(xrs, lds + G::X_OFF + 1024 * k, vo, (uint32_t)(512 * sb));
         }
     };
+    // AQ: two of the wave's weight DMAs go out before the quantization, the rest after it -- the
+    // wave's in-order issue stalls on the memory pipeline's back-pressure, and with all of them
+    // ahead the quantization (and so the activation barrier) waited behind that stall: Q8_0 4096^2
+    // x128 step 16.76 -> 15.77 us, Q4_K 15.83 -> 15.16, Q6_K 17.67 -> 16.52, Q4_K 11008x4096 x16
+    // 16.07 -> 15.70 (profiles/r05/rgemm_wpre_ab.txt: 0..4 and all before; A/B builds
+    // -DGQ_RGEMM_WPRE=n)
+#ifndef GQ_RGEMM_WPRE
+#define GQ_RGEMM_WPRE 2
+#endif
+    constexpr int WPRE = AQ != 0 && GQ_RGEMM_WPRE < G::WWI ? GQ_RGEMM_WPRE : G::WWI;
     issue_x();
-    issue_w();
+    issue_w(std::integral_constant<int, 0>{}, std::integral_constant<int, WPRE>{});
     GQ_RST(2);
 
     // 4. (AQ) quantize into the image: x~ = fp16(d*q) in act_quant's DEQ order (deq_quad), or the
@@ -339,6 +352,7 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
             *(u32x4 *)(ximg + u * (G::BN * 128) + 128 * r + 16 * (q ^ act_swz(r))) = o;
         }
     }
+    issue_w(std::integral_constant<int, WPRE>{}, std::integral_constant<int, G::WWI>{});
     // the activation image complete (every wave's DMAs, or every wave's quantized pieces): this
     // wave's x loads are older than its weight DMAs, so all but those are awaited
     constexpr int WN = (ABL & 1) ? 0 : G::WWI;
