@@ -39,10 +39,7 @@ struct Tuning {
     int rgemm_spol = 16;                      // GQ_RGEMM_SPOL: its partial stores' cache policy 0 / 2 (nt) / 16 (sc1)
     int sgemm_full = -1;                      // GQ_SGEMM_FULL: Q4_K 16/32-token tiles stream whole super-blocks:
                                               // 1 every streaming GEMM, 0 none, -1 single matrices (measured gain)
-    int fgemm = 0;                            // GQ_FGEMM: full-K tile GEMM 0 off / 1 wherever it applies
     int kstream = -1;                         // GQ_KSTREAM: K-chunked streaming MMQ -1 auto / 0 off / 1 wherever it applies
-    int fgemm_rw = 0;                         // GQ_FGEMM_RW: its row groups of 32 (2/4/8, 0: auto)
-    int fgemm_nb = 0;                         // GQ_FGEMM_NB: its 16-token tiles (2/4, 0: auto)
     int cus = 0;                              // GQ_CUS: compute units to plan for (0: the device's count)
     int ablate = 0;                           // GQ_ABLATE (GQ_ABLATION diagnostic builds only)
 };
@@ -154,17 +151,6 @@ hipError_t launch_rgemm(int fmt, int aq, const uint8_t *A, const uint16_t *X, in
 RGemmPlan plan_sgemm(int64_t M, int64_t N, int64_t K, int splits);
 hipError_t launch_sgemm(int fmt, const uint8_t *A, const uint16_t *X, uint16_t *C, void *partials, const RGemmPlan &p,
                         int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
-
-// Full-K tile GEMM (mmq_fgemm.hip): one workgroup per 32*rw rows x 16*nb tokens x all of K (8
-// waves = rw row groups x 8/rw K-interleaved waves, their partial tiles summed in LDS): no
-// split-K partials, no reduce launch.  Prepared x~ (X = [N][K] DEQ form).  Q8_0 and Q4_K.
-struct FGemmPlan {
-    bool ok = false;
-    int rw = 2, nb = 2;
-};
-FGemmPlan plan_fgemm(int fmt, int64_t M, int64_t N, int64_t K);
-hipError_t launch_fgemm(int fmt, const uint8_t *A, const uint16_t *X, uint16_t *C, const FGemmPlan &p, int64_t M,
-                        int64_t N, int64_t K, int64_t ldc, hipStream_t s);
 
 // Several streaming GEMMs in one launch (+ one grouped split-K reduce), at most 16 items sharing
 // the token count N; X = each item's prepared x~ ([N][K]).  The plan spreads the super-blocks

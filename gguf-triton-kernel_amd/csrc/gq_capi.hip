@@ -98,15 +98,6 @@ bool parse_key(Tuning &t, const char *key, long long v)
     } else if (k == "GQ_CUS") {
         if (v < 0 || v > 1024) return false;
         t.cus = (int)v;
-    } else if (k == "GQ_FGEMM") {
-        if (!in({0, 1})) return false;
-        t.fgemm = (int)v;
-    } else if (k == "GQ_FGEMM_RW") {
-        if (!in({0, 2, 4, 8})) return false;
-        t.fgemm_rw = (int)v;
-    } else if (k == "GQ_FGEMM_NB") {
-        if (!in({0, 2, 4})) return false;
-        t.fgemm_nb = (int)v;
     } else if (k == "GQ_KSTREAM") {
         if (!in({-1, 0, 1})) return false;
         t.kstream = (int)v;
@@ -123,7 +114,7 @@ void tuning_from_env(Tuning &t)
                                        "GQ_GEMM_NB", "GQ_GEMM_RG", "GQ_GEMM_LOADERS", "GQ_GEMM_SPLITS",
                                        "GQ_GEMM_PARTIAL", "GQ_GEMV_CAP", "GQ_GEMV_R", "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D",
                                        "GQ_RGEMM", "GQ_SGEMM", "GQ_SGEMM_SPLITS", "GQ_SGEMM_STREAMK", "GQ_RGEMM_NB", "GQ_RGEMM_SPOL",
-                                       "GQ_SGEMM_FULL", "GQ_FGEMM", "GQ_FGEMM_RW", "GQ_FGEMM_NB", "GQ_CUS", "GQ_KSTREAM",
+                                       "GQ_SGEMM_FULL", "GQ_CUS", "GQ_KSTREAM",
                                        "GQ_ABLATE"};
     for (const char *k : keys) {
         const char *e = getenv(k); // the only getenv of the library: once per process
@@ -302,18 +293,8 @@ bool use_rgemm(int t, int form, int64_t M, int64_t N, int64_t K)
 // The resident GEMM where it applies, ahead of the skinny kernel (4096^2 x16 step: Q4_K 6.8 vs
 // 9.7 us, Q8_0 7.8 vs 11.2, Q6_K 8.1 vs 12.9; x8 Q4_K 6.8 vs 9.3 -- profiles/r04/rg_small.txt)
 // unless the skinny kernel is forced (GQ_SKINNY=1)
-// Full-K tile GEMM (mmq_fgemm.hip): no split-K partials.  GQ_FGEMM=1: wherever it applies
-// (Q8_0 / Q4_K on the fp16 x~ GEMM path, one launch within the 2 GiB operand limit).
-bool use_fgemm(int t, int form, int64_t M, int64_t N, int64_t K)
-{
-    if (gq::tuning().fgemm != 1 || form != gq::AF_F16 || use_gemv(N, K) || use_blas(N, K) || K % 256 != 0) return false;
-    if (gemm_rows_per_launch(t, M, K) < M || gemm_toks_per_launch(N, K) < N) return false;
-    return gq::plan_fgemm(t, M, N, K).ok;
-}
-
 bool rgemm_route(int t, int form, int64_t M, int64_t N, int64_t K, int act)
 {
-    if (use_fgemm(t, form, M, N, K)) return false;
     if (!use_rgemm(t, form, M, N, K)) return false;
     return gq::tuning().skinny != 1 || !use_skinny(t, form, N, act);
 }
@@ -691,11 +672,6 @@ static int compute(gq_type t, int act, const void *A, void *workspace, size_t wo
             if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (kstream): %s", hipGetErrorString(e));
             return GQ_OK;
         }
-        if (use_fgemm(t, r.form, M, N, K)) {
-            e = gq::launch_fgemm(t, (const uint8_t *)A, c.xdeq, (uint16_t *)C, gq::plan_fgemm(t, M, N, K), M, N, K, ldc, s);
-            if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (fgemm): %s", hipGetErrorString(e));
-            return GQ_OK;
-        }
         if (rgemm_route(t, r.form, M, N, K, act)) {
             e = gq::launch_rgemm(t, 0, (const uint8_t *)A, c.xdeq, K, (uint16_t *)C, c.partials, gq::plan_rgemm(M, N, K),
                                  M, N, K, ldc, s);
@@ -787,7 +763,7 @@ int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int6
         return GQ_OK;
     }
     if (!r.gemv && !r.blas && act == GQ_ACT_Q8_1 && r.form == gq::AF_F16 && !use_skinny(t, r.form, N) &&
-        !use_sgemm(t, r.form, M, N, K) && !use_fgemm(t, r.form, M, N, K) &&
+        !use_sgemm(t, r.form, M, N, K) &&
         gemm_rows_per_launch(t, M, K) >= M &&
         gemm_toks_per_launch(N, K) >= N) {
         // 16/32-token tiles whose split fits LDS: the GEMM quantizes the activations itself (no
@@ -1179,7 +1155,6 @@ const char *gq_debug_route(gq_type t, gq_act act, int64_t M, int64_t N, int64_t 
     if (r.gemv) return "gemv_kernel";
     if (use_kstream(t, r.form, M, N, K, act, prepared != 0))
         return gq::kstream_splits(K) > 1 ? "kstream_kernel + kstream_reduce_kernel" : "kstream_kernel";
-    if (use_fgemm(t, r.form, M, N, K)) return "fgemm_kernel";
     if (rgemm_route(t, r.form, M, N, K, act)) return "rgemm_kernel + gemm_reduce_f16_kernel";
     if (use_skinny(t, r.form, N, act)) return "skinny_kernel";
     if (use_sgemm(t, r.form, M, N, K)) {
