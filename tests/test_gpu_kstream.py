@@ -46,7 +46,10 @@ def _check_rows(fmt, qA, B, got, M, N, K, nrows=48, seed=0):
 CASES = [(4096, 16, 4096), (256, 5, 4096), (1024, 13, 3072), (512, 8, 256), (768, 16, 768), (4096, 32, 4096),
          (512, 17, 1280), (2048, 24, 2816), (11008, 16, 4096), (64, 9, 1024),
          # K ranges (16 super-blocks each) summed by the second launch
-         (1024, 16, 8192), (512, 7, 11008), (256, 32, 4352), (128, 20, 28672)]
+         (1024, 16, 8192), (512, 7, 11008), (256, 32, 4352), (128, 20, 28672),
+         # edges: one 16-row item, one super-block (seven of the eight waves idle), the fewest
+         # and the most tokens of the two token-group kernels
+         (16, 5, 256), (16, 32, 256), (48, 31, 512), (32, 17, 4096)]
 
 
 @pytest.mark.parametrize("fmt", ["q8_0", "q4_k", "q6_k"])
