@@ -302,12 +302,12 @@ bool rgemm_route(int t, int form, int64_t M, int64_t N, int64_t K, int act)
 // K-chunked streaming MMQ (mmq_kstream.hip): 5..32 tokens (the fp8 variant from 3: its decode
 // form covers 1..2), K % 256 == 0, M % 16 == 0; one launch for K <= 4096 (x~ quantized in-kernel
 // from the raw activations, or read prepared).  GQ_KSTREAM=1: wherever it applies, 0: off.
-// By default on the prepared calls (x~ read as act_quant wrote it; single and grouped): 5..32
-// tokens measured 7-12% under the routes before it (MMQ us, default -> kstream, round 5
+// By default on the prepared calls (x~ read as act_quant wrote it; single and grouped) and the
+// raw grouped launch: 5..32 tokens measured 7-12% under the routes before it (MMQ us, default -> kstream, round 5
 // profiles/r05/ks_ab.txt: Q4_K 4096^2 x16 9.25 -> 7.96, 11008x4096 x16 15.31 -> 13.65,
 // 22016x4096 x16 24.23 -> 22.12, x32 30.52 -> 27.72, x8 24.02 -> 21.69; Q6_K 4096^2 x16 10.55 ->
 // 9.32; Q8_0 11008x4096 x16 18.05 -> 16.90).  Quantizing in-kernel (gq_mmq_ex) it is slower on the
-// small matrices (every workgroup quantizes its whole K of x), so the raw call keeps its routes.
+// small matrices (every workgroup quantizes its whole K of x): a raw call takes it on the tall ones.
 // A K longer than 4096 is cut into ranges summed by a second launch (fp32 partials in the
 // workspace): by default only inside a grouped launch (the layer's ffn_down beside the K = 4096
 // projections); split = false asks for the one-launch form.
@@ -318,8 +318,13 @@ bool use_kstream(int t, int form, int64_t M, int64_t N, int64_t K, int act, bool
     if (ks == 0 || form != gq::AF_F16 || use_blas(N, K) || !gq::kstream_ok(t, M, N, K)) return false;
     if (N < (act == GQ_ACT_FP8_E4M3 ? 3 : 5)) return false;
     if (gq::kstream_splits(K) > 1 && !split && ks != 1) return false;
-    if (ks == 1) return true;
-    return prepared;
+    if (ks == 1 || prepared) return true;
+    // a raw call quantizes in-kernel (every workgroup its whole K of x): ahead of the resident GEMM
+    // on the tall matrices at 5..16 tokens (Q4_K 11008 / 14336 / 22016 x4096 x16 15.79 / 17.74 /
+    // 25.14 -> 15.41 / 17.36 / 23.23 us, Q6_K 11008 19.79 -> 19.15, Q8_0 11008 18.69 -> 18.33, x8
+    // 15.61 -> 15.37), behind it on 4096-row matrices (9.27 -> 11.18) and at 32 tokens (18.51 ->
+    // 23.98) -- profiles/r05/raw_kstream_ab.txt
+    return act == GQ_ACT_Q8_1 && N <= 16 && M >= 8192;
 }
 size_t kstream_ws(int t, int64_t M, int64_t N, int64_t K)
 {
@@ -999,7 +1004,8 @@ int gq_mmq_grouped_ex(gq_act act, const gq_group_item *items, int n, int64_t N, 
         gq::KItem ki[16];
         for (int i = 0; i < m; ++i) {
             const gq::DecodeItem &d = di[i];
-            if (!use_kstream(d.fmt, gq::AF_F16, d.M, N, d.K, act) || gq::kstream_splits(d.K) > 1 || d.ldx % 8 != 0 ||
+            // (the grouped launch's own route: the stream wherever it applies, GQ_KSTREAM=0 refuses)
+            if (!use_kstream(d.fmt, gq::AF_F16, d.M, N, d.K, act, true) || gq::kstream_splits(d.K) > 1 || d.ldx % 8 != 0 ||
                 ((uintptr_t)d.X & 15) != 0 || !kstream_fits(d.M, N, d.K, d.ldx, d.ldc))
                 return fail(GQ_EUNSUPPORTED, "item %d: not a grouped K-chunked-stream shape (N=%lld, M=%lld, K=%lld)", i,
                             (long long)N, (long long)d.M, (long long)d.K);

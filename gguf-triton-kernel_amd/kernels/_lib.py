@@ -285,12 +285,13 @@ def mmq(gtype: int, A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int,
 
 
 def mmq_grouped(items, N: int, act: str = "q8_1"):
-    """One grouped decode launch (gq_mmq_grouped_ex) for several MMQs with the same token count N
-    (1..4; act="fp8": 1..2): items = [(gtype, A, B, M, K, out or None), ...], every B an fp16
-    (N, K) tensor.
-    Returns the (N, M) outputs (bit-identical to mmq() per item), or None when the library
-    reports the shapes unsupported (N > 4, or an item that is no one-launch decode shape) --
-    nothing was launched then and the caller runs mmq() per item."""
+    """One grouped launch (gq_mmq_grouped_ex) for several MMQs with the same token count N:
+    items = [(gtype, A, B, M, K, out or None), ...], every B an fp16 (N, K) tensor.  1..4 tokens
+    (act="fp8": 1..2): the streaming decode kernel, bit-identical to mmq() per item; 5..32 (fp8:
+    3..32): the K-chunked streaming MMQ (K <= 4096, M % 16 == 0), bit-identical to each item's
+    call on that kernel.  Returns the (N, M) outputs, or None when the library reports the shapes
+    unsupported (N > 32, or an item that is no shape of the launch) -- nothing was launched then
+    and the caller runs mmq() per item."""
     if not items:
         return []
     dev = items[0][1].device

@@ -87,9 +87,10 @@ int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int6
  * Same result as gq_mmq within the stated tolerances, not always the same kernels: for
  * N <= 4 gq_mmq runs the one-launch fused decode kernel (quantizer in LDS) while the split
  * form quantizes to the workspace and runs the decode-shaped GEMV; at N = 5..32 (K <= 4096,
- * M % 16 == 0) the split form runs the K-chunked streaming MMQ while gq_mmq keeps the resident
- * GEMM (the same x~ and products, summed over K in another fp32 order: within 4e-3, not bit for
- * bit; GQ_KSTREAM=1 puts both on the stream, GQ_KSTREAM=0 both off it, and then the bits match);
+ * M % 16 == 0) the split form runs the K-chunked streaming MMQ, and gq_mmq does too at N <= 16 on
+ * M >= 8192 rows, else the resident GEMM (the same x~ and products, summed over K in another fp32
+ * order: within 4e-3, not bit for bit; GQ_KSTREAM=1 puts both on the stream, GQ_KSTREAM=0 both
+ * off it, and then the bits match);
  * for Q8_0 with the int8 GEMM form enabled (GQ_GEMM_I8=1) gq_act_prepare writes both activation
  * forms.
  */

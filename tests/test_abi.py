@@ -211,7 +211,7 @@ def test_grouped_host_argument_checks():
     arr[1] = kl.GroupItem(7, fake, fake, 4096, fake, 4096, 4096, 4096)           # unknown type
     assert L.gq_mmq_grouped(arr, 2, 1, None) != kl.GQ_OK
     arr[1] = kl.GroupItem(kl.GQ_Q4_K, fake, fake, 4096, fake, 4096, 0, 4096)     # M = 0: skipped
-    assert L.gq_mmq_grouped(arr, 2, 5, None) == kl.GQ_EUNSUPPORTED              # N = 5: not decode
+    assert L.gq_mmq_grouped(arr, 2, 33, None) == kl.GQ_EUNSUPPORTED             # N = 33: no grouped form
     arr[1] = kl.GroupItem(kl.GQ_Q4_K, None, fake, 4096, fake, 4096, 64, 4096)    # null A
     assert L.gq_mmq_grouped(arr, 2, 1, None) == kl.GQ_EINVAL
 

@@ -107,17 +107,21 @@ def test_grouped_mixed_formats_strides():
 
 
 def test_grouped_refuses_non_decode_shapes():
-    """N = 5 (not a decode size) and an item whose activations do not fit LDS: refused (None),
-    nothing launched, the output untouched; mmq() per item is the caller's path then."""
+    """N = 33 (past the grouped forms: decode 1..4, K-chunked stream 5..32), M = 40 at 8 tokens (not
+    whole 16-row items) and an item whose activations do not fit LDS: refused (None), nothing
+    launched, the output untouched; mmq() per item is the caller's path then."""
     import kernels._lib as kl
     dev = _dev()
     qA = torch.from_numpy(random_blocks("q4_k", 64, 1024, seed=1).view(np.int8)).to(dev)
-    for N, K in ((5, 1024),):
+    for N, K in ((33, 1024),):
         B = torch.from_numpy(random_activations(N, K, seed=2)).to(dev)
         out = torch.full((N, 64), 3.0, dtype=torch.float16, device=dev)
         assert kl.mmq_grouped([(kl.GQ_Q4_K, qA, B, 64, K, out)], N) is None
         torch.cuda.synchronize()
         assert torch.all(out == 3.0)
+    qC = torch.from_numpy(random_blocks("q4_k", 40, 1024, seed=5).view(np.int8)).to(dev)
+    B = torch.from_numpy(random_activations(8, 1024, seed=6)).to(dev)
+    assert kl.mmq_grouped([(kl.GQ_Q4_K, qC, B, 40, 1024, None)], 8) is None
     K = 131072  # 4 tokens x 128K codes: no room in LDS beside the ring
     qB = torch.from_numpy(random_blocks("q8_0", 16, K, seed=3).view(np.int8)).to(dev)
     B = torch.from_numpy(random_activations(4, K, seed=4)).to(dev)

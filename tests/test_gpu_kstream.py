@@ -140,3 +140,28 @@ def test_kstream_fp8_matches_prepared_f8deq(tune):
         Cp = kl.mmq_prepared(t, A_t, ws, M, N, K, act="fp8")
         torch.cuda.synchronize()
         assert torch.equal(C.view(torch.int16), Cp.view(torch.int16)), fmt
+
+def test_kstream_grouped_default_tuning():
+    """gq_mmq_grouped at 5..32 tokens under the default tuning takes the K-chunked stream (its
+    own route: no GQ_KSTREAM needed) and gives each item's stream bits (the raw call pinned to the
+    stream, GQ_KSTREAM=1, for the 4096-row items the default sends to the resident GEMM)."""
+    import kernels._lib as kl
+    N = 12
+    spec = [("q4_k", 4096, 4096), ("q6_k", 1024, 4096), ("q8_0", 8192, 2816)]
+    xs = {K: _t(random_activations(N, K, seed=K + 1)) for K in (4096, 2816)}
+    items, As = [], []
+    for i, (fmt, M, K) in enumerate(spec):
+        A_t = _t(random_blocks(fmt, M, K, seed=200 + i).view(np.int8))
+        items.append((kl.TYPES[fmt], A_t, xs[K], M, K, None))
+        As.append(A_t)
+    outs = kl.mmq_grouped(items, N)
+    assert outs is not None, kl.lib().gq_last_error()
+    torch.cuda.synchronize()
+    kl.set_tuning("GQ_KSTREAM", 1)
+    try:
+        for i, (fmt, M, K) in enumerate(spec):
+            solo = kl.mmq(kl.TYPES[fmt], As[i], xs[K], M, N, K)
+            torch.cuda.synchronize()
+            assert torch.equal(outs[i].view(torch.int16), solo.view(torch.int16)), f"item {i}"
+    finally:
+        kl.reset_tuning()

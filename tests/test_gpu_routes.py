@@ -12,11 +12,13 @@ pytestmark = pytest.mark.gpu
     ("q8_0", 4096, 128, 4096, False, "rgemm_kernel"),        # the headline: resident split, q8_1 in-kernel
     ("q4_k", 4096, 128, 4096, True, "rgemm_kernel"),
     ("q4_k", 4096, 16, 4096, False, "rgemm_kernel"),         # ahead of the skinny kernel
-    ("q4_k", 11008, 16, 4096, False, "rgemm_kernel"),        # three resident workgroups per CU
-    ("q8_0", 11008, 16, 4096, False, "rgemm_kernel"),        # up to four rounds at <= 32 tokens
+    ("q4_k", 11008, 16, 4096, False, "kstream_kernel"),      # raw 5..16 tokens on >= 8192 rows (round 5)
+    ("q8_0", 11008, 16, 4096, False, "kstream_kernel"),
+    ("q4_k", 11008, 32, 4096, False, "rgemm_kernel"),        # up to four resident rounds at <= 32 tokens
     ("q6_k", 11008, 16, 4096, True, "kstream_kernel"),      # prepared 5..32 tokens, K <= 4096 (round 5)
     ("q4_k", 4096, 16, 4096, True, "kstream_kernel"),
-    ("q4_k", 22016, 16, 4096, False, "rgemm_kernel"),
+    ("q4_k", 22016, 16, 4096, False, "kstream_kernel"),
+    ("q4_k", 22016, 24, 4096, False, "rgemm_kernel"),
     ("q8_0", 28672, 16, 8192, False, "skinny_kernel"),        # (more than four rounds)
     ("q6_k", 28672, 16, 8192, True, "sgemm_kernel"),
     ("q6_k", 28672, 128, 8192, True, "sgemm_kernel"),

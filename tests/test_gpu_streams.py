@@ -18,7 +18,7 @@ CASES = [
     # fmt, M, N, K, the route's first kernel (gq_debug_route)
     ("q8_0", 4096, 128, 4096, "rgemm_kernel"),    # the headline: 16 splits + reduce
     ("q4_k", 4096, 16, 4096, "rgemm_kernel"),     # (prepared: the K-chunked stream)
-    ("q6_k", 8192, 16, 4096, "rgemm_kernel"),
+    ("q6_k", 8192, 16, 4096, "kstream_kernel"),   # raw and prepared: the K-chunked stream (8192+ rows)
     ("q6_k", 11008, 128, 4096, "sgemm_kernel"),   # streaming GEMM, split-K + reduce
     ("q4_k", 28672, 16, 8192, "skinny_kernel"),
     ("q6_k", 4096, 1, 4096, "stream_decode_kernel"),
