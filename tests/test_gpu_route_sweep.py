@@ -69,3 +69,23 @@ def test_grouped_accepts_its_shapes(N):
             assert torch.equal(o.view(torch.int16), r.view(torch.int16)), i
         else:
             assert O.max_rel_err(o.cpu().numpy(), r.cpu().numpy().astype(np.float32)) <= GEMM_TOL, i
+
+
+@pytest.mark.parametrize("fmt", ["q8_0", "q4_k", "q6_k"])
+@pytest.mark.parametrize("M,K", [(512, 4096), (8192, 4096)])
+def test_fp8_raw_and_prepared_agree_over_token_counts(fmt, M, K):
+    """The fp8 activation variant: the same sweep (its decode form at 1..2 tokens, the K-chunked
+    stream and the fp16-x~ kernels from 3)."""
+    import kernels._lib as kl
+    t = kl.TYPES[fmt]
+    A = _t(random_blocks(fmt, M, K, seed=M + K + 1).view(np.int8))
+    for N in (1, 2, 3, 5, 16, 33, 128):
+        B = _t(random_activations(N, K, seed=N + 2 * K))
+        raw = kl.mmq(t, A, B, M, N, K, act="fp8")
+        ws = torch.empty(kl.workspace_size(t, M, N, K, act="fp8"), dtype=torch.uint8, device=_dev())
+        kl.act_prepare(B, N, K, ws, act="fp8")
+        prep = kl.mmq_prepared(t, A, ws, M, N, K, act="fp8")
+        torch.cuda.synchronize()
+        r, p = raw.cpu().numpy(), prep.cpu().numpy()
+        assert np.isfinite(r.astype(np.float32)).all(), (fmt, M, N, K)
+        assert O.max_rel_err(p, r.astype(np.float32)) <= GEMM_TOL, (fmt, M, N, K, kl.route_name(t, M, N, K, act="fp8"))
