@@ -432,7 +432,7 @@ template <int F, int NB> struct SCfg {
     static constexpr int SLOT = W_BYTES + X_BYTES;
     static constexpr int WH_INSTR = (RBM * NPH + 63) / 64, NWH = (WH_INSTR + RW - 1) / RW;
     static constexpr int XH_INSTR = X_BYTES / 1024, NXH = (XH_INSTR + RW - 1) / RW;
-    static constexpr int NPS = ((ABL & 1) ? 0 : NWH) + NXH; // DMA instructions per wave and stage
+    static constexpr int NPS = ((ABL & 1) ? 0 : NWH) + ((ABL & 2) ? 0 : NXH); // DMA instructions per wave and stage
     static constexpr bool PAD = WH_INSTR % RW != 0 || XH_INSTR % RW != 0 || XH_INSTR < RW;
     static constexpr int NS = (LDS_CAP - 1024) / SLOT > SG_NSMAX ? SG_NSMAX : (LDS_CAP - 1024) / SLOT; // ring slots
     static constexpr int SCRATCH = NS * SLOT;
@@ -509,7 +509,7 @@ __device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const 
         }
         // activation half image: piece P = 64k + lane: sub-stage ul = P / (BN*8), token r, slot qd
 #pragma unroll
-        for (int i = 0; i < G::NXH; ++i) {
+        for (int i = 0; i < ((ABL & 2) ? 0 : G::NXH); ++i) {
             const int k = wave + RW * i, pp = 64 * k + lane;
             const bool real = k < G::XH_INSTR;
             const int ul = pp / (G::BN * 8), r = (pp / 8) % G::BN, qd = pp & 7, q = qd ^ act_swz(r);
