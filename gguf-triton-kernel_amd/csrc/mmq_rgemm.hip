@@ -64,12 +64,23 @@ constexpr int LDS_CAP = 160 * 1024;
 // hsrc<F>(h, pc):
 //   Q8_0  9 pieces from byte 128h (blocks 4h..4h+3 at image byte 8h..; 8 bytes of overlap)
 //   Q4_K  5 pieces: the 16-byte header, then qs bytes 64h..64h+63
-//   Q6_K  9 pieces: ql 64h.. (4), qh 128+32h.. (2), bytes 192..207 (scales), 194..209 (d at image
-//         byte 126), the last again (padding to 144 B: a 128-B stride is 2 bank sets)
+//   Q6_K  8 pieces: ql 64h.. (4), qh 128+32h.. (2), bytes 192..207 (scales), 194..209 (d at image
+//         byte 126); a 128-B stride is 2 bank sets, so row r's pieces are XOR-permuted by r & 7
+//         (hpos_swz).  (Until round 5 a ninth padding piece made the stride 144 B instead; the 8
+//         pieces move 11% fewer weight DMA instructions: Q6_K 70B x128 -3%, profiles/r05/q6k_nph8_ab.txt)
 template <int F> struct HImg;
 template <> struct HImg<Q8_0> { static constexpr int NPH = 9; };
 template <> struct HImg<Q4_K> { static constexpr int NPH = 5; };
-template <> struct HImg<Q6_K> { static constexpr int NPH = 9; };
+#ifndef GQ_Q6_NPH
+#define GQ_Q6_NPH 8 // (-DGQ_Q6_NPH=9: the padded image, A/B builds)
+#endif
+template <> struct HImg<Q6_K> { static constexpr int NPH = GQ_Q6_NPH; };
+// Q6_K with 8 pieces (no padding piece): the 128-B row stride puts rows r and r+2 on the same
+// banks, so piece pc of row r lands at position pc ^ (r & 7) (2-way at most)
+template <int F> __device__ __forceinline__ int hpos_swz(int r)
+{
+    return F == Q6_K && HImg<F>::NPH == 8 ? (r & 7) : 0;
+}
 template <int F> __device__ __forceinline__ uint32_t hsrc(int h, int pc)
 {
     if constexpr (F == Q8_0) return 128u * h + 16u * pc;
@@ -115,11 +126,32 @@ template <int F> __device__ __forceinline__ void block_piece(int kb, int j, int 
 }
 
 // A fragments of sub-stage u (half h = u >> 1) for the row whose half image starts at img
-template <int F> __device__ __forceinline__ void half_frags(const uint8_t *img, int g, int u, f16x8 (&frag)[2])
+// (the Q6_K half image's fragments with its pieces at pc ^ sw: q6k_half_frags' arithmetic)
+__device__ __forceinline__ void q6k_half_frags_swz(const uint8_t *img, int g, int h, int v, int sw, f16x8 (&frag)[2])
+{
+    auto at = [sw](int off) { return (((off >> 4) ^ sw) << 4) | (off & 15); };
+    const float d = h2f(*(const uint16_t *)(img + at(126)));
+    const u32x2 ql = *(const u32x2 *)(img + at(32 * v + 8 * g));
+    const u32x2 qh = *(const u32x2 *)(img + at(64 + 8 * g));
+    const h2 bias = splat(-1056.f); // 1024 + 32
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+        const float scv = (float)*(const int8_t *)(img + at(96 + 8 * h + 4 * n + 2 * v + (g >> 1)));
+        const h2 dsc = splat(d * scv);
+        const int sq = 4 * n + 2 * v;
+        const uint32_t c0 = ((ql.x >> (4 * n)) & 0x0f0f0f0fu) | (((qh.x >> sq) & 0x03030303u) << 4);
+        const uint32_t c1 = ((ql.y >> (4 * n)) & 0x0f0f0f0fu) | (((qh.y >> sq) & 0x03030303u) << 4);
+        frag[n] = frag4((pair02(c0) + bias) * dsc, (pair13(c0) + bias) * dsc, (pair02(c1) + bias) * dsc,
+                        (pair13(c1) + bias) * dsc);
+    }
+}
+
+template <int F> __device__ __forceinline__ void half_frags(const uint8_t *img, int g, int u, int r, f16x8 (&frag)[2])
 {
     const int h = u >> 1;
     if constexpr (F == Q8_0) stage_frags<Q8_0>(img - 128 * h, g, u, frag, 0); // (16-byte aligned: HRB = 144)
     else if constexpr (F == Q4_K) q4k_frags(img, img + 16 + 32 * (u & 1), g, u, frag);
+    else if constexpr (HImg<F>::NPH == 8) q6k_half_frags_swz(img, g, h, u & 1, hpos_swz<F>(r), frag);
     else q6k_half_frags(img, g, h, u & 1, frag);
 }
 
@@ -139,7 +171,7 @@ __device__ __forceinline__ void mul_substage(const uint8_t *wimg, const uint8_t 
     f16x8 af[RRG][2];
 #pragma unroll
     for (int rg = 0; rg < RRG; ++rg)
-        half_frags<F>(wimg + (16 * HImg<F>::NPH) * (rbase + 16 * rg + l16), g, u, af[rg]);
+        half_frags<F>(wimg + (16 * HImg<F>::NPH) * (rbase + 16 * rg + l16), g, u, l16, af[rg]);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
         f16x8 bk[NB];
@@ -300,7 +332,7 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
 #pragma unroll
         for (int i = I0; i < I1; ++i) {
             const int p = 64 * i + lane, h = p / (32 * G::NPH), rem = p - h * (32 * G::NPH);
-            const int r = rem / G::NPH, pc = rem - r * G::NPH;
+            const int r = rem / G::NPH, pc = (rem - r * G::NPH) ^ hpos_swz<F>(r);
             const int64_t row = m0 + 32 * wave + r < M ? m0 + 32 * wave + r : M - 1;
             dma16(wrs, wimg + 1024 * i, (uint32_t)(row * row_bytes) + hsrc<F>(h, pc), (uint32_t)(G::SB * sb)); // (+16 lane)
         }
@@ -501,7 +533,7 @@ __device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const 
         const int h = j & 1;
 #pragma unroll
         for (int i = 0; i < ((ABL & 1) ? 0 : G::NWH); ++i) {
-            const int k = wave + RW * i, p = 64 * k + lane, r = p / G::NPH, pc = p - r * G::NPH;
+            const int k = wave + RW * i, p = 64 * k + lane, r = p / G::NPH, pc = (p - r * G::NPH) ^ hpos_swz<F>(r);
             const bool real = k < G::WH_INSTR;
             const int64_t row = m0 + r < M ? m0 + r : M - 1;
             const uint32_t vo = real ? (uint32_t)(row * row_bytes) + hsrc<F>(h, pc) : 0u;

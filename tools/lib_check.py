@@ -1,5 +1,5 @@
 """Parity of a diagnostic build of libgguf_mmq.so: each config's raw call against the same
-library's call with the streaming GEMM switched off (GQ_SGEMM=0: another kernel, other fp32
+library's call with the streaming, resident and K-chunked GEMMs switched off (another kernel, other fp32
 summation order): max |difference| over max |reference| (the GEMM tolerance is 4e-3).
 
 Usage: python tools/lib_check.py --lib=PATH CONFIG ...   (CONFIG: fmt_MxK_mN)
@@ -35,6 +35,8 @@ for cfg in args:
     route = kl.route_name(t, M, N, K)
     out = kl.mmq(t, A, B, M, N, K).float().cpu().numpy()
     kl.set_tuning("GQ_SGEMM", 0)
+    kl.set_tuning("GQ_RGEMM", 0)
+    kl.set_tuning("GQ_KSTREAM", 0)
     ref = kl.mmq(t, A, B, M, N, K).float().cpu().numpy()
     alt = kl.route_name(t, M, N, K)
     kl.reset_tuning()
