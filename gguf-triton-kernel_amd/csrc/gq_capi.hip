@@ -413,13 +413,23 @@ size_t deq_bytes(int64_t N, int64_t K) { return align_up((size_t)N * K * 2); }
 size_t code_bytes(int64_t N, int64_t K) { return align_up((size_t)N * K); }
 size_t scale_bytes(int64_t N, int64_t K) { return align_up((size_t)(K / 32) * (size_t)scale_ld(N) * 4); }
 
+// Decode token counts (q8_1: the GEMV tokens, fp8: 1-2): gq_act_prepare also keeps an fp16 copy
+// of the activations at the end of the activation part, so that gq_mmq_prepared runs the same
+// one-launch decode as gq_mmq (bit-identical to it) instead of the GEMV on the SOA form (Q6_K
+// 28672x8192 x1 60.6 -> 35.4 us; profiles/r05/prepared_decode_ab.txt)
+bool prep_raw(int act, int64_t N, int64_t K)
+{
+    return act == GQ_ACT_FP8_E4M3 ? N <= 2 && gq::gemm_supported(gq::Q8_0, K) : use_gemv(N, K);
+}
+size_t raw_bytes(int act, int64_t N, int64_t K) { return prep_raw(act, N, K) ? align_up((size_t)N * K * 2) : 0; }
+
 // Activation part of the workspace (what gq_act_prepare[_ex] writes); depends on act, N, K only.
 size_t act_bytes(int act, int64_t N, int64_t K)
 {
-    if (act == GQ_ACT_FP8_E4M3) return deq_bytes(N, K); // the fp8 variant's x~
+    if (act == GQ_ACT_FP8_E4M3) return deq_bytes(N, K) + raw_bytes(act, N, K); // the fp8 variant's x~
     if (use_gemv(N, K)) {
         // SOA q8_1: codes + d + s
-        return align_up((size_t)N * K) + 2 * align_up((size_t)N * (K / 32) * sizeof(float));
+        return align_up((size_t)N * K) + 2 * align_up((size_t)N * (K / 32) * sizeof(float)) + raw_bytes(act, N, K);
     }
     return deq_bytes(N, K) + code_bytes(N, K) + 2 * scale_bytes(N, K); // (+ s: the integer skinny kernel)
 }
@@ -596,6 +606,7 @@ struct Carved {
     int8_t *xq;       // SOA codes (decode) / GEMM codes (int8 form, fp8 variant)
     float *xd, *xs;   // SOA d, s (decode) / GEMM block-major scales
     uint16_t *xdeq;
+    uint16_t *xraw;   // decode token counts: the fp16 activations (rows K apart; prep_raw)
     float *partials;
 };
 
@@ -603,6 +614,7 @@ static Carved carve(int act, void *workspace, int64_t N, int64_t K)
 {
     uint8_t *ws = (uint8_t *)workspace;
     Carved c{};
+    if (prep_raw(act, N, K)) c.xraw = (uint16_t *)(ws + act_bytes(act, N, K) - raw_bytes(act, N, K));
     if (act == GQ_ACT_FP8_E4M3) {
         c.xdeq = (uint16_t *)ws;
     } else if (use_gemv(N, K)) {
@@ -641,6 +653,8 @@ static int prepare(int act, const void *B, int64_t N, int64_t K, int64_t ldb, vo
         if (e == hipSuccess && (forms & 2))
             e = gq::launch_act_quant(gq::ACT_I8, (const uint16_t *)B, ldb, N, K, c.xq, c.xd, (forms & 4) ? c.xs : nullptr, s);
     }
+    if (e == hipSuccess && c.xraw)
+        e = hipMemcpy2DAsync(c.xraw, (size_t)K * 2, B, (size_t)ldb * 2, (size_t)K * 2, (size_t)N, hipMemcpyDeviceToDevice, s);
     if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (act_quant): %s", hipGetErrorString(e));
     return GQ_OK;
 }
@@ -654,6 +668,12 @@ static int compute(gq_type t, int act, const void *A, void *workspace, size_t wo
     if (workspace_bytes < need) return fail(GQ_EINVAL, "workspace %zu bytes < required %zu", workspace_bytes, need);
     const Route r = route(t, act, N, K);
     Carved c = carve(act, workspace, N, K);
+    if (c.xraw && fused_decode_route(t, act, N, K)) { // gq_mmq's one-launch decode on the prepared copy
+        const hipError_t e = gq::launch_decode_fused(t, (const uint8_t *)A, c.xraw, K, (uint16_t *)C, M, N, K, ldc, s,
+                                                     act == GQ_ACT_FP8_E4M3);
+        if (e != hipSuccess) return fail(GQ_EHIP, "HIP launch failed (decode): %s", hipGetErrorString(e));
+        return GQ_OK;
+    }
     if (r.blas) {
         uint16_t *W = (uint16_t *)c.partials; // after the activations: fp16 W, then the BLAS workspace
         uint8_t *bws = (uint8_t *)W + align_up((size_t)M * K * 2);
@@ -861,7 +881,13 @@ int gq_act_prepare_grouped(gq_act act, const gq_prep_item *items, int n, void *s
         }
         if (ns == gq::kMaxDeqSegs && (rc = flush()) != GQ_OK) return rc;
         // the fp16 x~ form sits at the front of the workspace (carve)
-        segs[ns++] = gq::DeqSeg{(const uint16_t *)it.B, it.ldb, N, K, carve(act, it.workspace, N, K).xdeq, 0};
+        const Carved c = carve(act, it.workspace, N, K);
+        segs[ns++] = gq::DeqSeg{(const uint16_t *)it.B, it.ldb, N, K, c.xdeq, 0};
+        if (c.xraw) { // (fp8 at 1-2 tokens: the decode's copy, as prepare())
+            const hipError_t e = hipMemcpy2DAsync(c.xraw, (size_t)K * 2, it.B, (size_t)it.ldb * 2, (size_t)K * 2,
+                                                  (size_t)N, hipMemcpyDeviceToDevice, s);
+            if (e != hipSuccess) return fail(GQ_EHIP, "HIP copy failed (grouped act_quant): %s", hipGetErrorString(e));
+        }
     }
     return flush();
 }
@@ -1156,7 +1182,7 @@ const char *gq_debug_route(gq_type t, gq_act act, int64_t M, int64_t N, int64_t 
     if (check_common(t, M, N, K) != GQ_OK || check_act(act, K) != GQ_OK || M <= 0 || N <= 0 || K <= 0) return "none";
     g_err.clear();
     const Route r = route(t, act, N, K);
-    if (!prepared && fused_decode_route(t, act, N, K)) return "stream_decode_kernel";
+    if (fused_decode_route(t, act, N, K) && (!prepared || prep_raw(act, N, K))) return "stream_decode_kernel";
     if (r.blas) return "dequant_kernel + hipBLASLt";
     if (r.gemv) return "gemv_kernel";
     if (use_kstream(t, r.form, M, N, K, act, prepared != 0))

@@ -85,8 +85,10 @@ int gq_mmq_ex(gq_type t, gq_act act, const void *A, const void *B, void *C, int6
  * gq_mmq_workspace_size(t, M, N, K) bytes in total) for split-K partial sums.  One prepare
  * can serve several weight matrices that share an input (Q/K/V, gate/up).
  * Same result as gq_mmq within the stated tolerances, not always the same kernels: for
- * N <= 4 gq_mmq runs the one-launch fused decode kernel (quantizer in LDS) while the split
- * form quantizes to the workspace and runs the decode-shaped GEMV; at N = 5..32 (K <= 4096,
+ * N <= 4 (fp8: N <= 2) gq_act_prepare also keeps an fp16 copy of B in the workspace and
+ * gq_mmq_prepared runs gq_mmq's one-launch fused decode on it -- the same kernel and bits as
+ * gq_mmq (round 5; the split form ran the decode-shaped GEMV on the SOA q8_1 form before, and
+ * still does where the fused decode does not fit, e.g. 4 tokens at K = 11008); at N = 5..32 (K <= 4096,
  * M % 16 == 0) the split form runs the K-chunked streaming MMQ, and gq_mmq does too at N <= 16 on
  * M >= 8192 rows, else the resident GEMM (the same x~ and products, summed over K in another fp32
  * order: within 4e-3, not bit for bit; GQ_KSTREAM=1 puts both on the stream, GQ_KSTREAM=0 both

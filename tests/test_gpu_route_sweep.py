@@ -89,3 +89,24 @@ def test_fp8_raw_and_prepared_agree_over_token_counts(fmt, M, K):
         r, p = raw.cpu().numpy(), prep.cpu().numpy()
         assert np.isfinite(r.astype(np.float32)).all(), (fmt, M, N, K)
         assert O.max_rel_err(p, r.astype(np.float32)) <= GEMM_TOL, (fmt, M, N, K, kl.route_name(t, M, N, K, act="fp8"))
+
+
+@pytest.mark.parametrize("act,Ns", [("q8_1", (1, 2, 3, 4)), ("fp8", (1, 2))])
+@pytest.mark.parametrize("fmt,M,K", [("q8_0", 4096, 4096), ("q4_k", 11008, 4096), ("q6_k", 1024, 8192),
+                                     ("q4_k", 96, 256)])
+def test_prepared_decode_is_the_raw_decode(act, Ns, fmt, M, K):
+    """At decode token counts gq_act_prepare keeps a copy of the activations and gq_mmq_prepared
+    runs gq_mmq's one-launch decode on it: the same kernel on the same input, so the same bits."""
+    import kernels._lib as kl
+    t = kl.TYPES[fmt]
+    A = _t(random_blocks(fmt, M, K, seed=M + 3 * K).view(np.int8))
+    for N in Ns:
+        assert kl.route_name(t, M, N, K, act=act) == "stream_decode_kernel", (fmt, M, N, K, act)
+        assert kl.route_name(t, M, N, K, act=act, prepared=True) == "stream_decode_kernel", (fmt, M, N, K, act)
+        B = _t(random_activations(N, K, seed=7 * N + K))
+        raw = kl.mmq(t, A, B, M, N, K, act=act)
+        ws = torch.empty(kl.workspace_size(t, M, N, K, act=act), dtype=torch.uint8, device=_dev())
+        kl.act_prepare(B, N, K, ws, act=act)
+        prep = kl.mmq_prepared(t, A, ws, M, N, K, act=act)
+        torch.cuda.synchronize()
+        assert torch.equal(raw.view(torch.int16), prep.view(torch.int16)), (fmt, M, N, K, act)

@@ -39,8 +39,8 @@ def test_side_stream_and_graph_replay(fmt, M, N, K, first, prepared):
     dev = _dev()
     t = kl.TYPES[fmt]
     route = kl.route_name(t, M, N, K, prepared=prepared)
-    if prepared and first == "stream_decode_kernel":
-        first = "gemv_kernel"  # (the prepared call of a decode shape reads the SOA activations)
+    # (a prepared call of a decode shape runs the same one-launch decode on the workspace's copy
+    # of the activations -- round 5; it read the SOA form through the GEMV before)
     if prepared and N <= 32 and first == "rgemm_kernel":
         first = "kstream_kernel"  # (prepared 5..32 tokens: the K-chunked stream, one launch)
     assert route.startswith(first), route
