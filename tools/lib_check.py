@@ -1,5 +1,5 @@
 """Parity of a diagnostic build of libgguf_mmq.so: each config's raw call against the same
-library's call with the streaming, resident and K-chunked GEMMs switched off (another kernel, other fp32
+library's call with the streaming, resident and K-chunked GEMMs and the fused decode switched off (another kernel, other fp32
 summation order): max |difference| over max |reference| (the GEMM tolerance is 4e-3).
 
 Usage: python tools/lib_check.py --lib=PATH CONFIG ...   (CONFIG: fmt_MxK_mN)
@@ -37,6 +37,7 @@ for cfg in args:
     kl.set_tuning("GQ_SGEMM", 0)
     kl.set_tuning("GQ_RGEMM", 0)
     kl.set_tuning("GQ_KSTREAM", 0)
+    kl.set_tuning("GQ_NO_FUSED_DECODE", 1)
     ref = kl.mmq(t, A, B, M, N, K).float().cpu().numpy()
     alt = kl.route_name(t, M, N, K)
     kl.reset_tuning()
