@@ -586,7 +586,7 @@ __global__ __launch_bounds__(64 * KW, KWPC * KW / 4) void kstream_kernel(const K
     if (threadIdx.x < 2) sync[threadIdx.x] = 0;
     __syncthreads();
     // this workgroup's items: those whose first weight byte (the parts' bytes in order) falls in
-    // [t0, t1), an equal share of the launch's bytes
+    // [t0, t1), an equal share of the launch's cost (weight bytes, weighted per format: launch_kstream)
     const int64_t t0 = a.wtot * blockIdx.x / gridDim.x, t1 = a.wtot * (blockIdx.x + 1) / gridDim.x;
     int seq = 0;
     for (int i = 0; i < a.n; ++i) {
@@ -723,7 +723,11 @@ hipError_t launch_kstream(const KItem *items, int n, int64_t N, int aq, void *pa
             p.nsbp = nsb - p.kofs < per ? nsb - p.kofs : per;
             p.cw = (p.nsbp + KW - 1) / KW;
             const int64_t sbb = it.fmt == Q8_0 ? 272 : (it.fmt == Q4_K ? 144 : 210);
-            p.w = (int)(16 * p.nsbp * sbb);
+            // the deal's cost of a 16-row item: per super-block its bytes - 55 (GQ_KSTREAM_SBW): Q4_K 89,
+            // Q6_K 155, Q8_0 217 -- a Q6_K super-block's dequantization costs more per byte than the
+            // bytes alone say; the 7B layer 3-4% faster than a deal by bytes at 5..32 tokens (x16
+            // 52.7 -> 50.8 us; profiles/r05/kstream_deal_ab.txt).  Any deal gives the same bits.
+            p.w = (int)(16 * p.nsbp * (sbb + tuning().kstream_sbw));
             p.wcum = wcum;
             const int64_t ng = it.M / 16;
             wcum += ng * p.w;
