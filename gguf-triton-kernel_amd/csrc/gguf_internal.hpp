@@ -40,6 +40,7 @@ struct Tuning {
     int sgemm_full = -1;                      // GQ_SGEMM_FULL: Q4_K 16/32-token tiles stream whole super-blocks:
                                               // 1 every streaming GEMM, 0 none, -1 single matrices (measured gain)
     int kstream = -1;                         // GQ_KSTREAM: K-chunked streaming MMQ -1 auto / 0 off / 1 wherever it applies
+    int sgemm_skw = 0;                        // GQ_SGEMM_SKW: grouped stream-K unit cost: -1 equal, else super-block bytes + this
     int kstream_sbw = -55;                    // GQ_KSTREAM_SBW: grouped stream's deal, cost per super-block = its bytes + this
     int cus = 0;                              // GQ_CUS: compute units to plan for (0: the device's count)
     int ablate = 0;                           // GQ_ABLATE (GQ_ABLATION diagnostic builds only)
@@ -169,8 +170,9 @@ struct SGroupPlan {
     int nb = 8, tiles_n = 1, blocks = 0;
     int tiles_m[16] = {}, splits[16] = {}, wg0[16] = {};
     bool streamk = false;  // (tile, super-block) units spread evenly over the workgroups (auto splits)
-    int U = 0;             // stream-K: units; blocks = the workgroups
+    int U = 0;             // stream-K: total cost of the units (each part's units cost[i]); blocks = the workgroups
     int ustart[16] = {}, scap[16] = {};
+    int cost[16] = {}, cstart[16] = {}; // stream-K: a part's per-unit cost, the cost before its first unit
     size_t poff[16] = {};
     size_t partial_bytes = 0;
 };

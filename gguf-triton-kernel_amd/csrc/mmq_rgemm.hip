@@ -483,6 +483,7 @@ struct SPart {
     int64_t M, K, ldc;
     int tiles_m, tiles_n, splits, wg0;
     int ustart, scap; // stream-K: the part's first unit (tile-major (tile, super-block) order), partial slots per tile
+    int cost, cstart; // stream-K: cost per unit, cost before the part's first unit
 };
 struct SParts {
     int n;
@@ -498,6 +499,7 @@ struct RPart {
     int64_t M, ldc;
     int tiles_m, tiles_n, splits, wg0;
     int ustart, nsb, scap;
+    int cost, cstart;
 };
 struct RParts {
     int n;
@@ -507,8 +509,14 @@ struct RParts {
 };
 
 // stream-K: the workgroups whose unit ranges hold the first and the last unit of [u0, u1)
+// (U: the total cost; workgroup w holds the units whose cost start is in [wU/W, (w+1)U/W))
 __device__ __forceinline__ int sk_first_wg(int u0, int U, int W) { return (int)(((int64_t)(u0 + 1) * W + U - 1) / U) - 1; }
 __device__ __forceinline__ int sk_last_wg(int u1, int U, int W) { return (int)(((int64_t)u1 * W + U - 1) / U) - 1; }
+// the workgroup holding unit u of a part (its cost start: cstart + (u - ustart) * cost)
+template <typename Q> __device__ __forceinline__ int sk_owner(const Q &q, int u, int U, int W)
+{
+    return sk_first_wg(q.cstart + (u - q.ustart) * q.cost, U, W);
+}
 
 template <int F, int NB>
 __device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
@@ -736,22 +744,27 @@ __global__ __launch_bounds__(64 * RW) void sgemm_grouped_kernel(const SParts a)
     // stream-K: this workgroup's units [u0, u1) of the parts' (tile, super-block) sequence, as
     // segments of at most one tile each; a tile all of whose units one workgroup holds is stored
     // whole, else each of its S_t workgroups writes partial slot k (in workgroup order)
-    int u = (int)((int64_t)b * a.U / a.W);
-    const int u1 = (int)((int64_t)(b + 1) * a.U / a.W);
+    const int64_t c0 = (int64_t)b * a.U / a.W, c1 = (int64_t)(b + 1) * a.U / a.W;
     bool first = true;
-    while (u < u1) {
-        int i = 0;
-        while (i + 1 < a.n && u >= a.p[i + 1].ustart) ++i;
+    for (int i = 0; i < a.n; ++i) {
         const SPart &q = a.p[i];
-        const int nsb = (int)(q.K / 256), local = u - q.ustart, tile = local / nsb, sb = local - tile * nsb;
-        const int t0 = q.ustart + tile * nsb, t1 = t0 + nsb;
-        const int end = u1 < t1 ? u1 : t1;
-        const int wf = sk_first_wg(t0, a.U, a.W), st = sk_last_wg(t1, a.U, a.W) - wf + 1;
-        const TileId id{tile % q.tiles_m, tile / q.tiles_m, st == 1 ? 0 : b - wf, q.tiles_m, q.tiles_n, st == 1 ? 1 : q.scap};
-        if (!first) __builtin_amdgcn_s_barrier(); // (the previous segment's last stage is read by every wave)
-        run(q, id, sb, sb + (end - u));
-        first = false;
-        u = end;
+        const int nsb = (int)(q.K / 256), nu = q.tiles_m * q.tiles_n * nsb;
+        const int64_t lo = c0 - q.cstart, hi = c1 - q.cstart;
+        if (hi <= 0) break; // (parts in cost order)
+        int u = q.ustart + (int)(lo <= 0 ? 0 : (lo + q.cost - 1) / q.cost);
+        const int64_t k1 = (hi + q.cost - 1) / q.cost;
+        const int u1 = q.ustart + (int)(k1 < nu ? k1 : nu);
+        while (u < u1) {
+            const int local = u - q.ustart, tile = local / nsb, sb = local - tile * nsb;
+            const int t0 = q.ustart + tile * nsb, t1 = t0 + nsb;
+            const int end = u1 < t1 ? u1 : t1;
+            const int wf = sk_owner(q, t0, a.U, a.W), st = sk_owner(q, t1 - 1, a.U, a.W) - wf + 1;
+            const TileId id{tile % q.tiles_m, tile / q.tiles_m, st == 1 ? 0 : b - wf, q.tiles_m, q.tiles_n, st == 1 ? 1 : q.scap};
+            if (!first) __builtin_amdgcn_s_barrier(); // (the previous segment's last stage is read by every wave)
+            run(q, id, sb, sb + (end - u));
+            first = false;
+            u = end;
+        }
     }
 }
 
@@ -775,7 +788,7 @@ __global__ __launch_bounds__(256) void reduce_grouped_kernel(const RParts a)
     int S = q.splits, ss = q.splits; // splits summed, partial slots per tile
     if (a.streamk) {
         const int t0 = q.ustart + tile * q.nsb;
-        S = sk_last_wg(t0 + q.nsb, a.U, a.W) - sk_first_wg(t0, a.U, a.W) + 1;
+        S = sk_owner(q, t0 + q.nsb - 1, a.U, a.W) - sk_owner(q, t0, a.U, a.W) + 1;
         ss = q.scap;
         if (S == 1) return; // (stored whole by its workgroup)
     }
@@ -963,19 +976,40 @@ SGroupPlan plan_sgemm_grouped(const SGroupItem *items, int n, int64_t N, int spl
         // (a 7B layer at 8 / 32 / 64 / 128 tokens: 64.1 / 67.2 / 80.6 / 102.1 us against 66.3
         // per call / 72.7 / 82.0 / 102.6 whole-tile splits: profiles/r04/ab9_layer.txt); single
         // matrices measured slower (GQ_SGEMM_STREAMK=1 forces it there, gq_capi.hip sgemm_streamk)
-        const int W = (int)(units < cus ? units : cus), U = (int)units;
-        auto first_wg = [&](int64_t u0) { return (int)(((u0 + 1) * W + U - 1) / U) - 1; };
-        auto last_wg = [&](int64_t u1) { return (int)((u1 * W + U - 1) / U) - 1; };
+        // each unit weighted by its format -- its super-block's bytes (GQ_SGEMM_SKW = 0; bytes + SKW,
+        // or -1: every unit alike, the round-4 split) -- the workgroups splitting the total cost: the
+        // 7B layer at 40 / 64 / 128 tokens 77.2 / 78.8 / 100.9 -> 72.2 / 73.4 / 97.8 us
+        // (profiles/r05/sgemm_grouped_cost_ab.txt; -55, the K-chunked stream's best, 74.6 / 76.1 / 99.2)
+        const int skw = tuning().sgemm_skw;
+        int64_t ctot = 0;
+        for (int i = 0; i < n; ++i) {
+            const int sbb = items[i].fmt == Q8_0 ? 272 : (items[i].fmt == Q4_K ? 144 : 210);
+            g.cost[i] = skw < -120 || skw == -1 ? 1 : sbb + skw;
+            g.cstart[i] = (int)ctot;
+            ctot += (int64_t)g.tiles_m[i] * tn * (items[i].K / 256) * g.cost[i];
+        }
+        if (ctot >= ((int64_t)1 << 30)) return g;
+        // every workgroup's cost range at least the dearest unit, so that it holds a unit of each
+        // tile it spans (no unwritten partial slot between a tile's first and last workgroup)
+        int cmax = 1;
+        for (int i = 0; i < n; ++i) cmax = g.cost[i] > cmax ? g.cost[i] : cmax;
+        int64_t wmax = units < cus ? units : cus;
+        if (wmax > ctot / cmax) wmax = ctot / cmax > 0 ? ctot / cmax : 1;
+        const int W = (int)wmax, U = (int)ctot;
+        auto owner = [&](int i, int64_t u) { // the workgroup holding unit u of part i
+            const int64_t c = g.cstart[i] + (u - g.ustart[i]) * g.cost[i];
+            return (int)(((c + 1) * W + U - 1) / U) - 1;
+        };
         int64_t ust = 0;
         size_t pb = 0;
         for (int i = 0; i < n; ++i) {
             const int64_t nsb = items[i].K / 256, nt = (int64_t)g.tiles_m[i] * tn;
+            g.ustart[i] = (int)ust;
             int cap = 1;
             for (int64_t t = 0; t < nt; ++t) {
-                const int64_t t0 = ust + t * nsb, st = last_wg(t0 + nsb) - first_wg(t0) + 1;
+                const int64_t t0 = ust + t * nsb, st = owner(i, t0 + nsb - 1) - owner(i, t0) + 1;
                 cap = st > cap ? (int)st : cap;
             }
-            g.ustart[i] = (int)ust;
             g.scap[i] = cap;
             g.splits[i] = cap;
             g.poff[i] = pb;
@@ -1034,11 +1068,11 @@ hipError_t launch_sgemm_grouped(const SGroupItem *items, int n, int64_t N, const
     for (int i = 0; i < n; ++i) {
         uint16_t *P = (uint16_t *)((uint8_t *)partials + g.poff[i]);
         a.p[i] = SPart{items[i].fmt, items[i].A, items[i].X, items[i].C, P, items[i].M, items[i].K, items[i].ldc,
-                       g.tiles_m[i], g.tiles_n, g.splits[i], g.wg0[i], g.ustart[i], g.scap[i]};
+                       g.tiles_m[i], g.tiles_n, g.splits[i], g.wg0[i], g.ustart[i], g.scap[i], g.cost[i], g.cstart[i]};
         if (g.splits[i] > 1) {
             const int tpu = g.nb == 1 ? 1 : 2, upt = RW * RRG * (g.nb / tpu) * 64, bpt = (upt + UPB - 1) / UPB;
             r.p[r.n++] = RPart{P,         items[i].C, items[i].M, items[i].ldc, g.tiles_m[i], g.tiles_n, g.splits[i], rb,
-                               g.ustart[i], (int)(items[i].K / 256), g.scap[i]};
+                               g.ustart[i], (int)(items[i].K / 256), g.scap[i], g.cost[i], g.cstart[i]};
             rb += g.tiles_m[i] * g.tiles_n * bpt;
         }
     }
