@@ -18,6 +18,7 @@ struct Tuning {
     int decode_nt4_cache = 1;                 // GQ_DECODE_NT4_CACHE
     int decode_f8_itc = 1;                    // GQ_DECODE_F8_ITC: fp8 decode keeps x~ in registers at one token
     int decode_early = -1;                    // GQ_DECODE_EARLY: ring refill vs quantization (-1: auto)
+    int decode_q6w = 0;                       // GQ_DECODE_Q6W: grouped decode's Q6_K byte weight in percent (0: the built-in 115/150)
     int decode_q6_img = -1;                   // GQ_DECODE_Q6_IMG: Q6_K aligned ring image (-1: K <= 4096)
     int gemm_aq = 1;                          // GQ_GEMM_AQ: in-kernel quantization of 16/32-token tiles
     int gemm_nb = 0;                          // GQ_GEMM_NB: 16-token groups per tile, 1/2/4/8 (0: auto)

@@ -101,6 +101,9 @@ bool parse_key(Tuning &t, const char *key, long long v)
     } else if (k == "GQ_KSTREAM") {
         if (!in({-1, 0, 1})) return false;
         t.kstream = (int)v;
+    } else if (k == "GQ_DECODE_Q6W") {
+        if (v < 0 || v > 400) return false;
+        t.decode_q6w = (int)v;
     } else if (k == "GQ_SGEMM_SKW") {
         if (v < -120 || v > 100000) return false;
         t.sgemm_skw = (int)v;
@@ -120,7 +123,7 @@ void tuning_from_env(Tuning &t)
                                        "GQ_GEMM_NB", "GQ_GEMM_RG", "GQ_GEMM_LOADERS", "GQ_GEMM_SPLITS",
                                        "GQ_GEMM_PARTIAL", "GQ_GEMV_CAP", "GQ_GEMV_R", "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D",
                                        "GQ_RGEMM", "GQ_SGEMM", "GQ_SGEMM_SPLITS", "GQ_SGEMM_STREAMK", "GQ_RGEMM_NB", "GQ_RGEMM_SPOL",
-                                       "GQ_SGEMM_FULL", "GQ_CUS", "GQ_KSTREAM", "GQ_KSTREAM_SBW", "GQ_SGEMM_SKW",
+                                       "GQ_SGEMM_FULL", "GQ_CUS", "GQ_KSTREAM", "GQ_KSTREAM_SBW", "GQ_SGEMM_SKW", "GQ_DECODE_Q6W",
                                        "GQ_ABLATE"};
     for (const char *k : keys) {
         const char *e = getenv(k); // the only getenv of the library: once per process

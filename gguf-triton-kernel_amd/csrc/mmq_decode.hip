@@ -1039,7 +1039,12 @@ hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipS
                 // Q4_K's): measured on the Q4_K_M 7B layer, profiles/r03/tails/grouped_q6k_weight_ab.log
                 // (re-swept after the Q6_K ring image: 0.9-1.75 at one and two tokens, none better,
                 // profiles/r03/s3/grouped_q6w_sweep.log)
-                const double q6w = nt == 1 ? 1.15 : (nt == 2 ? 1.5 : 1.0);
+                // The fp8 form (v_dot2 on fp16 pairs, a different VALU mix): 1.30 / 1.00 at one / two
+                // tokens (fp8 layer x1 38.4 -> 37.2 us, x2 53.9 -> 51.2; profiles/r05/decode_q6w_fp8_ab.txt).
+                // GQ_DECODE_Q6W (percent) overrides both.
+                const double q6w = tuning().decode_q6w > 0 ? tuning().decode_q6w / 100.0
+                                   : fp8 ? (nt == 1 ? 1.30 : 1.0)
+                                         : (nt == 1 ? 1.15 : (nt == 2 ? 1.5 : 1.0));
                 bytes[np] = (double)items[i].M * (double)row_bytes(items[i].fmt, items[i].K) *
                             (items[i].fmt == Q6_K ? q6w : 1.0);
                 total += bytes[np];
