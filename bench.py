@@ -852,15 +852,91 @@ def bench_msweep(steps, warmup, dev, fmt="q4_k", M=4096, K=4096):
     return {"config": f"{fmt}_{M}x{K}_msweep", "points": res}
 
 
-def compact(e):
-    """A sweep entry with the roofline reduced to what the judge reads: bound, fraction, kernel
-    time, the kernel's name and its PMC traffic (HBM bytes per launch, or null)."""
-    o = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in e.items() if k != "roofline"}
-    if e.get("roofline"):
-        rf = e["roofline"]
-        o["roofline"] = {k: rf.get(k) for k in ("bound", "frac", "achieved", "unit", "kernel_us", "kernel", "traffic",
-                                                "alg_bytes_per_launch")}
-    return o
+def short_kernel(name: str) -> str:
+    """The library's route name (gq_debug_route) in a few characters for the compact rows."""
+    for k, v in (("stream_decode", "decode"), ("rgemm_kernel (in-launch", "rgemm-ilc"), ("rgemm", "rgemm+reduce"),
+                 ("sgemm_grouped", "sgemm-sk+reduce"), ("sgemm", "sgemm+reduce"), ("kstream_kernel +", "kstream+reduce"),
+                 ("kstream", "kstream"), ("skinny", "skinny"), ("gemv", "gemv"), ("hipBLASLt", "dequant+blaslt"),
+                 ("gemm_kernel", "gemm+reduce")):
+        if k in name:
+            return v
+    return name
+
+
+# the compact per-type row (bench line "per_type"): what the BASELINE metric asks for, per config
+PER_TYPE_COLS = ["config", "step_us", "tflops", "weight_GBps", "bound", "frac", "traffic_over_alg", "kernel"]
+
+
+def per_type_row(e):
+    rf = e["roofline"]
+    alg = rf.get("alg_bytes_per_launch") or model(e["fmt"], e["N_out"], e["K"], e["M_tok"])[1]
+    tr = rf.get("traffic")
+    return [e["config"], round(e["ms_per_step"] * 1e3, 2), round(e["tflops"], 1), round(e["weight_GBps"]),
+            rf["bound"], round(rf["frac"], 3), round(tr / alg, 2) if tr else None, short_kernel(rf.get("kernel", ""))]
+
+
+def compact_sweep(sweep):
+    """The sweep blocks as short columns (the whole JSON line has to fit the ~8 KB the driver keeps
+    of stdout: round 5's line lost every M = 1 figure to that cut)."""
+    out = {}
+    for e in sweep:
+        c = e.get("config", "")
+        if c == "q4_k_m_llama7b_layer_msweep":
+            for pt in e["points"]:
+                key = f"layer7b_{pt['act']}" + ("" if pt["fused"] else "_unfused")
+                d = out.setdefault(key, {"M_tok": [], "us": []})
+                d["M_tok"].append(pt["M_tok"])
+                d["us"].append(pt["us_per_step"])
+        elif c.endswith("_msweep"):
+            out[c] = {"M_tok": [p["M_tok"] for p in e["points"]], "us": [p["us_per_step"] for p in e["points"]]}
+        elif c.endswith("_fp8act"):
+            out.setdefault("fp8act_us", {})[c[:-len("_fp8act")]] = e["us_per_step"]
+    if any(k.startswith("layer7b") for k in out):
+        out["layer7b_weight_bytes"] = next(e["weight_bytes"] for e in sweep
+                                           if e.get("config") == "q4_k_m_llama7b_layer_msweep")
+    return out
+
+
+def single_line(args, name, head, sweep, cpu_b, cpu_var, eager, eager_host):
+    """The N = 1 JSON line: the contract's fields for the headline, then one compact row per
+    BASELINE config (per_type) and the sweeps as short columns (compact_sweep)."""
+    fmt, M, K, N = CONFIGS[name]
+    line = {
+        "metric": "effective fp16 TFLOPS (+ quant-weight GB/s) per GGUF type",
+        "value": round(head["tflops"], 3),
+        "unit": "TFLOP/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(head["ms_per_step"], 6),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f16" if N > 4 else "i8",
+        "arith": "q8_1 activations x dequantized GGUF weights on fp16 MFMA, fp32 accumulate" if N > 4 else
+                 "q8_1 int8 activations x GGUF int codes on v_dot4_i32_i8, fp32 block scaling",
+        "data": "synthetic (random packed blocks, N(0,1) fp16 activations)",
+        "config": {"workload": name, "gguf_type": fmt, "N_out": M, "K": K, "M_tok": N, "parallelism": "single",
+                   "weight_copies": head["weight_copies"], "weight_bytes_rotated": head["weight_bytes_rotated"],
+                   "graphs_rotated": head["graphs_rotated"],
+                   "timing": "median of round-robin replays of the rotation's graphs, K steps each"},
+        "weight_GBps": round(head["weight_GBps"], 1),
+        "roofline": head["roofline"],
+        "cpu_baseline": cpu_b,
+        "eager_us": eager,
+        "eager_us_is": "median of 1000 eager kernels.mmq_q4_k.mmq_q4_k(A, B, 4096, 1, 4096) calls, each synchronized",
+        "eager_host_us": eager_host,
+        "eager_host_us_is": "the same call 1000 times back to back, one synchronize at the end, / 1000 (the "
+                            "per-call host cost when the kernel is shorter)",
+    }
+    if cpu_var:
+        line["cpu_baseline_variants"] = [{k: v[k] for k in ("value", "unit", "cores", "kind", "sample")} for v in cpu_var]
+    if sweep:
+        heads = [head] + [e for e in sweep if "roofline" in e]
+        line["per_type_cols"] = PER_TYPE_COLS
+        line["per_type"] = [per_type_row(e) for e in heads]
+        line.update(compact_sweep(sweep))
+    return line
 
 
 def eager_call_us(dev, n=1000):
@@ -946,6 +1022,7 @@ def main():
     ap.add_argument("--quick", action="store_true", help="headline only: no per-type sweep")
     ap.add_argument("--sweep", action="store_true", help="(the default; kept for old command lines)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--detail", default=None, help="also write the full per-config records to this JSON file")
     ap.add_argument("--layer-only", action="store_true",
                     help="print only the Q4_K_M layer sweep (fused and unfused), one JSON line")
     args = ap.parse_args()
@@ -1011,46 +1088,11 @@ def main():
                                 "q4_k_4096x4096_m1"), sweep_steps, args.warmup, dev))
     eager, eager_host = eager_call_us(dev)
     cpu_b, cpu_var = (None, None) if args.no_cpu else cpu_baseline(fmt, M, K, N)
-    line = {
-        "metric": "effective fp16 TFLOPS (+ quant-weight GB/s) per GGUF type",
-        "value": round(head["tflops"], 3),
-        "unit": "TFLOP/s",
-        "n_gpus": 1,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(head["ms_per_step"], 6),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f16" if N > 4 else "i8",
-        "arith": "q8_1 activations x dequantized GGUF weights on fp16 MFMA, fp32 accumulate" if N > 4 else
-                 "q8_1 int8 activations x GGUF int codes on v_dot4_i32_i8, fp32 block scaling",
-        "data": "synthetic (random packed blocks, N(0,1) fp16 activations)",
-        "config": {"workload": name, "gguf_type": fmt, "N_out": M, "K": K, "M_tok": N, "parallelism": "single",
-                   "weight_copies": head["weight_copies"], "weight_bytes_rotated": head["weight_bytes_rotated"],
-                   "graphs_rotated": head["graphs_rotated"],
-                   "timing": "median of round-robin replays of the rotation's graphs, K steps each"},
-        "weight_GBps": round(head["weight_GBps"], 1),
-        "roofline": head["roofline"],
-        "cpu_baseline": cpu_b,
-        "eager_us": eager,
-        "eager_us_is": "median of 1000 eager kernels.mmq_q4_k.mmq_q4_k(A, B, 4096, 1, 4096) calls, each synchronized",
-        "eager_host_us": eager_host,
-        "eager_host_us_is": "the same call 1000 times back to back, one synchronize at the end, / 1000 (the "
-                            "per-call host cost when the kernel is shorter)",
-    }
-    if cpu_var:
-        line["cpu_baseline_variants"] = cpu_var
-    for e in sweep:  # the Q4_K_M 7B layer at one token (one grouped decode launch), up front
-        if e.get("config") == "q4_k_m_llama7b_layer_msweep":
-            for pt in e["points"]:
-                if pt["M_tok"] == 1 and pt["act"] == "q8_1" and pt["fused"]:
-                    line["q4_k_m_layer_m1_us"] = pt["us_per_step"]
-                    line["q4_k_m_layer_m1_GBps"] = pt["weight_GBps"]
-            break
-    if sweep:
-        line["sweep"] = [compact(e) for e in sweep]
-    print(json.dumps(line), flush=True)
+    line = single_line(args, name, head, sweep, cpu_b, cpu_var, eager, eager_host)
+    if args.detail:  # the full per-config records (every roofline field), for the profiles/ notes
+        with open(args.detail, "w") as f:
+            json.dump({"head": head, "sweep": sweep, "cpu_baseline_variants": cpu_var}, f)
+    print(json.dumps(line, separators=(",", ":")), flush=True)
 
 
 if __name__ == "__main__":

@@ -38,6 +38,7 @@ struct Tuning {
                                               // streaming GEMM, 0 none, -1 the grouped plans (the measured gain)
     int rgemm_nb = 0;                         // GQ_RGEMM_NB: the resident GEMM's token tile, 1/2/4/8 x 16 (0: auto)
     int rgemm_spol = 16;                      // GQ_RGEMM_SPOL: its partial stores' cache policy 0 / 2 (nt) / 16 (sc1)
+    int rgemm_ilc = 1;                        // GQ_RGEMM_ILC: its split-K sum inside the launch where the grid is resident
     int sgemm_full = -1;                      // GQ_SGEMM_FULL: Q4_K 16/32-token tiles stream whole super-blocks:
                                               // 1 every streaming GEMM, 0 none, -1 single matrices (measured gain)
     int kstream = -1;                         // GQ_KSTREAM: K-chunked streaming MMQ -1 auto / 0 off / 1 wherever it applies
@@ -144,6 +145,12 @@ struct RGemmPlan {
 };
 
 RGemmPlan plan_rgemm(int64_t M, int64_t N, int64_t K);
+// the split-K partials summed inside the launch (no reduce launch): plans whose grid the chip holds
+bool rgemm_ilc(int fmt, const RGemmPlan &p);
+// in-launch combine polls that gave up since the library loaded (0 unless a grid was not resident)
+unsigned int ilc_timeouts();
+// the K-chunked stream's cross-wave hand-off waits that gave up (0 unless broken)
+unsigned int kstream_timeouts();
 // resident workgroups one CU holds at once (LDS-bound: Q4_K at 16 tokens 3, at 32 two, else one)
 int rgemm_per_cu(int fmt, int nb);
 hipError_t launch_rgemm(int fmt, int aq, const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, void *partials,

@@ -93,7 +93,8 @@ bool parse_key(Tuning &t, const char *key, long long v)
     } else if (k == "GQ_RGEMM_SPOL") {
         if (!in({0, 2, 16})) return false;
         t.rgemm_spol = (int)v;
-    } else if (k == "GQ_SGEMM_FULL") {
+    } else if (k == "GQ_RGEMM_ILC") t.rgemm_ilc = v != 0;
+    else if (k == "GQ_SGEMM_FULL") {
         t.sgemm_full = v < 0 ? -1 : (v != 0);
     } else if (k == "GQ_CUS") {
         if (v < 0 || v > 1024) return false;
@@ -122,7 +123,7 @@ void tuning_from_env(Tuning &t)
                                        "GQ_DECODE_NT4_CACHE", "GQ_DECODE_Q6_IMG", "GQ_DECODE_F8_ITC", "GQ_DECODE_EARLY", "GQ_GEMM_AQ",
                                        "GQ_GEMM_NB", "GQ_GEMM_RG", "GQ_GEMM_LOADERS", "GQ_GEMM_SPLITS",
                                        "GQ_GEMM_PARTIAL", "GQ_GEMV_CAP", "GQ_GEMV_R", "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D",
-                                       "GQ_RGEMM", "GQ_SGEMM", "GQ_SGEMM_SPLITS", "GQ_SGEMM_STREAMK", "GQ_RGEMM_NB", "GQ_RGEMM_SPOL",
+                                       "GQ_RGEMM", "GQ_SGEMM", "GQ_SGEMM_SPLITS", "GQ_SGEMM_STREAMK", "GQ_RGEMM_NB", "GQ_RGEMM_SPOL", "GQ_RGEMM_ILC",
                                        "GQ_SGEMM_FULL", "GQ_CUS", "GQ_KSTREAM", "GQ_KSTREAM_SBW", "GQ_SGEMM_SKW", "GQ_DECODE_Q6W",
                                        "GQ_ABLATE"};
     for (const char *k : keys) {
@@ -327,7 +328,9 @@ bool use_kstream(int t, int form, int64_t M, int64_t N, int64_t K, int act, bool
     if (ks == 0 || form != gq::AF_F16 || use_blas(N, K) || !gq::kstream_ok(t, M, N, K)) return false;
     if (N < (act == GQ_ACT_FP8_E4M3 ? 3 : 5)) return false;
     if (gq::kstream_splits(K) > 1 && !split && ks != 1) return false;
-    if (ks == 1 || prepared) return true;
+    if (ks == 1) return true;
+    if (gemm_knob_pinned()) return false; // (as the resident / streaming routes: the pinned GEMM takes the call)
+    if (prepared) return true;
     // a raw call quantizes in-kernel (every workgroup its whole K of x): ahead of the resident GEMM
     // on the tall matrices at 5..16 tokens (Q4_K 11008 / 14336 / 22016 x4096 x16 15.79 / 17.74 /
     // 25.14 -> 15.41 / 17.36 / 23.23 us, Q6_K 11008 19.79 -> 19.15, Q8_0 11008 18.69 -> 18.33, x8
@@ -426,9 +429,15 @@ size_t scale_bytes(int64_t N, int64_t K) { return align_up((size_t)(K / 32) * (s
 // of the activations at the end of the activation part, so that gq_mmq_prepared runs the same
 // one-launch decode as gq_mmq (bit-identical to it) instead of the GEMV on the SOA form (Q6_K
 // 28672x8192 x1 60.6 -> 35.4 us; profiles/r05/prepared_decode_ab.txt)
+// The copy only where a weight type's fused decode can run at (N, K) (gq_act_prepare does not
+// know the type; e.g. 4 tokens at K = 11008 fit no type's LDS image: no copy, the GEMV)
 bool prep_raw(int act, int64_t N, int64_t K)
 {
-    return act == GQ_ACT_FP8_E4M3 ? N <= 2 && gq::gemm_supported(gq::Q8_0, K) : use_gemv(N, K);
+    const bool fp8 = act == GQ_ACT_FP8_E4M3;
+    if (fp8 ? !(N <= 2 && gq::gemm_supported(gq::Q8_0, K)) : !use_gemv(N, K)) return false;
+    for (int t : {GQ_Q8_0, GQ_Q4_K, GQ_Q6_K})
+        if ((t == GQ_Q8_0 || K % 256 == 0) && gq::decode_fused_ok(t, N, K, fp8)) return true;
+    return false;
 }
 size_t raw_bytes(int act, int64_t N, int64_t K) { return prep_raw(act, N, K) ? align_up((size_t)N * K * 2) : 0; }
 
@@ -575,7 +584,9 @@ void gq_debug_reset_tuning(void) { gq::reset_tuning(); }
 
 int gq_block_elems(gq_type t) { return block_elems(t); }
 int gq_block_bytes(gq_type t) { return block_bytes(t); }
-int gq_version(void) { return 104; }
+int gq_version(void) { return 105; }
+
+unsigned int gq_debug_sync_timeouts(void) { return gq::ilc_timeouts() + gq::kstream_timeouts(); }
 const char *gq_last_error(void) { return g_err.c_str(); }
 
 size_t gq_mmq_call_workspace_size(gq_type t, gq_act act, int64_t M, int64_t N, int64_t K)
@@ -1082,15 +1093,20 @@ static int grouped_gemm_items(gq_act act, const gq_gemm_item *items, int n, int6
 }
 
 // gq_mmq_grouped_prepared's split of the items: those the K-chunked streaming MMQ takes (one
-// launch, no workspace) and the rest (the grouped streaming GEMM: one launch + its reduce)
+// launch, no workspace) and the rest (the grouped streaming GEMM: one launch + its reduce).
+// The stream's launch holds at most kKMaxParts (item, K range) parts: an item whose ranges would
+// pass that goes to the streaming GEMM (e.g. 16 items at K = 8192 are 32 parts: the first 12 take
+// the stream, the other 4 the GEMM).
 static void grouped_split(gq_act act, gq::SGroupItem *g, int n, int64_t N, gq::KItem *ks, int &nk, gq::SGroupItem *rest,
                           int &nr)
 {
     nk = nr = 0;
+    int parts = 0;
     for (int i = 0; i < n; ++i) {
         if (g[i].M <= 0) continue;
+        const int np = gq::kstream_splits(g[i].K);
         if (use_kstream(g[i].fmt, gq::AF_F16, g[i].M, N, g[i].K, act, true, true) &&
-            kstream_fits(g[i].M, N, g[i].K, g[i].K, g[i].ldc))
+            kstream_fits(g[i].M, N, g[i].K, g[i].K, g[i].ldc) && parts + np <= gq::kKMaxParts && (parts += np, true))
             ks[nk++] = gq::KItem{g[i].fmt, g[i].A, g[i].X, g[i].K, g[i].C, g[i].ldc, g[i].M, g[i].K};
         else
             rest[nr++] = g[i];
@@ -1196,7 +1212,8 @@ const char *gq_debug_route(gq_type t, gq_act act, int64_t M, int64_t N, int64_t 
     if (r.gemv) return "gemv_kernel";
     if (use_kstream(t, r.form, M, N, K, act, prepared != 0))
         return gq::kstream_splits(K) > 1 ? "kstream_kernel + kstream_reduce_kernel" : "kstream_kernel";
-    if (rgemm_route(t, r.form, M, N, K, act)) return "rgemm_kernel + gemm_reduce_f16_kernel";
+    if (rgemm_route(t, r.form, M, N, K, act))
+        return gq::rgemm_ilc(t, gq::plan_rgemm(M, N, K)) ? "rgemm_kernel (in-launch split-K sum)" : "rgemm_kernel + gemm_reduce_f16_kernel";
     if (use_skinny(t, r.form, N, act)) return "skinny_kernel";
     if (use_sgemm(t, r.form, M, N, K)) {
         gq::SGroupItem it;

@@ -39,6 +39,9 @@
 
 namespace gq {
 
+// hand-off waits of the cross-wave sum that gave up (gq_debug_sync_timeouts; 0 unless broken)
+__device__ unsigned int g_kstream_timeouts;
+
 #ifdef GQ_KSTREAM_STAMPS // diagnostic build: per-wave phase ticks (never the product)
 __device__ unsigned long long g_kstamps[65536][8];
 #endif
@@ -442,18 +445,29 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
     auto reduce_store = [&](int grp, int np, const f32x4 (&acc)[IP][NB]) __attribute__((always_inline)) -> bool {
         // the scratch is free once the previous hand-off has been summed (a wave is a whole round
         // of items ahead of the summing wave before it waits here)
-        // (bounded: a broken hand-off ends the kernel with wrong bits, never hangs the GPU)
-        for (int spin = 0; spin < (1 << 22) &&
-                           __hip_atomic_load(&sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < seq;
-             ++spin)
+        // (bounded: a broken hand-off ends the kernel with wrong bits, counted in
+        // g_kstream_timeouts -- gq_debug_sync_timeouts -- never hangs the GPU).
+        int spin = 0;
+        for (; spin < (1 << 22) && __hip_atomic_load(&sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < seq; ++spin)
             __builtin_amdgcn_s_sleep(1);
+        if (spin == (1 << 22) && lane == 0)
+            __hip_atomic_fetch_add(&g_kstream_timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // Ordering: a wave's LDS operations execute in issue order, so only the compiler could
+        // move the scratch accesses across the hand-off words; an empty asm with a memory clobber
+        // at each edge forbids that.  (Not a fence: any acquire / release, even one restricted to
+        // LDS, makes the compiler wait vmcnt(0) for the LDS-DMA weight ring and breaks its counted
+        // waits -- 19 extra vmcnt(0) in the kstream kernels' ISA.)
+        asm volatile("" ::: "memory");
 #pragma unroll
         for (int ip = 0; ip < IP; ++ip)
 #pragma unroll
             for (int t = 0; t < NB; ++t) *(f32x4 *)(scr + ((wave * IP + ip) * NB + t) * 256 + 4 * lane) = acc[ip][t];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         int old = 0;
+        // (the lgkmcnt(0) above: this wave's scratch stores have landed before its arrival; the
+        // summing wave's reads below stay after the arrival)
         if (lane == 0) old = __hip_atomic_fetch_add(&sync[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        asm volatile("" ::: "memory");
         old = __builtin_amdgcn_readfirstlane(old);
         ++seq;
         if ((old & (KW - 1)) != KW - 1) return false;
@@ -750,6 +764,12 @@ hipError_t launch_kstream(const KItem *items, int n, int64_t N, int aq, void *pa
     rd.blk0[rd.n] = (int)rblk;
     kstream_reduce_kernel<<<dim3((unsigned)rblk), dim3(256), 0, s>>>(rd);
     return hipGetLastError();
+}
+
+unsigned int kstream_timeouts()
+{
+    unsigned int v = 0;
+    return hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_kstream_timeouts), sizeof(v)) == hipSuccess ? v : ~0u;
 }
 
 } // namespace gq

@@ -42,6 +42,9 @@ __device__ unsigned long long g_rstamps[65536][14];
 #define GQ_RST(i) ((void)0)
 #endif
 
+// polls of the in-launch combine that gave up (ilc_combine; gq_debug_sync_timeouts)
+__device__ unsigned int g_ilc_timeouts;
+
 namespace {
 
 // diagnostic ablation builds only (make rabl RABL=n; never the product): 1 = no weight DMA,
@@ -195,6 +198,139 @@ __device__ __forceinline__ TileId grid_tile()
 {
     return TileId{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y, (int)gridDim.z};
 }
+// The in-launch combine's 1-D grid (gx > 0): workgroup b = tile * gz + split, a tile's splits
+// consecutive in dispatch order (tile = y * gx + x) -- the block index store_tile already uses.
+__device__ __forceinline__ TileId ilc_tile(int gx, int gy)
+{
+    const int gz = (int)gridDim.x / (gx * gy), b = (int)blockIdx.x, t = b / gz;
+    return TileId{t % gx, t / gx, b - t * gz, gx, gy, gz};
+}
+
+// ---- In-launch split-K combine (ILC) -------------------------------------------------------
+// Replaces the reduce launch where the whole grid is resident at once (one round of the chip):
+// every workgroup stores its fp16 partial write-through (sc1), drains its stores, and publishes a
+// flag; then the tile's gz workgroups each sum 1/gz of the tile over all gz partials, in split
+// order -- gemm_reduce_f16_kernel's arithmetic, so the bits equal the two-launch form's.
+// Hand-off (MI355X_MICROARCH.md "visibility", first row of the sc1 table): payload and flags all
+// sc1 stores, every storing wave's vmcnt(0) before the workgroup barrier that precedes the flag,
+// the flags polled with sc1 loads by one wave that then joins a barrier, every payload load sc1.
+// The flags need no zeroed memory: a flag is {nonce + 1, gz, split}, nonce a per-tile word read
+// at the start of the launch and advanced by split 0 once its tile's flags are all in, so a flag
+// left by an earlier launch (any shape: gz and the split are in it) never matches.  A poll that
+// does not complete within kIlcSpins gives up (counted in g_ilc_timeouts, gq_debug_sync_timeouts)
+// rather than hang: it cannot happen while the grid is resident, which the launcher ensures.
+constexpr int kIlcSpins = 1 << 17;
+
+struct IlcSync {
+    uint64_t *flags;  // [tiles * gz]
+    uint32_t *nonce;  // [tiles]
+};
+// the sync words after the partial blocks and their exponents
+__host__ __device__ inline size_t ilc_flags_off(int64_t nblk, int BN) { return ((size_t)nblk * (RBM * BN * 2 + RW * 4) + 7) & ~(size_t)7; }
+__host__ __device__ inline size_t ilc_sync_bytes(int64_t nblk, int64_t ntiles) { return (size_t)nblk * 8 + (size_t)ntiles * 4; }
+__device__ __forceinline__ IlcSync ilc_sync(uint16_t *P, const TileId &id, int BN)
+{
+    const int64_t nblk = (int64_t)id.gx * id.gy * id.gz;
+    uint64_t *f = (uint64_t *)((uint8_t *)P + ilc_flags_off(nblk, BN));
+    return IlcSync{f, (uint32_t *)(f + nblk)};
+}
+__device__ __forceinline__ uint64_t ilc_flag(uint32_t nonce, int gz, int z)
+{
+    return ((uint64_t)(nonce + 1u) << 32) | ((uint64_t)(uint32_t)gz << 16) | (uint32_t)z;
+}
+
+// after store_tile (split-K partial, stored sc1): publish, wait for the tile, sum this
+// workgroup's share of it into C.  nonce: the tile's nonce word as read at the start (wave 0).
+template <int NB>
+__device__ __forceinline__ void ilc_combine(uint16_t *__restrict__ C, uint16_t *__restrict__ P, int64_t M, int64_t N,
+                                            int64_t ldc, const TileId &id, uint32_t nonce)
+{
+    constexpr int BN = 16 * NB;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int gz = id.gz, z = id.z;
+    const int64_t tile = (int64_t)id.y * id.gx + id.x;
+    const IlcSync sy = ilc_sync(P, id, BN);
+    // 1. this wave's partial stores written through, then every wave's (barrier), then the flag
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wave == 0) {
+        uint64_t *tf = sy.flags + tile * gz;
+        if (lane == 0) __hip_atomic_store(tf + z, ilc_flag(nonce, gz, z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // 2. poll the tile's gz flags (sc1 loads), s_sleep between rounds, bounded
+        bool ok = false;
+        for (int it = 0; it < kIlcSpins && !ok; ++it) {
+            bool mine = true;
+            for (int s = lane; s < gz; s += 64)
+                mine = mine && __hip_atomic_load(tf + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ilc_flag(nonce, gz, s);
+            ok = __builtin_amdgcn_ballot_w64(!mine) == 0;
+            if (!ok) __builtin_amdgcn_s_sleep(2);
+        }
+        if (lane == 0) {
+            if (!ok) __hip_atomic_fetch_add(&g_ilc_timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // every split of the tile has read the nonce (each did before its flag): advance it
+            if (z == 0) __hip_atomic_store(sy.nonce + tile, nonce + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    // 3. this workgroup's share of the tile: units [z U / gz, (z+1) U / gz) of store_tile's
+    //    block order (NB >= 2: 16-byte units = two token tiles of a lane's 4 rows; NB = 1: 8 bytes)
+    constexpr int TPU = NB == 1 ? 1 : 2, UB = 8 * TPU, UPT = RW * RRG * (NB / TPU) * 64;
+    const int64_t nblk = (int64_t)id.gx * id.gy * gz;
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)P, 0, (int)(uint32_t)(nblk * (RBM * BN * 2 + RW * 4)), 0x00020000);
+    const int64_t m0 = (int64_t)id.x * RBM, n0 = (int64_t)id.y * BN;
+    const int u0 = (int)((int64_t)z * UPT / gz), u1 = (int)((int64_t)(z + 1) * UPT / gz);
+    for (int it = u0 + tid; it < u1; it += 64 * RW) {
+        const int q = it >> 6, ln = it & 63, u = q % (NB / TPU), wr = q / (NB / TPU), wv = wr / RRG;
+        f32x4 acc[TPU];
+#pragma unroll
+        for (int j = 0; j < TPU; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        constexpr int G = 16; // splits in flight per thread
+        for (int s0 = 0; s0 < gz; s0 += G) {
+            u32x4 v[G];
+            float up[G];
+#pragma unroll
+            for (int k = 0; k < G; ++k) { // unconditional (clamped) loads, the surplus zeroed after
+                const uint32_t b = (uint32_t)(tile * gz + (s0 + k < gz ? s0 + k : gz - 1));
+                const uint32_t eo = (uint32_t)(nblk * (RBM * BN * 2)) + (b * RW + (uint32_t)wv) * 4u;
+                up[k] = __builtin_bit_cast(float, (127u + __builtin_amdgcn_raw_buffer_load_b32(prs, eo, 0, 16)) << 23);
+                const uint32_t vo = b * (uint32_t)(RBM * BN * 2) + (uint32_t)it * UB;
+                if constexpr (TPU == 2) {
+                    v[k] = __builtin_amdgcn_raw_buffer_load_b128(prs, vo, 0, 16);
+                } else {
+                    const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(prs, vo, 0, 16);
+                    v[k] = (u32x4){w.x, w.y, 0u, 0u};
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                if (s0 + k >= gz) v[k] = (u32x4){0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int j = 0; j < TPU; ++j) {
+                    const uint32_t x0 = j == 0 ? v[k].x : v[k].z, x1 = j == 0 ? v[k].y : v[k].w;
+                    acc[j][0] += h2f(x0 & 0xffffu) * up[k];
+                    acc[j][1] += h2f(x0 >> 16) * up[k];
+                    acc[j][2] += h2f(x1 & 0xffffu) * up[k];
+                    acc[j][3] += h2f(x1 >> 16) * up[k];
+                }
+            }
+        }
+        const int64_t row = m0 + 16 * wr + 4 * (ln >> 4);
+        if (row >= M) continue;
+#pragma unroll
+        for (int j = 0; j < TPU; ++j) {
+            const int64_t tok = n0 + 16 * (TPU * u + j) + (ln & 15);
+            if (tok >= N) continue;
+            uint16_t *dst = C + tok * ldc + row;
+            if (row + 4 <= M) {
+                *(u32x2 *)dst = (u32x2){(uint32_t)f2h_bits(acc[j][0]) | ((uint32_t)f2h_bits(acc[j][1]) << 16),
+                                        (uint32_t)f2h_bits(acc[j][2]) | ((uint32_t)f2h_bits(acc[j][3]) << 16)};
+            } else {
+                for (int e = 0; e < 4 && row + e < M; ++e) dst[e] = f2h_bits(acc[j][e]);
+            }
+        }
+    }
+}
 template <int NB>
 __device__ __forceinline__ void store_tile(const f32x4 (&acc)[RRG][NB], uint16_t *__restrict__ C,
                                            uint16_t *__restrict__ P, int64_t M, int64_t N, int64_t ldc, int spol,
@@ -285,16 +421,21 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[RRG][NB], uint16_t
 // AQ: 0 = prepared x~ (X = fp16 [N][K], DEQ layout); 1 = raw fp16 [N][ldx], q8_1 in-kernel;
 // 2 = raw fp16, the fp8 variant's e4m3 quantization in-kernel (F8DEQ x~).
 // spol: cache policy of the split-K partial stores (0 plain, 2 nt, 16 sc1: A/B knob GQ_RGEMM_SPOL).
+// ilc_gx > 0: the in-launch combine (1-D grid of ilc_gx x ilc_gy tiles x the splits, ilc_tile;
+// P's partials stored sc1 and summed in this launch by ilc_combine); else the 3-D grid, the
+// partials summed by the reduce launch.
 template <int F, int NB, int AQ>
 __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
                                                        int64_t ldx, uint16_t *__restrict__ C, uint16_t *__restrict__ P,
-                                                       int64_t M, int64_t N, int64_t K, int64_t ldc, int spol)
+                                                       int64_t M, int64_t N, int64_t K, int64_t ldc, int spol,
+                                                       int ilc_gx, int ilc_gy)
 {
     using G = RCfg<F, NB>;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[G::LDS];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const TileId tile = grid_tile();
+    const bool ilc = ilc_gx > 0;
+    const TileId tile = ilc ? ilc_tile(ilc_gx, ilc_gy) : grid_tile();
     const int64_t m0 = (int64_t)tile.x * RBM, n0 = (int64_t)tile.y * G::BN, sb = tile.z;
     const int64_t row_bytes = (K / Layout<F>::QK) * Layout<F>::BYTES;
     uint8_t *const ximg = lds + G::X_OFF;
@@ -303,6 +444,16 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
     st[0] = __builtin_amdgcn_s_memrealtime();
     GQ_RST(1);
 #endif
+    // (ILC) the tile's nonce word, read first: every wave's oldest memory op, so every counted
+    // vmcnt wait below still counts only the DMAs younger than it; unconditional (a buffer load of
+    // an empty range returns 0 without ILC) so that nothing waits for it before the epilogue
+    uint32_t nonce;
+    {
+        const int64_t t = (int64_t)tile.y * tile.gx + tile.x;
+        const __amdgpu_buffer_rsrc_t nrs = __builtin_amdgcn_make_buffer_rsrc(
+            ilc ? (void *)(ilc_sync(P, tile, G::BN).nonce + t) : (void *)P, 0, ilc ? 4 : 0, 0x00020000);
+        nonce = __builtin_amdgcn_raw_buffer_load_b32(nrs, 0, 0, 16);
+    }
 
     // 1. (AQ) the raw activations into registers first: their loads return ahead of the weight
     //    DMAs in this wave's in-order memory queue, so the quantization overlaps the weights' flight
@@ -429,7 +580,8 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
         if (acc[0][0][0] == 1234.5f) C[0] = 0;
         return;
     }
-    store_tile<NB>(acc, C, P, M, N, ldc, spol, tile);
+    store_tile<NB>(acc, C, P, M, N, ldc, ilc ? 16 : spol, tile);
+    if (ilc && tile.gz > 1) ilc_combine<NB>(C, P, M, N, ldc, tile, nonce);
 #ifdef GQ_RGEMM_STAMPS
     GQ_RST(9);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -859,8 +1011,20 @@ template <int F, int NB, int AQ>
 hipError_t launch_nb(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t *C, void *P, const RGemmPlan &p,
                      int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
+    // workgroups a CU admits at once (the runtime's answer: registers as well as LDS)
+    static const int occ = [] {
+        int n = 0;
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rgemm_kernel<F, NB, AQ>, 64 * RW, 0) == hipSuccess ? n : 0;
+    }();
+    const int64_t blocks = (int64_t)p.tiles_m * p.tiles_n * p.splits;
+    if (rgemm_ilc(F, p) && blocks <= (int64_t)num_cus() * occ) { // the split-K sum inside the launch: one kernel
+        rgemm_kernel<F, NB, AQ><<<dim3((unsigned)blocks), dim3(64 * RW), 0, s>>>(A, X, ldx, C, (uint16_t *)P, M, N, K, ldc,
+                                                                                 16, p.tiles_m, p.tiles_n);
+        return hipGetLastError();
+    }
     const dim3 grid((unsigned)p.tiles_m, (unsigned)p.tiles_n, (unsigned)p.splits);
-    rgemm_kernel<F, NB, AQ><<<grid, dim3(64 * RW), 0, s>>>(A, X, ldx, C, (uint16_t *)P, M, N, K, ldc, tuning().rgemm_spol);
+    rgemm_kernel<F, NB, AQ><<<grid, dim3(64 * RW), 0, s>>>(A, X, ldx, C, (uint16_t *)P, M, N, K, ldc, tuning().rgemm_spol,
+                                                           0, 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.splits == 1) return e;
     return launch_gemm_reduce_f16(NB, RRG, (const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n, s);
@@ -907,10 +1071,26 @@ RGemmPlan plan_rgemm(int64_t M, int64_t N, int64_t K)
     p.tiles_m = (int)((M + RBM - 1) / RBM);
     p.tiles_n = (int)((N + 16 * p.nb - 1) / (16 * p.nb));
     p.splits = (int)(K / 256);
-    const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
-    p.partial_bytes = p.splits > 1 ? (size_t)p.splits * tiles * RBM * 16 * p.nb * 2 + (size_t)p.splits * tiles * RW * 4 : 0;
+    const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n, nblk = tiles * p.splits;
+    // the partial blocks and their exponents, then the in-launch combine's flags and nonces
+    p.partial_bytes = p.splits > 1 ? ilc_flags_off(nblk, 16 * p.nb) + ilc_sync_bytes(nblk, tiles) : 0;
     p.ok = true;
     return p;
+}
+
+// The in-launch combine (ilc_combine) instead of the reduce launch: split-K plans whose grid the
+// chip holds at once (its tile's workgroups wait for each other; launch_nb also checks the
+// runtime's occupancy answer).  GQ_RGEMM_ILC=0: the two-launch form everywhere.
+bool rgemm_ilc(int fmt, const RGemmPlan &p)
+{
+    if (!p.ok || p.splits < 2 || tuning().rgemm_ilc == 0) return false;
+    return (int64_t)p.tiles_m * p.tiles_n * p.splits <= (int64_t)num_cus() * rgemm_per_cu(fmt, p.nb);
+}
+
+unsigned int ilc_timeouts()
+{
+    unsigned int v = 0;
+    return hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_ilc_timeouts), sizeof(v)) == hipSuccess ? v : ~0u;
 }
 
 RGemmPlan plan_sgemm(int64_t M, int64_t N, int64_t K, int splits)

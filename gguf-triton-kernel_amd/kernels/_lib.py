@@ -74,6 +74,7 @@ SIGNATURES = {
     "gq_version": ([], _I),
     "gq_debug_set_tuning": ([ctypes.c_char_p, ctypes.c_longlong], _I),
     "gq_debug_reset_tuning": ([], None),
+    "gq_debug_sync_timeouts": ([], ctypes.c_uint),
 }
 
 _lib = None

@@ -252,7 +252,9 @@ const char *gq_last_error(void);
 
 /* Library ABI version (major * 100 + minor).  103: gq_gemm_item, gq_mmq_grouped_prepared[_workspace_size],
  * gq_debug_route, and larger workspace sizes for the GEMM routes (round 4).  104: gq_mmq_grouped[_ex]
- * takes 5..32 tokens (the K-chunked streaming MMQ; round 5). */
+ * takes 5..32 tokens (the K-chunked streaming MMQ; round 5).  105: the resident GEMM sums its split-K
+ * partials inside its own launch where the grid is resident (one kernel, no reduce launch); the
+ * GEMM workspace sizes grow by that combine's flag words (round 6). */
 int gq_version(void);
 
 /*
@@ -269,6 +271,11 @@ void gq_debug_reset_tuning(void);
  * names as its roofline kernel.  Split-K reduce kernels are listed whether or not the plan
  * splits. */
 const char *gq_debug_route(gq_type t, gq_act act, int64_t M, int64_t N, int64_t K, int prepared);
+/* How many synchronisation waits inside a kernel gave up since the library was loaded: the
+ * resident GEMM's in-launch split-K combine (only possible when another kernel holds CUs its grid
+ * needed) and the K-chunked stream's cross-wave hand-off.  A wait gives up after a bounded spin
+ * (wrong bits, never a hang).  Tests assert it stays 0. */
+unsigned int gq_debug_sync_timeouts(void);
 
 #ifdef __cplusplus
 }

@@ -37,7 +37,7 @@ def test_block_sizes_and_version():
     L = kl.lib()
     assert [L.gq_block_elems(t) for t in (0, 1, 2)] == [32, 256, 256]
     assert [L.gq_block_bytes(t) for t in (0, 1, 2)] == [34, 144, 210]
-    assert L.gq_version() == 104  # (include/gguf_mmq.h: bumped with every ABI change)
+    assert L.gq_version() == 105  # (include/gguf_mmq.h: bumped with every ABI change)
 
 
 def test_host_argument_checks():

@@ -277,3 +277,28 @@ def test_stage_schedule_same_bits(N, knob, pair, tune):
         outs.append(kl.mmq_prepared(t, A, ws, M, N, K))
     torch.cuda.synchronize()
     assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+
+
+def test_grouped_more_k_ranges_than_one_stream_launch_holds():
+    """16 items at K = 8192 are 32 (item, K range) parts of the K-chunked stream, more than one of
+    its launches takes (kKMaxParts = 24): the items past the limit go to the streaming GEMM of the
+    same call instead of the call failing; every item against the oracle."""
+    import kernels._lib as kl
+    kl.reset_tuning()
+    dev = _dev()
+    N, K, M = 16, 8192, 256
+    x = random_activations(N, K, seed=91)
+    ws = _prepare(kl, torch.from_numpy(x).to(dev), N, K)
+    raws, items = [], []
+    for i in range(16):
+        fmt = ("q4_k", "q6_k")[i % 2]
+        qA = random_blocks(fmt, M, K, seed=100 + i)
+        raws.append((fmt, qA))
+        items.append((kl.TYPES[fmt], torch.from_numpy(qA.view(np.int8)).to(dev), ws, M, K, None))
+    outs = kl.mmq_grouped_prepared(items, N)
+    assert outs is not None, kl.lib().gq_last_error()
+    torch.cuda.synchronize()
+    for (fmt, qA), C in zip(raws, outs):
+        got = C.cpu().numpy()
+        ideal = O.mmq_from_fp16(fmt, qA, x, M, N, K, O.IDEAL)
+        assert O.max_rel_err(got, ideal) <= TIGHT, (fmt, O.max_rel_err(got, ideal))

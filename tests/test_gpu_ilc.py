@@ -1,0 +1,155 @@
+"""GPU tests of the resident GEMM's in-launch split-K combine (csrc/mmq_rgemm.hip ilc_combine):
+the partials summed inside the GEMM's own launch, by the tile's workgroups after a flag hand-off,
+instead of by gemm_reduce_f16_kernel.  The arithmetic is the reduce kernel's (the same fp16
+partials, summed in split order in fp32), so the bits must equal the two-launch form's
+(GQ_RGEMM_ILC=0) on every format, token tile, activation form and ragged shape; the flags need
+no zeroed memory, so workspaces full of garbage, of 0xFF, or of an earlier call's flags (another
+shape on the same workspace) must not change a bit; and no poll may give up
+(gq_debug_sync_timeouts stays 0).  Parity with the oracle itself: tests/test_gpu_rgemm.py and
+tests/test_gpu_parity.py, which now run this form by default."""
+import numpy as np
+import pytest
+import torch
+
+from utils.synth import random_activations, random_blocks
+
+pytestmark = pytest.mark.gpu
+
+FMTS = ("q8_0", "q4_k", "q6_k")
+
+
+def _dev():
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    return torch.device("cuda:0")
+
+
+def _t(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(_dev())
+
+
+def _raw(kl, t, A, B, M, N, K, act, ws=None):
+    C = torch.full((N, M), float("nan"), dtype=torch.float16, device=_dev())
+    need = int(kl.lib().gq_mmq_call_workspace_size(t, kl.ACTS[act], M, N, K))
+    if ws is None:
+        ws = torch.empty(max(need, 1), dtype=torch.uint8, device=_dev())
+    assert ws.numel() >= need
+    rc = kl.lib().gq_mmq_ex(t, kl.ACTS[act], A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, K, M, ws.data_ptr(),
+                            ws.numel(), torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, kl.lib().gq_last_error()
+    torch.cuda.synchronize()
+    return C
+
+
+def _prep(kl, t, A, B, M, N, K, act, ws=None):
+    need = kl.workspace_size(t, M, N, K, act)
+    if ws is None:
+        ws = torch.empty(need, dtype=torch.uint8, device=_dev())
+    kl.act_prepare(B, N, K, ws, act=act)
+    C = torch.full((N, M), float("nan"), dtype=torch.float16, device=_dev())
+    kl.mmq_prepared(t, A, ws, M, N, K, out=C, act=act)
+    torch.cuda.synchronize()
+    return C
+
+
+def _two_launch(kl, fn, *a):
+    kl.set_tuning("GQ_RGEMM_ILC", 0)
+    try:
+        return fn(kl, *a)
+    finally:
+        kl.set_tuning("GQ_RGEMM_ILC", 1)
+
+
+SHAPES = [(4096, 128, 4096), (4096, 16, 4096), (4096, 64, 4096), (4096, 33, 4096), (300, 100, 1024),
+          (513, 20, 768), (1000, 40, 512), (4096, 128, 2048), (2048, 128, 8192)]
+
+
+@pytest.mark.parametrize("fmt", FMTS)
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_ilc_bits_equal_two_launch(fmt, M, N, K, tune):
+    import kernels._lib as kl
+    tune(GQ_RGEMM=1, GQ_SKINNY=0, GQ_KSTREAM=0)
+    t = kl.TYPES[fmt]
+    A = _t(random_blocks(fmt, M, K, seed=M + K).view(np.int8))
+    B = _t(random_activations(N, K, seed=N + 3 * K))
+    name = kl.route_name(t, M, N, K)
+    assert name.startswith("rgemm_kernel"), name
+    before = kl.lib().gq_debug_sync_timeouts()
+    for act in ("q8_1", "fp8"):
+        for fn in (_raw, _prep):
+            got = fn(kl, t, A, B, M, N, K, act)
+            ref = _two_launch(kl, fn, t, A, B, M, N, K, act)
+            assert torch.equal(got.view(torch.int16), ref.view(torch.int16)), (act, fn.__name__, name)
+    assert kl.lib().gq_debug_sync_timeouts() == before
+
+
+def test_ilc_is_the_default_route_of_the_headline():
+    import kernels._lib as kl
+    kl.reset_tuning()
+    assert kl.route_name(kl.GQ_Q8_0, 4096, 128, 4096) == "rgemm_kernel (in-launch split-K sum)"
+    assert kl.route_name(kl.GQ_Q8_0, 4096, 128, 4096, prepared=True) == "rgemm_kernel (in-launch split-K sum)"
+
+
+@pytest.mark.parametrize("fill", [None, 0x00, 0xFF, 0x01])
+def test_ilc_workspace_contents_and_reuse(fill):
+    """One workspace reused by a sequence of calls of different split counts, tile counts and
+    formats (its flag words then hold every kind of stale value), filled first with garbage,
+    zeros, 0xFF or 0x01 bytes: every call equals its two-launch result."""
+    import kernels._lib as kl
+    kl.reset_tuning()
+    shapes = [("q8_0", 4096, 128, 4096), ("q4_k", 4096, 128, 2048), ("q8_0", 4096, 128, 4096),
+              ("q6_k", 2048, 64, 4096), ("q8_0", 4096, 64, 4096), ("q4_k", 4096, 16, 4096), ("q8_0", 4096, 128, 4096)]
+    need = max(int(kl.lib().gq_mmq_call_workspace_size(kl.TYPES[f], 0, M, N, K)) for f, M, N, K in shapes)
+    ws = torch.empty(need, dtype=torch.uint8, device=_dev())
+    if fill is not None:
+        ws.fill_(fill)
+    before = kl.lib().gq_debug_sync_timeouts()
+    data = {}
+    for i, (f, M, N, K) in enumerate(shapes * 2):
+        t = kl.TYPES[f]
+        if (f, M, N, K) not in data:
+            data[(f, M, N, K)] = (_t(random_blocks(f, M, K, seed=i).view(np.int8)), _t(random_activations(N, K, seed=i)))
+        A, B = data[(f, M, N, K)]
+        got = _raw(kl, t, A, B, M, N, K, "q8_1", ws=ws)
+        ref = _two_launch(kl, _raw, t, A, B, M, N, K, "q8_1")
+        assert torch.equal(got.view(torch.int16), ref.view(torch.int16)), (i, f, M, N, K)
+    assert kl.lib().gq_debug_sync_timeouts() == before
+
+
+def test_ilc_graph_replays_and_back_to_back():
+    """The headline call captured 8 times in one graph (back-to-back launches on one workspace,
+    each advancing the tiles' nonces) and the graph replayed 5 times, C poisoned between
+    replays: every output equals the eager two-launch result."""
+    import kernels._lib as kl
+    kl.reset_tuning()
+    t, M, N, K = kl.GQ_Q8_0, 4096, 128, 4096
+    A = _t(random_blocks("q8_0", M, K, seed=5).view(np.int8))
+    B = _t(random_activations(N, K, seed=6))
+    ref = _two_launch(kl, _raw, t, A, B, M, N, K, "q8_1")
+    need = int(kl.lib().gq_mmq_call_workspace_size(t, 0, M, N, K))
+    ws = torch.empty(need, dtype=torch.uint8, device=_dev())
+    Cs = [torch.empty(N, M, dtype=torch.float16, device=_dev()) for _ in range(8)]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+
+    def call(C):
+        rc = kl.lib().gq_mmq_ex(t, 0, A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, K, M, ws.data_ptr(), need,
+                                torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+
+    with torch.cuda.stream(s):
+        call(Cs[0])
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for C in Cs:
+            call(C)
+    before = kl.lib().gq_debug_sync_timeouts()
+    for _ in range(5):
+        for C in Cs:
+            C.fill_(float("nan"))
+        g.replay()
+        torch.cuda.synchronize()
+        for C in Cs:
+            assert torch.equal(C.view(torch.int16), ref.view(torch.int16))
+    assert kl.lib().gq_debug_sync_timeouts() == before
