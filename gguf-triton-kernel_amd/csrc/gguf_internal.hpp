@@ -14,36 +14,23 @@ struct Tuning {
     long long gemm_max_bytes = 1LL << 31;     // GQ_GEMM_MAX_BYTES: weight / activation bytes per GEMM launch
     int gemm_i8 = 0;                          // GQ_GEMM_I8: Q8_0 int8-MFMA form
     int fused_decode = 1;                     // GQ_NO_FUSED_DECODE=1 -> 0
-    int decode_maxnt = 0;                     // GQ_DECODE_MAXNT: token-group cap of the fused decode (0: auto)
-    int decode_nt4_cache = 1;                 // GQ_DECODE_NT4_CACHE
     int decode_f8_itc = 1;                    // GQ_DECODE_F8_ITC: fp8 decode keeps x~ in registers at one token
-    int decode_early = -1;                    // GQ_DECODE_EARLY: ring refill vs quantization (-1: auto)
-    int decode_q6w = 0;                       // GQ_DECODE_Q6W: grouped decode's Q6_K byte weight in percent (0: the built-in 115/150)
     int decode_q6_img = -1;                   // GQ_DECODE_Q6_IMG: Q6_K aligned ring image (-1: K <= 4096)
     int gemm_aq = 1;                          // GQ_GEMM_AQ: in-kernel quantization of 16/32-token tiles
-    int gemm_nb = 0;                          // GQ_GEMM_NB: 16-token groups per tile, 1/2/4/8 (0: auto)
     int gemm_rg = 0;                          // GQ_GEMM_RG: 1 or 2 (0: auto)
-    int gemm_loaders = -1;                    // GQ_GEMM_LOADERS: 0 or 4 (-1: auto)
     long long gemm_splits = 0;                // GQ_GEMM_SPLITS: split-K factor (0: auto)
     int gemm_partial_f32 = 0;                 // GQ_GEMM_PARTIAL=f32
-    long long gemv_cap = 0;                   // GQ_GEMV_CAP (0: auto)
-    int gemv_r = 0;                           // GQ_GEMV_R: rows per wave, 1/2/4 (0: auto)
     int skinny = -1;                          // GQ_SKINNY: 5..32-token kernel (-1 auto, 0 off, 1 every 1..32)
     int skinny_rg = 0;                        // GQ_SKINNY_RG: fragments per workgroup, 1..4 (0: auto)
-    int skinny_d = 0;                         // GQ_SKINNY_D: super-blocks in the register ring, 2..4 (0: auto)
     int rgemm = -1;                           // GQ_RGEMM: resident-split GEMM -1 auto / 0 off / 1 wherever it applies
     int sgemm = -1;                           // GQ_SGEMM: streaming 256-row GEMM -1 auto / 0 off / 1 wherever it applies
     int sgemm_splits = 0;                     // GQ_SGEMM_SPLITS (0: auto)
     int sgemm_streamk = -1;                   // GQ_SGEMM_STREAMK: stream-K unit split of the auto plan: 1 every
                                               // streaming GEMM, 0 none, -1 the grouped plans (the measured gain)
-    int rgemm_nb = 0;                         // GQ_RGEMM_NB: the resident GEMM's token tile, 1/2/4/8 x 16 (0: auto)
-    int rgemm_spol = 16;                      // GQ_RGEMM_SPOL: its partial stores' cache policy 0 / 2 (nt) / 16 (sc1)
     int rgemm_ilc = 1;                        // GQ_RGEMM_ILC: its split-K sum inside the launch where the grid is resident
     int sgemm_full = -1;                      // GQ_SGEMM_FULL: Q4_K 16/32-token tiles stream whole super-blocks:
                                               // 1 every streaming GEMM, 0 none, -1 single matrices (measured gain)
     int kstream = -1;                         // GQ_KSTREAM: K-chunked streaming MMQ -1 auto / 0 off / 1 wherever it applies
-    int sgemm_skw = 0;                        // GQ_SGEMM_SKW: grouped stream-K unit cost: -1 equal, else super-block bytes + this
-    int kstream_sbw = -55;                    // GQ_KSTREAM_SBW: grouped stream's deal, cost per super-block = its bytes + this
     int cus = 0;                              // GQ_CUS: compute units to plan for (0: the device's count)
     int ablate = 0;                           // GQ_ABLATE (GQ_ABLATION diagnostic builds only)
 };
@@ -159,6 +146,8 @@ hipError_t launch_rgemm(int fmt, int aq, const uint8_t *A, const uint16_t *X, in
 // super-blocks, half-super-block stages through an LDS ring; prepared x~ only (X = [N][K]).
 // splits <= 0: as many as keep the grid within one round of the chip.
 RGemmPlan plan_sgemm(int64_t M, int64_t N, int64_t K, int splits);
+// its split-K sum inside the launch (as rgemm_ilc; the streaming kernel holds one workgroup per CU)
+bool sgemm_ilc(const RGemmPlan &p);
 hipError_t launch_sgemm(int fmt, const uint8_t *A, const uint16_t *X, uint16_t *C, void *partials, const RGemmPlan &p,
                         int64_t M, int64_t N, int64_t K, int64_t ldc, hipStream_t s);
 

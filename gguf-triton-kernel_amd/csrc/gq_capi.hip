@@ -34,53 +34,26 @@ bool parse_key(Tuning &t, const char *key, long long v)
         t.gemm_max_bytes = v < (1LL << 31) ? v : (1LL << 31);
     } else if (k == "GQ_GEMM_I8") t.gemm_i8 = v != 0;
     else if (k == "GQ_NO_FUSED_DECODE") t.fused_decode = v == 0;
-    else if (k == "GQ_DECODE_MAXNT") {
-        if (v < 0 || v > 8) return false;
-        t.decode_maxnt = (int)v;
-    } else if (k == "GQ_DECODE_NT4_CACHE") t.decode_nt4_cache = v != 0;
     else if (k == "GQ_DECODE_F8_ITC") t.decode_f8_itc = v != 0;
     else if (k == "GQ_SGEMM_STREAMK") t.sgemm_streamk = v < 0 ? -1 : (v != 0);
-    else if (k == "GQ_RGEMM_NB") {
-        if (!in({0, 1, 2, 4, 8})) return false;
-        t.rgemm_nb = (int)v;
-    }
-    else if (k == "GQ_DECODE_EARLY") {
-        if (!in({-1, 0, 1, 2})) return false;
-        t.decode_early = (int)v;
-    }
     else if (k == "GQ_DECODE_Q6_IMG") {
         if (!in({-1, 0, 1})) return false;
         t.decode_q6_img = (int)v;
     }
     else if (k == "GQ_GEMM_AQ") t.gemm_aq = v != 0;
-    else if (k == "GQ_GEMM_NB") {
-        if (!in({0, 1, 2, 4, 8})) return false;
-        t.gemm_nb = (int)v;
-    } else if (k == "GQ_GEMM_RG") {
+    else if (k == "GQ_GEMM_RG") {
         if (!in({0, 1, 2})) return false;
         t.gemm_rg = (int)v;
-    } else if (k == "GQ_GEMM_LOADERS") {
-        if (!in({-1, 0, 4})) return false;
-        t.gemm_loaders = (int)v;
     } else if (k == "GQ_GEMM_SPLITS") {
         if (v < 0) return false;
         t.gemm_splits = v;
     } else if (k == "GQ_GEMM_PARTIAL") t.gemm_partial_f32 = v != 0; // 1 = f32
-    else if (k == "GQ_GEMV_CAP") {
-        if (v < 0) return false;
-        t.gemv_cap = v;
-    } else if (k == "GQ_GEMV_R") {
-        if (!in({0, 1, 2, 4})) return false;
-        t.gemv_r = (int)v;
-    } else if (k == "GQ_SKINNY") {
+    else if (k == "GQ_SKINNY") {
         if (!in({-1, 0, 1})) return false;
         t.skinny = (int)v;
     } else if (k == "GQ_SKINNY_RG") {
         if (!in({0, 1, 2, 3, 4})) return false;
         t.skinny_rg = (int)v;
-    } else if (k == "GQ_SKINNY_D") {
-        if (!in({0, 2, 3, 4})) return false;
-        t.skinny_d = (int)v;
     } else if (k == "GQ_RGEMM") {
         if (!in({-1, 0, 1})) return false;
         t.rgemm = (int)v;
@@ -90,9 +63,6 @@ bool parse_key(Tuning &t, const char *key, long long v)
     } else if (k == "GQ_SGEMM_SPLITS") {
         if (v < 0 || v > 4096) return false;
         t.sgemm_splits = (int)v;
-    } else if (k == "GQ_RGEMM_SPOL") {
-        if (!in({0, 2, 16})) return false;
-        t.rgemm_spol = (int)v;
     } else if (k == "GQ_RGEMM_ILC") t.rgemm_ilc = v != 0;
     else if (k == "GQ_SGEMM_FULL") {
         t.sgemm_full = v < 0 ? -1 : (v != 0);
@@ -102,15 +72,6 @@ bool parse_key(Tuning &t, const char *key, long long v)
     } else if (k == "GQ_KSTREAM") {
         if (!in({-1, 0, 1})) return false;
         t.kstream = (int)v;
-    } else if (k == "GQ_DECODE_Q6W") {
-        if (v < 0 || v > 400) return false;
-        t.decode_q6w = (int)v;
-    } else if (k == "GQ_SGEMM_SKW") {
-        if (v < -120 || v > 100000) return false;
-        t.sgemm_skw = (int)v;
-    } else if (k == "GQ_KSTREAM_SBW") {
-        if (v < -120 || v > 100000) return false;
-        t.kstream_sbw = (int)v;
     } else if (k == "GQ_ABLATE") t.ablate = (int)v;
     else return false;
     return true;
@@ -119,13 +80,11 @@ bool parse_key(Tuning &t, const char *key, long long v)
 void tuning_from_env(Tuning &t)
 {
     t = Tuning{};
-    static const char *const keys[] = {"GQ_BLAS_MIN_TOKENS", "GQ_GEMM_MAX_BYTES", "GQ_GEMM_I8", "GQ_NO_FUSED_DECODE", "GQ_DECODE_MAXNT",
-                                       "GQ_DECODE_NT4_CACHE", "GQ_DECODE_Q6_IMG", "GQ_DECODE_F8_ITC", "GQ_DECODE_EARLY", "GQ_GEMM_AQ",
-                                       "GQ_GEMM_NB", "GQ_GEMM_RG", "GQ_GEMM_LOADERS", "GQ_GEMM_SPLITS",
-                                       "GQ_GEMM_PARTIAL", "GQ_GEMV_CAP", "GQ_GEMV_R", "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_SKINNY_D",
-                                       "GQ_RGEMM", "GQ_SGEMM", "GQ_SGEMM_SPLITS", "GQ_SGEMM_STREAMK", "GQ_RGEMM_NB", "GQ_RGEMM_SPOL", "GQ_RGEMM_ILC",
-                                       "GQ_SGEMM_FULL", "GQ_CUS", "GQ_KSTREAM", "GQ_KSTREAM_SBW", "GQ_SGEMM_SKW", "GQ_DECODE_Q6W",
-                                       "GQ_ABLATE"};
+    static const char *const keys[] = {"GQ_BLAS_MIN_TOKENS", "GQ_GEMM_MAX_BYTES", "GQ_GEMM_I8", "GQ_NO_FUSED_DECODE",
+                                       "GQ_DECODE_Q6_IMG", "GQ_DECODE_F8_ITC", "GQ_GEMM_AQ", "GQ_GEMM_RG", "GQ_GEMM_SPLITS",
+                                       "GQ_GEMM_PARTIAL", "GQ_SKINNY", "GQ_SKINNY_RG", "GQ_RGEMM", "GQ_SGEMM",
+                                       "GQ_SGEMM_SPLITS", "GQ_SGEMM_STREAMK", "GQ_RGEMM_ILC", "GQ_SGEMM_FULL", "GQ_CUS",
+                                       "GQ_KSTREAM", "GQ_ABLATE"};
     for (const char *k : keys) {
         const char *e = getenv(k); // the only getenv of the library: once per process
         if (!e || !*e) continue;
@@ -260,7 +219,7 @@ bool use_skinny(int t, int form, int64_t N, int act = GQ_ACT_Q8_1)
 gq::SkinnyPlan skinny_plan(int t, int64_t M, int64_t N, int64_t K)
 {
     const gq::Tuning &tu = gq::tuning();
-    return gq::plan_skinny(t, M, N, K, tu.skinny_rg, tu.skinny_d);
+    return gq::plan_skinny(t, M, N, K, tu.skinny_rg, 0);
 }
 
 // Resident-split GEMM (mmq_rgemm.hip: 256 rows x <= 128 tokens x one super-block per workgroup,
@@ -275,7 +234,7 @@ gq::SkinnyPlan skinny_plan(int t, int64_t M, int64_t N, int64_t K)
 bool gemm_knob_pinned()
 {
     const gq::Tuning &u = gq::tuning();
-    return u.gemm_splits > 0 || u.gemm_nb || u.gemm_rg || u.gemm_loaders >= 0 || u.gemm_partial_f32;
+    return u.gemm_splits > 0 || u.gemm_rg || u.gemm_partial_f32;
 }
 
 bool use_rgemm(int t, int form, int64_t M, int64_t N, int64_t K)
@@ -1212,14 +1171,19 @@ const char *gq_debug_route(gq_type t, gq_act act, int64_t M, int64_t N, int64_t 
     if (r.gemv) return "gemv_kernel";
     if (use_kstream(t, r.form, M, N, K, act, prepared != 0))
         return gq::kstream_splits(K) > 1 ? "kstream_kernel + kstream_reduce_kernel" : "kstream_kernel";
-    if (rgemm_route(t, r.form, M, N, K, act))
-        return gq::rgemm_ilc(t, gq::plan_rgemm(M, N, K)) ? "rgemm_kernel (in-launch split-K sum)" : "rgemm_kernel + gemm_reduce_f16_kernel";
+    if (rgemm_route(t, r.form, M, N, K, act)) {
+        const gq::RGemmPlan p = gq::plan_rgemm(M, N, K);
+        return p.splits == 1 ? "rgemm_kernel"
+               : gq::rgemm_ilc(t, p) ? "rgemm_kernel (in-launch split-K sum)" : "rgemm_kernel + gemm_reduce_f16_kernel";
+    }
     if (use_skinny(t, r.form, N, act)) return "skinny_kernel";
     if (use_sgemm(t, r.form, M, N, K)) {
         gq::SGroupItem it;
         gq::SGroupPlan g;
-        return sgemm_streamk(t, M, N, K, it, g) ? "sgemm_grouped_kernel + reduce_grouped_kernel (stream-K)"
-                                               : "sgemm_kernel + gemm_reduce_f16_kernel";
+        if (sgemm_streamk(t, M, N, K, it, g)) return "sgemm_grouped_kernel + reduce_grouped_kernel (stream-K)";
+        const gq::RGemmPlan p = sgemm_plan(M, N, K);
+        return p.splits == 1 ? "sgemm_kernel"
+               : gq::sgemm_ilc(p) ? "sgemm_kernel (in-launch split-K sum)" : "sgemm_kernel + gemm_reduce_f16_kernel";
     }
     return "gemm_kernel + gemm_reduce_f16_kernel";
 }

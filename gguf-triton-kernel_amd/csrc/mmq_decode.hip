@@ -719,7 +719,6 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p, int wgs = 0)
     // group wins (4096^2 11.1 vs 14.3, 14336x4096 27.4 vs 29.7) -- profiles/r02/decode_maxnt_ab.txt.
     // By K, not by size: row shards of one matrix take the same path (bit-identical results).
     int nt_cap = fmt == Q6_K && K >= 8192 ? 2 : 4;
-    if (tuning().decode_maxnt > 0) nt_cap = tuning().decode_maxnt; // tuning override
     while (p.nt > 1 && p.nt > nt_cap) p.nt >>= 1;
     while ((size_t)RING + act_lds(fmt, p.nt, K, p.fp8) > (size_t)LDS_CAP) {
         if (p.nt == 1) return false;
@@ -769,14 +768,14 @@ bool pick(int fmt, int64_t M, int64_t N, int64_t K, Pick &p, int wgs = 0)
     // 0..7 (Q6_K 0..4), two 0..4 (Q6_K 0..1), four 0..1 -- e.g. K = 29568 at one token gives 8
     if (p.itc > itc_max(fmt, p.nt)) p.itc = 0;
     // four tokens, one unit per lane (K <= 4096): cached too (Q6_K 14336x4096 x4 27.7 -> 20.7 us,
-    // profiles/r02/decode_nt4_cache_ab.txt; GQ_DECODE_NT4_CACHE=0: off)
-    if (p.nt == 4 && units == 1 && tuning().decode_nt4_cache)
+    // profiles/r02/decode_nt4_cache_ab.txt)
+    if (p.nt == 4 && units == 1)
         p.itc = 1;
     if (p.fp8) { // (cached x~ at one token: GQ_DECODE_F8_ITC=0 turns it off)
         const int64_t fitc = (cpr + (1 << g.lp2) - 1) >> g.lp2;
         p.itc = p.nt == 1 && tuning().decode_f8_itc && fitc <= fp8_itc_max(fmt, 1) ? (int)fitc : 0;
     }
-    g.early = tuning().decode_early >= 0 ? tuning().decode_early : 0;
+    g.early = 0; // (1 / 2: the ring refilled under the quantization -- measured slower, profiles/r04/dec_early.txt)
     const int64_t waves = g.ngroups < W ? g.ngroups : W;
     p.grid = (int)((waves + DW - 1) / DW);
     return true;
@@ -1041,10 +1040,7 @@ hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipS
                 // profiles/r03/s3/grouped_q6w_sweep.log)
                 // The fp8 form (v_dot2 on fp16 pairs, a different VALU mix): 1.30 / 1.00 at one / two
                 // tokens (fp8 layer x1 38.4 -> 37.2 us, x2 53.9 -> 51.2; profiles/r05/decode_q6w_fp8_ab.txt).
-                // GQ_DECODE_Q6W (percent) overrides both.
-                const double q6w = tuning().decode_q6w > 0 ? tuning().decode_q6w / 100.0
-                                   : fp8 ? (nt == 1 ? 1.30 : 1.0)
-                                         : (nt == 1 ? 1.15 : (nt == 2 ? 1.5 : 1.0));
+                const double q6w = fp8 ? (nt == 1 ? 1.30 : 1.0) : (nt == 1 ? 1.15 : (nt == 2 ? 1.5 : 1.0));
                 bytes[np] = (double)items[i].M * (double)row_bytes(items[i].fmt, items[i].K) *
                             (items[i].fmt == Q6_K ? q6w : 1.0);
                 total += bytes[np];

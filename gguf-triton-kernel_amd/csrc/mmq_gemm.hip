@@ -883,7 +883,6 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, int act)
     GemmPlan p;
     p.act = act == AF_I8 && fmt != Q8_0 ? AF_F16 : act;
     p.nb = pick_nb(N);
-    if (tuning().gemm_nb) p.nb = tuning().gemm_nb; // (validated: 1, 2, 4 or 8)
     // two 16-row groups per wave (256-row tiles: half the activation traffic per weight) for
     // tall matrices at full token tiles
     // (Q4_K; Q6_K as a 224-B row image, Cfg::Q6S, only on request: half the activation re-reads
@@ -896,9 +895,8 @@ GemmPlan plan_gemm(int fmt, int64_t M, int64_t N, int64_t K, int act)
     if (p.act != AF_F16) p.rg = 1; // the code forms run 128-row tiles
     // four loader waves (DMA issue off the multiplying waves' path) for the 128-row fp16 form:
     // Q6_K 28672x8192x128 116.5 -> 103.7 us, Q4_K 4096^2x128 17.4 -> 16.7, Q8_0 4096^2x128
-    // 20.6 -> 20.1 (profiles/r02/loader_tune.txt); GQ_GEMM_LOADERS=0 restores all-wave issue
+    // 20.6 -> 20.1 (profiles/r02/loader_tune.txt)
     p.loaders = p.act == AF_F16 && p.rg == R1 ? 4 : 0;
-    if (tuning().gemm_loaders >= 0) p.loaders = p.act == AF_F16 && tuning().gemm_loaders == 4 ? 4 : 0;
     const int64_t nws = K / 256; // weight stages (super-blocks)
     if (nws == 0) return p;      // not a GEMM shape (gemm_supported() is false): nothing to plan
     const int64_t bm = 16 * NWAVE * p.rg;

@@ -73,8 +73,7 @@ hipError_t launch_one(const uint8_t *A, const int8_t *xq, const float *xd, const
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
     const int64_t groups = (M + 4 * R - 1) / (4 * R);
-    int64_t cap = 2048;
-    if (tuning().gemv_cap > 0) cap = tuning().gemv_cap; // tuning
+    const int64_t cap = 2048;
     dim3 grid((unsigned)(groups < cap ? groups : cap), (unsigned)((N + NT - 1) / NT)), block(256);
     gemv_kernel<F, NT, R><<<grid, block, 0, s>>>(A, xq, xd, xs, C, M, N, K, ldc);
     return hipGetLastError();
@@ -86,9 +85,8 @@ hipError_t launch_fmt(const uint8_t *A, const int8_t *xq, const float *xd, const
 {
     // rows per wave (profiles/r02/gemv_rows_tune.txt): 1-2 tokens Q8_0 4, Q4_K / Q6_K 2
     // (Q4_K 4096x28672 x2 30.3 -> 23.9 us, Q6_K 8192x28672 x2 64.9 -> 58.3); 3-4 tokens 2,
-    // Q6_K 4 (x4 81.7 -> 72.9); GQ_GEMV_R overrides
-    int r = N <= 2 ? (F == Q8_0 ? 4 : 2) : (F == Q6_K ? 4 : 2);
-    if (tuning().gemv_r) r = tuning().gemv_r; // (validated: 1, 2 or 4)
+    // Q6_K 4 (x4 81.7 -> 72.9)
+    const int r = N <= 2 ? (F == Q8_0 ? 4 : 2) : (F == Q6_K ? 4 : 2);
     if (N == 1) return r == 8 ? launch_one<F, 1, 8>(A, xq, xd, xs, C, M, N, K, ldc, s)
                               : r == 2 ? launch_one<F, 1, 2>(A, xq, xd, xs, C, M, N, K, ldc, s)
                                        : launch_one<F, 1, 4>(A, xq, xd, xs, C, M, N, K, ldc, s);

@@ -737,11 +737,11 @@ hipError_t launch_kstream(const KItem *items, int n, int64_t N, int aq, void *pa
             p.nsbp = nsb - p.kofs < per ? nsb - p.kofs : per;
             p.cw = (p.nsbp + KW - 1) / KW;
             const int64_t sbb = it.fmt == Q8_0 ? 272 : (it.fmt == Q4_K ? 144 : 210);
-            // the deal's cost of a 16-row item: per super-block its bytes - 55 (GQ_KSTREAM_SBW): Q4_K 89,
+            // the deal's cost of a 16-row item: per super-block its bytes - 55: Q4_K 89,
             // Q6_K 155, Q8_0 217 -- a Q6_K super-block's dequantization costs more per byte than the
             // bytes alone say; the 7B layer 3-4% faster than a deal by bytes at 5..32 tokens (x16
             // 52.7 -> 50.8 us; profiles/r05/kstream_deal_ab.txt).  Any deal gives the same bits.
-            p.w = (int)(16 * p.nsbp * (sbb + tuning().kstream_sbw));
+            p.w = (int)(16 * p.nsbp * (sbb - 55));
             p.wcum = wcum;
             const int64_t ng = it.M / 16;
             wcum += ng * p.w;

@@ -59,6 +59,7 @@ constexpr int RW = 8;                 // waves per workgroup (two per SIMD)
 constexpr int RRG = 2;                // 16-row groups per wave
 constexpr int RBM = 16 * RW * RRG;    // 256 rows per tile
 constexpr int LDS_CAP = 160 * 1024;
+constexpr int kSpol = 16; // split-K partial stores write-through (sc1)
 
 // The split's weights as two half-super-block images (K elements 0..127 and 128..255 of every
 // row), so that the multiply of the first half runs while the second half is still in flight.
@@ -237,6 +238,16 @@ __device__ __forceinline__ IlcSync ilc_sync(uint16_t *P, const TileId &id, int B
 __device__ __forceinline__ uint64_t ilc_flag(uint32_t nonce, int gz, int z)
 {
     return ((uint64_t)(nonce + 1u) << 32) | ((uint64_t)(uint32_t)gz << 16) | (uint32_t)z;
+}
+
+// the tile's nonce word (sc1 load; an empty buffer range without ILC returns 0): loaded
+// unconditionally so that nothing waits for it before the epilogue uses it
+__device__ __forceinline__ uint32_t ilc_nonce(uint16_t *P, const TileId &id, int BN, bool ilc)
+{
+    const int64_t t = (int64_t)id.y * id.gx + id.x;
+    const __amdgpu_buffer_rsrc_t nrs = __builtin_amdgcn_make_buffer_rsrc(
+        ilc ? (void *)(ilc_sync(P, id, BN).nonce + t) : (void *)P, 0, ilc ? 4 : 0, 0x00020000);
+    return __builtin_amdgcn_raw_buffer_load_b32(nrs, 0, 0, 16);
 }
 
 // after store_tile (split-K partial, stored sc1): publish, wait for the tile, sum this
@@ -420,7 +431,8 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[RRG][NB], uint16_t
 
 // AQ: 0 = prepared x~ (X = fp16 [N][K], DEQ layout); 1 = raw fp16 [N][ldx], q8_1 in-kernel;
 // 2 = raw fp16, the fp8 variant's e4m3 quantization in-kernel (F8DEQ x~).
-// spol: cache policy of the split-K partial stores (0 plain, 2 nt, 16 sc1: A/B knob GQ_RGEMM_SPOL).
+// spol: cache policy of the split-K partial stores (0 plain, 2 nt, 16 sc1; kSpol = sc1, measured
+// fastest with the reduce in the timed graph: profiles/r05/rgemm_spol_ab_with_reduce.txt).
 // ilc_gx > 0: the in-launch combine (1-D grid of ilc_gx x ilc_gy tiles x the splits, ilc_tile;
 // P's partials stored sc1 and summed in this launch by ilc_combine); else the 3-D grid, the
 // partials summed by the reduce launch.
@@ -447,13 +459,7 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
     // (ILC) the tile's nonce word, read first: every wave's oldest memory op, so every counted
     // vmcnt wait below still counts only the DMAs younger than it; unconditional (a buffer load of
     // an empty range returns 0 without ILC) so that nothing waits for it before the epilogue
-    uint32_t nonce;
-    {
-        const int64_t t = (int64_t)tile.y * tile.gx + tile.x;
-        const __amdgpu_buffer_rsrc_t nrs = __builtin_amdgcn_make_buffer_rsrc(
-            ilc ? (void *)(ilc_sync(P, tile, G::BN).nonce + t) : (void *)P, 0, ilc ? 4 : 0, 0x00020000);
-        nonce = __builtin_amdgcn_raw_buffer_load_b32(nrs, 0, 0, 16);
-    }
+    const uint32_t nonce = ilc_nonce(P, tile, G::BN, ilc);
 
     // 1. (AQ) the raw activations into registers first: their loads return ahead of the weight
     //    DMAs in this wave's in-order memory queue, so the quantization overlaps the weights' flight
@@ -837,22 +843,29 @@ template <int F, int NB> constexpr int sgemm_lds()
     return SCfg<F, NB>::LDS;
 }
 
+// ilc_gx > 0: the in-launch split-K combine, as rgemm_kernel's (1-D grid, ilc_tile)
 template <int F, int NB>
 __global__ __launch_bounds__(64 * RW) void sgemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
                                                        uint16_t *__restrict__ C, uint16_t *__restrict__ P, int64_t M,
-                                                       int64_t N, int64_t K, int64_t ldc, int spol, int full)
+                                                       int64_t N, int64_t K, int64_t ldc, int spol, int full, int ilc_gx,
+                                                       int ilc_gy)
 {
     __shared__ __attribute__((aligned(1024))) uint8_t lds[sgemm_lds<F, NB>()];
     // split z: super-blocks [z*nsb/S, (z+1)*nsb/S) (split lengths differ by one when S does not divide)
-    const TileId id = grid_tile();
+    const bool ilc = ilc_gx > 0;
+    const TileId id = ilc ? ilc_tile(ilc_gx, ilc_gy) : grid_tile();
     const int64_t nsb = K / 256, s0 = id.z * nsb / id.gz, s1 = (id.z + 1) * nsb / id.gz;
+    const uint32_t nonce = ilc_nonce(P, id, 16 * NB, ilc); // (the oldest memory op: see rgemm_kernel)
+    const int sp = ilc ? 16 : spol;
+    bool done = false;
     if constexpr (F == Q4_K && NB <= 2) {
         if (full) {
-            sgemm_full_body<NB>(A, X, C, P, M, N, K, ldc, spol, id, s0, s1, lds);
-            return;
+            sgemm_full_body<NB>(A, X, C, P, M, N, K, ldc, sp, id, s0, s1, lds);
+            done = true;
         }
     }
-    sgemm_body<F, NB>(A, X, C, P, M, N, K, ldc, spol, id, s0, s1, lds);
+    if (!done) sgemm_body<F, NB>(A, X, C, P, M, N, K, ldc, sp, id, s0, s1, lds);
+    if (ilc && id.gz > 1) ilc_combine<NB>(C, P, M, N, ldc, id, nonce);
 }
 
 // ---- several matrices in one launch (gq_mmq_grouped_prepared): part i = one matrix's
@@ -999,9 +1012,19 @@ template <int F, int NB>
 hipError_t launch_snb(const uint8_t *A, const uint16_t *X, uint16_t *C, void *P, const RGemmPlan &p, int64_t M,
                       int64_t N, int64_t K, int64_t ldc, hipStream_t s)
 {
+    static const int occ = [] {
+        int n = 0;
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, sgemm_kernel<F, NB>, 64 * RW, 0) == hipSuccess ? n : 0;
+    }();
+    const int64_t blocks = (int64_t)p.tiles_m * p.tiles_n * p.splits;
+    if (sgemm_ilc(p) && blocks <= (int64_t)num_cus() * occ) { // one kernel
+        sgemm_kernel<F, NB><<<dim3((unsigned)blocks), dim3(64 * RW), 0, s>>>(A, X, C, (uint16_t *)P, M, N, K, ldc, 16,
+                                                                             tuning().sgemm_full != 0, p.tiles_m, p.tiles_n);
+        return hipGetLastError();
+    }
     const dim3 grid((unsigned)p.tiles_m, (unsigned)p.tiles_n, (unsigned)p.splits);
-    sgemm_kernel<F, NB><<<grid, dim3(64 * RW), 0, s>>>(A, X, C, (uint16_t *)P, M, N, K, ldc, tuning().rgemm_spol,
-                                                        tuning().sgemm_full != 0);
+    sgemm_kernel<F, NB><<<grid, dim3(64 * RW), 0, s>>>(A, X, C, (uint16_t *)P, M, N, K, ldc, kSpol,
+                                                        tuning().sgemm_full != 0, 0, 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.splits == 1) return e;
     return launch_gemm_reduce_f16(NB, RRG, (const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n, s);
@@ -1023,7 +1046,7 @@ hipError_t launch_nb(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t 
         return hipGetLastError();
     }
     const dim3 grid((unsigned)p.tiles_m, (unsigned)p.tiles_n, (unsigned)p.splits);
-    rgemm_kernel<F, NB, AQ><<<grid, dim3(64 * RW), 0, s>>>(A, X, ldx, C, (uint16_t *)P, M, N, K, ldc, tuning().rgemm_spol,
+    rgemm_kernel<F, NB, AQ><<<grid, dim3(64 * RW), 0, s>>>(A, X, ldx, C, (uint16_t *)P, M, N, K, ldc, kSpol,
                                                            0, 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.splits == 1) return e;
@@ -1067,7 +1090,6 @@ RGemmPlan plan_rgemm(int64_t M, int64_t N, int64_t K)
     RGemmPlan p;
     if (M < 1 || N < 1 || K < 256 || K % 256 != 0) return p;
     p.nb = N > 64 ? 8 : (N > 32 ? 4 : (N > 16 ? 2 : 1));
-    if (tuning().rgemm_nb > 0) p.nb = tuning().rgemm_nb; // (A/B knob)
     p.tiles_m = (int)((M + RBM - 1) / RBM);
     p.tiles_n = (int)((N + 16 * p.nb - 1) / (16 * p.nb));
     p.splits = (int)(K / 256);
@@ -1085,6 +1107,12 @@ bool rgemm_ilc(int fmt, const RGemmPlan &p)
 {
     if (!p.ok || p.splits < 2 || tuning().rgemm_ilc == 0) return false;
     return (int64_t)p.tiles_m * p.tiles_n * p.splits <= (int64_t)num_cus() * rgemm_per_cu(fmt, p.nb);
+}
+
+bool sgemm_ilc(const RGemmPlan &p)
+{
+    if (!p.ok || p.splits < 2 || tuning().rgemm_ilc == 0) return false;
+    return (int64_t)p.tiles_m * p.tiles_n * p.splits <= (int64_t)num_cus();
 }
 
 unsigned int ilc_timeouts()
@@ -1105,7 +1133,8 @@ RGemmPlan plan_sgemm(int64_t M, int64_t N, int64_t K, int splits)
     int64_t S = splits > 0 ? splits : (tiles >= cus ? 1 : cus / tiles);
     if (S > nsb) S = nsb;
     p.splits = (int)(S < 1 ? 1 : S);
-    p.partial_bytes = p.splits > 1 ? (size_t)p.splits * tiles * RBM * 16 * p.nb * 2 + (size_t)p.splits * tiles * RW * 4 : 0;
+    const int64_t nblk = tiles * p.splits;
+    p.partial_bytes = p.splits > 1 ? ilc_flags_off(nblk, 16 * p.nb) + ilc_sync_bytes(nblk, tiles) : 0;
     p.ok = true;
     return p;
 }
@@ -1156,15 +1185,13 @@ SGroupPlan plan_sgemm_grouped(const SGroupItem *items, int n, int64_t N, int spl
         // (a 7B layer at 8 / 32 / 64 / 128 tokens: 64.1 / 67.2 / 80.6 / 102.1 us against 66.3
         // per call / 72.7 / 82.0 / 102.6 whole-tile splits: profiles/r04/ab9_layer.txt); single
         // matrices measured slower (GQ_SGEMM_STREAMK=1 forces it there, gq_capi.hip sgemm_streamk)
-        // each unit weighted by its format -- its super-block's bytes (GQ_SGEMM_SKW = 0; bytes + SKW,
-        // or -1: every unit alike, the round-4 split) -- the workgroups splitting the total cost: the
+        // each unit weighted by its format -- its super-block's bytes (every unit alike, the round-4
+        // split, was slower) -- the workgroups splitting the total cost: the
         // 7B layer at 40 / 64 / 128 tokens 77.2 / 78.8 / 100.9 -> 72.2 / 73.4 / 97.8 us
         // (profiles/r05/sgemm_grouped_cost_ab.txt; -55, the K-chunked stream's best, 74.6 / 76.1 / 99.2)
-        const int skw = tuning().sgemm_skw;
         int64_t ctot = 0;
         for (int i = 0; i < n; ++i) {
-            const int sbb = items[i].fmt == Q8_0 ? 272 : (items[i].fmt == Q4_K ? 144 : 210);
-            g.cost[i] = skw < -120 || skw == -1 ? 1 : sbb + skw;
+            g.cost[i] = items[i].fmt == Q8_0 ? 272 : (items[i].fmt == Q4_K ? 144 : 210);
             g.cstart[i] = (int)ctot;
             ctot += (int64_t)g.tiles_m[i] * tn * (items[i].K / 256) * g.cost[i];
         }
@@ -1237,7 +1264,7 @@ hipError_t launch_sgemm_grouped(const SGroupItem *items, int n, int64_t N, const
     RParts r{};
     a.n = n;
     a.N = N;
-    a.spol = tuning().rgemm_spol;
+    a.spol = kSpol;
     a.full = tuning().sgemm_full > 0;
     a.streamk = r.streamk = g.streamk ? 1 : 0;
     a.U = r.U = g.U;

@@ -260,7 +260,7 @@ int gq_version(void);
 /*
  * Debug / tuning only (no counterpart in the reference; not for production callers).  The
  * library reads its GQ_* tuning variables from the environment ONCE, at first use; this entry
- * overrides one of them by name (e.g. "GQ_GEMM_SPLITS", "GQ_RGEMM_NB") for later calls in the
+ * overrides one of them by name (e.g. "GQ_GEMM_SPLITS", "GQ_RGEMM_ILC") for later calls in the
  * process.  Values no kernel is instantiated for are rejected (GQ_EINVAL).  Not thread-safe
  * against calls running concurrently on other threads.  reset: back to the environment's values.
  */

@@ -153,3 +153,26 @@ def test_ilc_graph_replays_and_back_to_back():
         for C in Cs:
             assert torch.equal(C.view(torch.int16), ref.view(torch.int16))
     assert kl.lib().gq_debug_sync_timeouts() == before
+
+
+SGEMM_SHAPES = [("q6_k", 28672, 128, 8192), ("q6_k", 8192, 128, 28672), ("q4_k", 11008, 128, 4096),
+                ("q8_0", 11008, 64, 4096), ("q4_k", 4096, 128, 11008), ("q6_k", 3000, 40, 2048), ("q4_k", 9000, 17, 4096)]
+
+
+@pytest.mark.parametrize("fmt,M,N,K", SGEMM_SHAPES)
+def test_sgemm_ilc_bits_equal_two_launch(fmt, M, N, K, tune):
+    """The streaming GEMM's in-launch combine (sgemm_kernel, its splits chosen to fill one round
+    of the chip): bit for bit the two-launch form, prepared and raw calls."""
+    import kernels._lib as kl
+    tune(GQ_SGEMM=1, GQ_RGEMM=0, GQ_SKINNY=0, GQ_KSTREAM=0)
+    t = kl.TYPES[fmt]
+    name = kl.route_name(t, M, N, K, prepared=True)
+    assert name.startswith("sgemm_kernel"), name
+    A = _t(random_blocks(fmt, M, K, seed=M + 7).view(np.int8))
+    B = _t(random_activations(N, K, seed=N + 11))
+    before = kl.lib().gq_debug_sync_timeouts()
+    for fn in (_prep, _raw):
+        got = fn(kl, t, A, B, M, N, K, "q8_1")
+        ref = _two_launch(kl, fn, t, A, B, M, N, K, "q8_1")
+        assert torch.equal(got.view(torch.int16), ref.view(torch.int16)), (fn.__name__, name)
+    assert kl.lib().gq_debug_sync_timeouts() == before
