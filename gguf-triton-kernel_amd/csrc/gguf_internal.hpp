@@ -171,6 +171,7 @@ struct SGroupPlan {
     int ustart[16] = {}, scap[16] = {};
     int cost[16] = {}, cstart[16] = {}; // stream-K: a part's per-unit cost, the cost before its first unit
     size_t poff[16] = {};
+    size_t foff[16] = {}, noff[16] = {}; // stream-K split parts: the in-launch combine's flags, nonces
     size_t partial_bytes = 0;
 };
 SGroupPlan plan_sgemm_grouped(const SGroupItem *items, int n, int64_t N, int splits);

@@ -199,12 +199,20 @@ __device__ __forceinline__ TileId grid_tile()
 {
     return TileId{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y, (int)gridDim.z};
 }
-// The in-launch combine's 1-D grid (gx > 0): workgroup b = tile * gz + split, a tile's splits
-// consecutive in dispatch order (tile = y * gx + x) -- the block index store_tile already uses.
+// The in-launch combine's 1-D grid (gx > 0): position p = tile * gz + split (tile = y * gx + x,
+// the block index store_tile already uses).  Workgroups are dealt to the 8 XCDs round robin by
+// launch index b, so with 8 | blocks, p = (b % 8) * (blocks / 8) + b / 8: each XCD runs a
+// contiguous run of positions -- a tile's consecutive splits on one XCD, as the 3-D grid had them
+// (neighbouring super-blocks of a row share a 128-byte line: Q4_K's 144-byte super-blocks nearly
+// all do; split over XCDs the line is fetched into two L2s -- the first 1-D order, tile-major in
+// b, measured +3.0 us on Q4_K 4096^2 x128, +0.6 on Q8_0's 272-byte super-blocks,
+// profiles/r06/ilc_ab_v1.txt).  Each XCD dispatches its positions in order, so the tiles complete
+// in order whatever part of the grid is resident.
 __device__ __forceinline__ TileId ilc_tile(int gx, int gy)
 {
-    const int gz = (int)gridDim.x / (gx * gy), b = (int)blockIdx.x, t = b / gz;
-    return TileId{t % gx, t / gx, b - t * gz, gx, gy, gz};
+    const int nb = (int)gridDim.x, gz = nb / (gx * gy), b = (int)blockIdx.x;
+    const int p = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b, t = p / gz;
+    return TileId{t % gx, t / gx, p - t * gz, gx, gy, gz};
 }
 
 // ---- In-launch split-K combine (ILC) -------------------------------------------------------
@@ -250,79 +258,71 @@ __device__ __forceinline__ uint32_t ilc_nonce(uint16_t *P, const TileId &id, int
     return __builtin_amdgcn_raw_buffer_load_b32(nrs, 0, 0, 16);
 }
 
-// after store_tile (split-K partial, stored sc1): publish, wait for the tile, sum this
-// workgroup's share of it into C.  nonce: the tile's nonce word as read at the start (wave 0).
+// wave 0: poll the S flags of one tile (sc1 loads, s_sleep between rounds, bounded); true when
+// all carry {nonce + 1, S, slot}
+__device__ __forceinline__ bool ilc_wait(const uint64_t *tf, uint32_t nonce, int S)
+{
+    const int lane = threadIdx.x & 63;
+    bool ok = false;
+    for (int it = 0; it < kIlcSpins && !ok; ++it) {
+        bool mine = true;
+        for (int s = lane; s < S; s += 64)
+            mine = mine && __hip_atomic_load(tf + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ilc_flag(nonce, S, s);
+        ok = __builtin_amdgcn_ballot_w64(!mine) == 0;
+        if (!ok) __builtin_amdgcn_s_sleep(2);
+    }
+    if (!ok && lane == 0) __hip_atomic_fetch_add(&g_ilc_timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return ok;
+}
+
+// Share k of nsh of one tile's split-K sum into C: units [k U / nsh, (k+1) U / nsh) of store_tile's
+// block order (NB >= 2: 16-byte units = two token tiles of a lane's 4 rows; NB = 1: 8 bytes), the
+// partials of slots 0..S-1 of block row `tile` (blocks tile * slots + s, nblk blocks in all, their
+// exponents after them) summed in slot order -- gemm_reduce_f16_kernel's / reduce_grouped_kernel's
+// arithmetic.  Every load sc1 (the partials were written through by other CUs in this launch).
 template <int NB>
-__device__ __forceinline__ void ilc_combine(uint16_t *__restrict__ C, uint16_t *__restrict__ P, int64_t M, int64_t N,
-                                            int64_t ldc, const TileId &id, uint32_t nonce)
+__device__ __forceinline__ void ilc_sum(uint16_t *__restrict__ C, const uint16_t *__restrict__ P, int64_t M, int64_t N,
+                                        int64_t ldc, int64_t m0, int64_t n0, int64_t tile, int slots, int64_t nblk, int S,
+                                        int k, int nsh)
 {
     constexpr int BN = 16 * NB;
-    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int gz = id.gz, z = id.z;
-    const int64_t tile = (int64_t)id.y * id.gx + id.x;
-    const IlcSync sy = ilc_sync(P, id, BN);
-    // 1. this wave's partial stores written through, then every wave's (barrier), then the flag
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (wave == 0) {
-        uint64_t *tf = sy.flags + tile * gz;
-        if (lane == 0) __hip_atomic_store(tf + z, ilc_flag(nonce, gz, z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // 2. poll the tile's gz flags (sc1 loads), s_sleep between rounds, bounded
-        bool ok = false;
-        for (int it = 0; it < kIlcSpins && !ok; ++it) {
-            bool mine = true;
-            for (int s = lane; s < gz; s += 64)
-                mine = mine && __hip_atomic_load(tf + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ilc_flag(nonce, gz, s);
-            ok = __builtin_amdgcn_ballot_w64(!mine) == 0;
-            if (!ok) __builtin_amdgcn_s_sleep(2);
-        }
-        if (lane == 0) {
-            if (!ok) __hip_atomic_fetch_add(&g_ilc_timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            // every split of the tile has read the nonce (each did before its flag): advance it
-            if (z == 0) __hip_atomic_store(sy.nonce + tile, nonce + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    __syncthreads();
-    // 3. this workgroup's share of the tile: units [z U / gz, (z+1) U / gz) of store_tile's
-    //    block order (NB >= 2: 16-byte units = two token tiles of a lane's 4 rows; NB = 1: 8 bytes)
     constexpr int TPU = NB == 1 ? 1 : 2, UB = 8 * TPU, UPT = RW * RRG * (NB / TPU) * 64;
-    const int64_t nblk = (int64_t)id.gx * id.gy * gz;
+    const int tid = threadIdx.x;
     const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
         (void *)P, 0, (int)(uint32_t)(nblk * (RBM * BN * 2 + RW * 4)), 0x00020000);
-    const int64_t m0 = (int64_t)id.x * RBM, n0 = (int64_t)id.y * BN;
-    const int u0 = (int)((int64_t)z * UPT / gz), u1 = (int)((int64_t)(z + 1) * UPT / gz);
+    const int u0 = (int)((int64_t)k * UPT / nsh), u1 = (int)((int64_t)(k + 1) * UPT / nsh);
     for (int it = u0 + tid; it < u1; it += 64 * RW) {
         const int q = it >> 6, ln = it & 63, u = q % (NB / TPU), wr = q / (NB / TPU), wv = wr / RRG;
         f32x4 acc[TPU];
 #pragma unroll
         for (int j = 0; j < TPU; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
         constexpr int G = 16; // splits in flight per thread
-        for (int s0 = 0; s0 < gz; s0 += G) {
+        for (int s0 = 0; s0 < S; s0 += G) {
             u32x4 v[G];
             float up[G];
 #pragma unroll
-            for (int k = 0; k < G; ++k) { // unconditional (clamped) loads, the surplus zeroed after
-                const uint32_t b = (uint32_t)(tile * gz + (s0 + k < gz ? s0 + k : gz - 1));
+            for (int g = 0; g < G; ++g) { // unconditional (clamped) loads, the surplus zeroed after
+                const uint32_t b = (uint32_t)(tile * slots + (s0 + g < S ? s0 + g : S - 1));
                 const uint32_t eo = (uint32_t)(nblk * (RBM * BN * 2)) + (b * RW + (uint32_t)wv) * 4u;
-                up[k] = __builtin_bit_cast(float, (127u + __builtin_amdgcn_raw_buffer_load_b32(prs, eo, 0, 16)) << 23);
+                up[g] = __builtin_bit_cast(float, (127u + __builtin_amdgcn_raw_buffer_load_b32(prs, eo, 0, 16)) << 23);
                 const uint32_t vo = b * (uint32_t)(RBM * BN * 2) + (uint32_t)it * UB;
                 if constexpr (TPU == 2) {
-                    v[k] = __builtin_amdgcn_raw_buffer_load_b128(prs, vo, 0, 16);
+                    v[g] = __builtin_amdgcn_raw_buffer_load_b128(prs, vo, 0, 16);
                 } else {
                     const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(prs, vo, 0, 16);
-                    v[k] = (u32x4){w.x, w.y, 0u, 0u};
+                    v[g] = (u32x4){w.x, w.y, 0u, 0u};
                 }
             }
 #pragma unroll
-            for (int k = 0; k < G; ++k) {
-                if (s0 + k >= gz) v[k] = (u32x4){0u, 0u, 0u, 0u};
+            for (int g = 0; g < G; ++g) {
+                if (s0 + g >= S) v[g] = (u32x4){0u, 0u, 0u, 0u};
 #pragma unroll
                 for (int j = 0; j < TPU; ++j) {
-                    const uint32_t x0 = j == 0 ? v[k].x : v[k].z, x1 = j == 0 ? v[k].y : v[k].w;
-                    acc[j][0] += h2f(x0 & 0xffffu) * up[k];
-                    acc[j][1] += h2f(x0 >> 16) * up[k];
-                    acc[j][2] += h2f(x1 & 0xffffu) * up[k];
-                    acc[j][3] += h2f(x1 >> 16) * up[k];
+                    const uint32_t x0 = j == 0 ? v[g].x : v[g].z, x1 = j == 0 ? v[g].y : v[g].w;
+                    acc[j][0] += h2f(x0 & 0xffffu) * up[g];
+                    acc[j][1] += h2f(x0 >> 16) * up[g];
+                    acc[j][2] += h2f(x1 & 0xffffu) * up[g];
+                    acc[j][3] += h2f(x1 >> 16) * up[g];
                 }
             }
         }
@@ -341,6 +341,33 @@ __device__ __forceinline__ void ilc_combine(uint16_t *__restrict__ C, uint16_t *
             }
         }
     }
+}
+
+// after store_tile (split-K partial, stored sc1): publish, wait for the tile, sum this
+// workgroup's share of it into C.  nonce: the tile's nonce word as read at the start (wave 0).
+template <int NB>
+__device__ __forceinline__ void ilc_combine(uint16_t *__restrict__ C, uint16_t *__restrict__ P, int64_t M, int64_t N,
+                                            int64_t ldc, const TileId &id, uint32_t nonce)
+{
+    constexpr int BN = 16 * NB;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int gz = id.gz, z = id.z;
+    const int64_t tile = (int64_t)id.y * id.gx + id.x;
+    const IlcSync sy = ilc_sync(P, id, BN);
+    // 1. this wave's partial stores written through, then every wave's (barrier), then the flag
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wave == 0) {
+        uint64_t *tf = sy.flags + tile * gz;
+        if (lane == 0) __hip_atomic_store(tf + z, ilc_flag(nonce, gz, z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ilc_wait(tf, nonce, gz); // 2. every split's flag
+        // every split of the tile has read the nonce (each did before its flag): advance it
+        if (lane == 0 && z == 0) __hip_atomic_store(sy.nonce + tile, nonce + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    // 3. this workgroup's share of the tile
+    ilc_sum<NB>(C, P, M, N, ldc, (int64_t)id.x * RBM, (int64_t)id.y * BN, tile, gz, (int64_t)id.gx * id.gy * gz, gz, z,
+                gz);
 }
 template <int NB>
 __device__ __forceinline__ void store_tile(const f32x4 (&acc)[RRG][NB], uint16_t *__restrict__ C,
@@ -642,6 +669,8 @@ struct SPart {
     int tiles_m, tiles_n, splits, wg0;
     int ustart, scap; // stream-K: the part's first unit (tile-major (tile, super-block) order), partial slots per tile
     int cost, cstart; // stream-K: cost per unit, cost before the part's first unit
+    uint64_t *flags;  // in-launch combine: [tile * scap + slot]
+    uint32_t *nonce;  // [tile]
 };
 struct SParts {
     int n;
@@ -649,6 +678,7 @@ struct SParts {
     int spol;
     int streamk, U, W; // stream-K: U units over W workgroups, workgroup w = units [wU/W, (w+1)U/W)
     int full;          // GQ_SGEMM_FULL (Q4_K, NB <= 2: sgemm_full_body)
+    int ilc;           // stream-K: the split tiles summed in this launch (no reduce launch)
     SPart p[kMaxSParts];
 };
 struct RPart {
@@ -877,6 +907,13 @@ template <int NB> constexpr int max_slds()
 }
 
 template <int NB>
+__global__ __launch_bounds__(64 * RW) void sgemm_grouped_kernel(const SParts a);
+template <int NB> int grouped_occ()
+{
+    int n = 0;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, sgemm_grouped_kernel<NB>, 64 * RW, 0) == hipSuccess ? n : 0;
+}
+template <int NB>
 __global__ __launch_bounds__(64 * RW) void sgemm_grouped_kernel(const SParts a)
 {
     __shared__ __attribute__((aligned(1024))) uint8_t lds[max_slds<NB>()];
@@ -911,6 +948,10 @@ __global__ __launch_bounds__(64 * RW) void sgemm_grouped_kernel(const SParts a)
     // whole, else each of its S_t workgroups writes partial slot k (in workgroup order)
     const int64_t c0 = (int64_t)b * a.U / a.W, c1 = (int64_t)(b + 1) * a.U / a.W;
     bool first = true;
+    // (ILC) the split tiles this workgroup wrote a slot of: only its first and its last tile can be
+    // split (a tile between them lies wholly in its range), so at most two
+    int nsp = 0, sp_part[2], sp_tile[2], sp_k[2], sp_st[2];
+    uint32_t sp_nonce[2];
     for (int i = 0; i < a.n; ++i) {
         const SPart &q = a.p[i];
         const int nsb = (int)(q.K / 256), nu = q.tiles_m * q.tiles_n * nsb;
@@ -925,11 +966,53 @@ __global__ __launch_bounds__(64 * RW) void sgemm_grouped_kernel(const SParts a)
             const int end = u1 < t1 ? u1 : t1;
             const int wf = sk_owner(q, t0, a.U, a.W), st = sk_owner(q, t1 - 1, a.U, a.W) - wf + 1;
             const TileId id{tile % q.tiles_m, tile / q.tiles_m, st == 1 ? 0 : b - wf, q.tiles_m, q.tiles_n, st == 1 ? 1 : q.scap};
+            if (a.ilc && st > 1) { // the tile's nonce word, read before this slot's flag can exist
+                if (nsp < 2) {
+                    const __amdgpu_buffer_rsrc_t nrs = __builtin_amdgcn_make_buffer_rsrc(q.nonce + tile, 0, 4, 0x00020000);
+                    sp_nonce[nsp] = __builtin_amdgcn_raw_buffer_load_b32(nrs, 0, 0, 16);
+                    sp_part[nsp] = i;
+                    sp_tile[nsp] = tile;
+                    sp_k[nsp] = b - wf;
+                    sp_st[nsp] = st;
+                } else if (threadIdx.x == 0) { // (impossible by the plan; made visible, never silent)
+                    __hip_atomic_fetch_add(&g_ilc_timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                ++nsp;
+            }
             if (!first) __builtin_amdgcn_s_barrier(); // (the previous segment's last stage is read by every wave)
             run(q, id, sb, sb + (end - u));
             first = false;
             u = end;
         }
+    }
+    if (!a.ilc || nsp == 0) return;
+    // in-launch combine (ilc_combine's hand-off): every slot this workgroup wrote is published,
+    // then each of its split tiles awaited and this workgroup's share of it (share k of st)
+    // summed into C in slot order -- reduce_grouped_kernel's arithmetic, its bits
+    if (nsp > 2) nsp = 2;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wave == 0) {
+        for (int c = 0; c < nsp; ++c) {
+            const SPart &q = a.p[sp_part[c]];
+            if (lane == 0)
+                __hip_atomic_store(q.flags + (int64_t)sp_tile[c] * q.scap + sp_k[c], ilc_flag(sp_nonce[c], sp_st[c], sp_k[c]),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        for (int c = 0; c < nsp; ++c) {
+            const SPart &q = a.p[sp_part[c]];
+            ilc_wait(q.flags + (int64_t)sp_tile[c] * q.scap, sp_nonce[c], sp_st[c]);
+            if (lane == 0 && sp_k[c] == 0)
+                __hip_atomic_store(q.nonce + sp_tile[c], sp_nonce[c] + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    for (int c = 0; c < nsp; ++c) {
+        const SPart &q = a.p[sp_part[c]];
+        const int t = sp_tile[c];
+        ilc_sum<NB>(q.C, q.P, q.M, a.N, q.ldc, (int64_t)(t % q.tiles_m) * RBM, (int64_t)(t / q.tiles_m) * (16 * NB), t,
+                    q.scap, (int64_t)q.tiles_m * q.tiles_n * q.scap, sp_st[c], sp_k[c], sp_st[c]);
     }
 }
 
@@ -1223,6 +1306,15 @@ SGroupPlan plan_sgemm_grouped(const SGroupItem *items, int n, int64_t N, int spl
             if (cap > 1) pb += ((size_t)cap * nt * (RBM * 16 * g.nb * 2 + RW * 4) + 255) & ~(size_t)255;
             ust += nt * nsb;
         }
+        // the in-launch combine's flags [tile * scap + slot] and nonces [tile] of the split parts
+        for (int i = 0; i < n; ++i) {
+            if (g.scap[i] < 2) continue;
+            const int64_t nt = (int64_t)g.tiles_m[i] * tn;
+            g.foff[i] = pb;
+            pb += (size_t)nt * g.scap[i] * 8;
+            g.noff[i] = pb;
+            pb = (pb + (size_t)nt * 4 + 255) & ~(size_t)255;
+        }
         g.streamk = true;
         g.U = U;
         g.blocks = W;
@@ -1267,6 +1359,9 @@ hipError_t launch_sgemm_grouped(const SGroupItem *items, int n, int64_t N, const
     a.spol = kSpol;
     a.full = tuning().sgemm_full > 0;
     a.streamk = r.streamk = g.streamk ? 1 : 0;
+    static const int occ[4] = {grouped_occ<1>(), grouped_occ<2>(), grouped_occ<4>(), grouped_occ<8>()};
+    const int oc = occ[g.nb == 1 ? 0 : (g.nb == 2 ? 1 : (g.nb == 4 ? 2 : 3))];
+    a.ilc = g.streamk && tuning().rgemm_ilc != 0 && g.blocks <= num_cus() * oc ? 1 : 0;
     a.U = r.U = g.U;
     a.W = r.W = g.blocks;
     r.N = N;
@@ -1275,8 +1370,9 @@ hipError_t launch_sgemm_grouped(const SGroupItem *items, int n, int64_t N, const
     for (int i = 0; i < n; ++i) {
         uint16_t *P = (uint16_t *)((uint8_t *)partials + g.poff[i]);
         a.p[i] = SPart{items[i].fmt, items[i].A, items[i].X, items[i].C, P, items[i].M, items[i].K, items[i].ldc,
-                       g.tiles_m[i], g.tiles_n, g.splits[i], g.wg0[i], g.ustart[i], g.scap[i], g.cost[i], g.cstart[i]};
-        if (g.splits[i] > 1) {
+                       g.tiles_m[i], g.tiles_n, g.splits[i], g.wg0[i], g.ustart[i], g.scap[i], g.cost[i], g.cstart[i],
+                       (uint64_t *)((uint8_t *)partials + g.foff[i]), (uint32_t *)((uint8_t *)partials + g.noff[i])};
+        if (g.splits[i] > 1 && !a.ilc) {
             const int tpu = g.nb == 1 ? 1 : 2, upt = RW * RRG * (g.nb / tpu) * 64, bpt = (upt + UPB - 1) / UPB;
             r.p[r.n++] = RPart{P,         items[i].C, items[i].M, items[i].ldc, g.tiles_m[i], g.tiles_n, g.splits[i], rb,
                                g.ustart[i], (int)(items[i].K / 256), g.scap[i], g.cost[i], g.cstart[i]};
