@@ -176,3 +176,37 @@ def test_sgemm_ilc_bits_equal_two_launch(fmt, M, N, K, tune):
         ref = _two_launch(kl, fn, t, A, B, M, N, K, "q8_1")
         assert torch.equal(got.view(torch.int16), ref.view(torch.int16)), (fn.__name__, name)
     assert kl.lib().gq_debug_sync_timeouts() == before
+
+
+@pytest.mark.parametrize("N", [40, 64, 96, 128])
+def test_grouped_stream_k_ilc_bits_equal_two_launch(N):
+    """The grouped streaming GEMM's stream-K plan (a 7B Q4_K_M layer's seven projections) with
+    its split tiles summed in-launch: every projection bit for bit the reduce_grouped_kernel form."""
+    import kernels._lib as kl
+    from gguf import LLAMA_LAYER_SHAPES, q4_k_m_layer_types
+    kl.reset_tuning()
+    dev = _dev()
+    types = q4_k_m_layer_types(0, 32)
+    x = _t(random_activations(N, 4096, seed=N))
+    h = _t(random_activations(N, 11008, seed=N + 1))
+    wx = torch.empty(kl.workspace_size(kl.GQ_Q4_K, 256, N, 4096), dtype=torch.uint8, device=dev)
+    wh = torch.empty(kl.workspace_size(kl.GQ_Q4_K, 256, N, 11008), dtype=torch.uint8, device=dev)
+    kl.act_prepare(x, N, 4096, wx)
+    kl.act_prepare(h, N, 11008, wh)
+    items = []
+    for i, (n, (M, K)) in enumerate(LLAMA_LAYER_SHAPES.items()):
+        A = _t(random_blocks(types[n], M, K, seed=i).view(np.int8))
+        items.append((kl.TYPES[types[n]], A, wh if K == 11008 else wx, M, K, None))
+    before = kl.lib().gq_debug_sync_timeouts()
+    got = kl.mmq_grouped_prepared(items, N)
+    assert got is not None, kl.lib().gq_last_error()
+    torch.cuda.synchronize()
+    kl.set_tuning("GQ_RGEMM_ILC", 0)
+    try:
+        ref = kl.mmq_grouped_prepared(items, N)
+        torch.cuda.synchronize()
+    finally:
+        kl.reset_tuning()
+    for a, b in zip(got, ref):
+        assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+    assert kl.lib().gq_debug_sync_timeouts() == before
