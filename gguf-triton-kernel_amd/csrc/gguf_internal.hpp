@@ -27,7 +27,7 @@ struct Tuning {
     int sgemm_splits = 0;                     // GQ_SGEMM_SPLITS (0: auto)
     int sgemm_streamk = -1;                   // GQ_SGEMM_STREAMK: stream-K unit split of the auto plan: 1 every
                                               // streaming GEMM, 0 none, -1 the grouped plans (the measured gain)
-    int rgemm_ilc = 1;                        // GQ_RGEMM_ILC: its split-K sum inside the launch where the grid is resident
+    int rgemm_ilc = 0;                        // GQ_RGEMM_ILC: split-K sums inside the GEMM launch (measured slower: opt-in)
     int sgemm_full = -1;                      // GQ_SGEMM_FULL: Q4_K 16/32-token tiles stream whole super-blocks:
                                               // 1 every streaming GEMM, 0 none, -1 single matrices (measured gain)
     int kstream = -1;                         // GQ_KSTREAM: K-chunked streaming MMQ -1 auto / 0 off / 1 wherever it applies

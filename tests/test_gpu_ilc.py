@@ -59,6 +59,10 @@ def _two_launch(kl, fn, *a):
         kl.set_tuning("GQ_RGEMM_ILC", 1)
 
 
+# (the in-launch combine measured 0.3-0.5 us slower than the two launches on every resident shape
+# and 1-4 us on the streaming ones, profiles/r06/ilc_ab_v2.txt: it is opt-in, GQ_RGEMM_ILC=1)
+
+
 SHAPES = [(4096, 128, 4096), (4096, 16, 4096), (4096, 64, 4096), (4096, 33, 4096), (300, 100, 1024),
           (513, 20, 768), (1000, 40, 512), (4096, 128, 2048), (2048, 128, 8192)]
 
@@ -67,7 +71,7 @@ SHAPES = [(4096, 128, 4096), (4096, 16, 4096), (4096, 64, 4096), (4096, 33, 4096
 @pytest.mark.parametrize("M,N,K", SHAPES)
 def test_ilc_bits_equal_two_launch(fmt, M, N, K, tune):
     import kernels._lib as kl
-    tune(GQ_RGEMM=1, GQ_SKINNY=0, GQ_KSTREAM=0)
+    tune(GQ_RGEMM=1, GQ_SKINNY=0, GQ_KSTREAM=0, GQ_RGEMM_ILC=1)
     t = kl.TYPES[fmt]
     A = _t(random_blocks(fmt, M, K, seed=M + K).view(np.int8))
     B = _t(random_activations(N, K, seed=N + 3 * K))
@@ -82,20 +86,22 @@ def test_ilc_bits_equal_two_launch(fmt, M, N, K, tune):
     assert kl.lib().gq_debug_sync_timeouts() == before
 
 
-def test_ilc_is_the_default_route_of_the_headline():
+def test_ilc_route_names(tune):
     import kernels._lib as kl
     kl.reset_tuning()
+    assert kl.route_name(kl.GQ_Q8_0, 4096, 128, 4096) == "rgemm_kernel + gemm_reduce_f16_kernel"
+    tune(GQ_RGEMM_ILC=1)
     assert kl.route_name(kl.GQ_Q8_0, 4096, 128, 4096) == "rgemm_kernel (in-launch split-K sum)"
     assert kl.route_name(kl.GQ_Q8_0, 4096, 128, 4096, prepared=True) == "rgemm_kernel (in-launch split-K sum)"
 
 
 @pytest.mark.parametrize("fill", [None, 0x00, 0xFF, 0x01])
-def test_ilc_workspace_contents_and_reuse(fill):
+def test_ilc_workspace_contents_and_reuse(fill, tune):
     """One workspace reused by a sequence of calls of different split counts, tile counts and
     formats (its flag words then hold every kind of stale value), filled first with garbage,
     zeros, 0xFF or 0x01 bytes: every call equals its two-launch result."""
     import kernels._lib as kl
-    kl.reset_tuning()
+    tune(GQ_RGEMM_ILC=1)
     shapes = [("q8_0", 4096, 128, 4096), ("q4_k", 4096, 128, 2048), ("q8_0", 4096, 128, 4096),
               ("q6_k", 2048, 64, 4096), ("q8_0", 4096, 64, 4096), ("q4_k", 4096, 16, 4096), ("q8_0", 4096, 128, 4096)]
     need = max(int(kl.lib().gq_mmq_call_workspace_size(kl.TYPES[f], 0, M, N, K)) for f, M, N, K in shapes)
@@ -115,12 +121,12 @@ def test_ilc_workspace_contents_and_reuse(fill):
     assert kl.lib().gq_debug_sync_timeouts() == before
 
 
-def test_ilc_graph_replays_and_back_to_back():
+def test_ilc_graph_replays_and_back_to_back(tune):
     """The headline call captured 8 times in one graph (back-to-back launches on one workspace,
     each advancing the tiles' nonces) and the graph replayed 5 times, C poisoned between
     replays: every output equals the eager two-launch result."""
     import kernels._lib as kl
-    kl.reset_tuning()
+    tune(GQ_RGEMM_ILC=1)
     t, M, N, K = kl.GQ_Q8_0, 4096, 128, 4096
     A = _t(random_blocks("q8_0", M, K, seed=5).view(np.int8))
     B = _t(random_activations(N, K, seed=6))
@@ -164,7 +170,7 @@ def test_sgemm_ilc_bits_equal_two_launch(fmt, M, N, K, tune):
     """The streaming GEMM's in-launch combine (sgemm_kernel, its splits chosen to fill one round
     of the chip): bit for bit the two-launch form, prepared and raw calls."""
     import kernels._lib as kl
-    tune(GQ_SGEMM=1, GQ_RGEMM=0, GQ_SKINNY=0, GQ_KSTREAM=0)
+    tune(GQ_SGEMM=1, GQ_RGEMM=0, GQ_SKINNY=0, GQ_KSTREAM=0, GQ_RGEMM_ILC=1)
     t = kl.TYPES[fmt]
     name = kl.route_name(t, M, N, K, prepared=True)
     assert name.startswith("sgemm_kernel"), name
@@ -179,12 +185,12 @@ def test_sgemm_ilc_bits_equal_two_launch(fmt, M, N, K, tune):
 
 
 @pytest.mark.parametrize("N", [40, 64, 96, 128])
-def test_grouped_stream_k_ilc_bits_equal_two_launch(N):
+def test_grouped_stream_k_ilc_bits_equal_two_launch(N, tune):
     """The grouped streaming GEMM's stream-K plan (a 7B Q4_K_M layer's seven projections) with
     its split tiles summed in-launch: every projection bit for bit the reduce_grouped_kernel form."""
     import kernels._lib as kl
     from gguf import LLAMA_LAYER_SHAPES, q4_k_m_layer_types
-    kl.reset_tuning()
+    tune(GQ_RGEMM_ILC=1)
     dev = _dev()
     types = q4_k_m_layer_types(0, 32)
     x = _t(random_activations(N, 4096, seed=N))
@@ -202,11 +208,8 @@ def test_grouped_stream_k_ilc_bits_equal_two_launch(N):
     assert got is not None, kl.lib().gq_last_error()
     torch.cuda.synchronize()
     kl.set_tuning("GQ_RGEMM_ILC", 0)
-    try:
-        ref = kl.mmq_grouped_prepared(items, N)
-        torch.cuda.synchronize()
-    finally:
-        kl.reset_tuning()
+    ref = kl.mmq_grouped_prepared(items, N)
+    torch.cuda.synchronize()
     for a, b in zip(got, ref):
         assert torch.equal(a.view(torch.int16), b.view(torch.int16))
     assert kl.lib().gq_debug_sync_timeouts() == before
