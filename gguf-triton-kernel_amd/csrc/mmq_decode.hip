@@ -606,23 +606,6 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
             };
             const int RS = 64 >> geo.lp2; // rows per pass
             int rp = 0;
-#ifndef GQ_DECODE_ROWPAIR
-#define GQ_DECODE_ROWPAIR 1
-#endif
-            if (GQ_DECODE_ROWPAIR && RS == 1) {
-                // one row per pass (64 lanes per row): two rows at a time, so that the two rows'
-                // dot products and DPP reductions -- independent chains -- interleave; each row's
-                // sum is formed exactly as alone (same lanes, same order: the same bits)
-                float acc2[NT];
-#pragma unroll
-                for (int t = 0; t < NT; ++t) acc2[t] = 0.f;
-                for (; rp + 1 < nr; rp += 2) {
-                    pass(rp, acc);
-                    pass(rp + 1, acc2);
-                    out(rp, acc);
-                    out(rp + 1, acc2);
-                }
-            }
             for (; rp < nr; rp += RS) {
                 pass(rp, acc);
                 out(rp, acc);

@@ -70,7 +70,7 @@ round)
   timeout -k 10 600 python3 tools/pmc_traffic.py $TCFGS > gpurun_out/round_traffic.log 2>&1 &&
   PASSES="FETCH_SIZE|SQ_VALU_MFMA_BUSY_CYCLES,SQ_BUSY_CYCLES,GRBM_GUI_ACTIVE|TA_BUSY_avr,TCC_HIT_sum,TCC_MISS_sum|SQ_INSTS_LDS,SQ_INSTS_VMEM_RD,SQ_INSTS_VALU,SQ_INSTS_MFMA" \
     bash tools/gpu.sh pmc $PCFGS > gpurun_out/round_pmc.log 2>&1 &&
-  timeout -k 10 600 python3 -u bench.py > gpurun_out/round_bench.json 2> gpurun_out/round_bench.err &&
+  timeout -k 10 600 python3 -u bench.py --detail gpurun_out/round_detail.json > gpurun_out/round_bench.json 2> gpurun_out/round_bench.err &&
   mkdir -p gpurun_out/round_prof && cd /tmp && export TMPDIR=/tmp &&
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/round_prof" -o run -- \
     python3 "$ROOT/bench.py" > "$ROOT/gpurun_out/round_prof/bench.json" 2> "$ROOT/gpurun_out/round_prof/bench.err" &&

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (the two-row pass was measured neutral-to-slower and removed after this A/B: profiles/r06/decode_rowpair_ab.txt;
+#  the dpair0 target went with it)
 # Round 6: decode with two-row passes (default) vs without (lib/libgguf_mmq_dpair0.so): the decode
 # parity tests, then interleaved step A/B at one token and the 7B layer at 1-2 tokens.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
