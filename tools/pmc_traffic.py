@@ -24,11 +24,13 @@ OUT = os.path.join(ROOT, "gpurun_out", "pmc_traffic")
 
 
 def run(cfg):
-    d = os.path.join(OUT, cfg)
+    d = os.path.join(OUT, cfg + ("_" + os.path.basename(os.environ["PMC_LIB"]) if os.environ.get("PMC_LIB") else ""))
     os.makedirs(d, exist_ok=True)
     env = dict(os.environ, TMPDIR="/tmp")
+    lib = os.environ.get("PMC_LIB")  # A/B of a diagnostic build: that library, records not written to profiles/
     cmd = ["rocprofv3", "--pmc", "FETCH_SIZE", "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run",
-           "--", sys.executable, os.path.join(ROOT, "tools", "gemm_tune.py"), "--step", cfg]
+           "--", sys.executable, os.path.join(ROOT, "tools", "gemm_tune.py"), "--step"] + \
+          ([f"--lib={os.path.abspath(lib)}"] if lib else []) + [cfg]
     subprocess.run(["timeout", "-k", "10", "120"] + cmd, check=True, cwd="/tmp", env=env,
                    stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     vals = {}
@@ -54,8 +56,10 @@ def run(cfg):
            "fetch_size_kib_mean": sum(v) / len(v), "hbm_bytes_per_launch": hbm,
            "alg_bytes_per_launch": alg, "traffic_over_alg": hbm / alg,
            "method": "rocprofv3 --pmc FETCH_SIZE (own pass), x1024 x2 (gfx950 correction)"}
-    for dst in (os.path.join(ROOT, "profiles"), OUT):  # profiles/ for bench.py, gpurun_out/ to bring back
-        with open(os.path.join(dst, f"pmc_{cfg}.json"), "w") as fh:
+    if lib:
+        rec["lib"] = os.path.basename(lib)
+    for dst in ((OUT,) if lib else (os.path.join(ROOT, "profiles"), OUT)):  # profiles/ for bench.py, gpurun_out/ to bring back
+        with open(os.path.join(dst, f"pmc_{cfg}{'_' + os.path.basename(lib) if lib else ''}.json"), "w") as fh:
             json.dump(rec, fh, indent=1)
     print(json.dumps(rec), flush=True)
 
