@@ -291,7 +291,7 @@ __device__ __forceinline__ void ilc_sum(uint16_t *__restrict__ C, const uint16_t
     const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
         (void *)P, 0, (int)(uint32_t)(nblk * (RBM * BN * 2 + RW * 4)), 0x00020000);
     const int u0 = (int)((int64_t)k * UPT / nsh), u1 = (int)((int64_t)(k + 1) * UPT / nsh);
-    for (int it = u0 + tid; it < u1; it += 64 * RW) {
+    for (int it = u0 + tid; it < u1; it += (int)blockDim.x) {
         const int q = it >> 6, ln = it & 63, u = q % (NB / TPU), wr = q / (NB / TPU), wv = wr / RRG;
         f32x4 acc[TPU];
 #pragma unroll
@@ -369,6 +369,33 @@ __device__ __forceinline__ void ilc_combine(uint16_t *__restrict__ C, uint16_t *
     ilc_sum<NB>(C, P, M, N, ldc, (int64_t)id.x * RBM, (int64_t)id.y * BN, tile, gz, (int64_t)id.gx * id.gy * gz, gz, z,
                 gz);
 }
+// The split-K sum as its own launch (the default; the in-launch combine is opt-in): ilc_sum's
+// arithmetic -- gemm_reduce_f16_kernel's, the same bits -- with 16-byte units, the exponents read
+// by vector loads and every split of a unit in flight at once (S <= 16; gemm_reduce_f16_kernel:
+// 8-byte items, scalar exponent loads, 8 splits per round).  256 threads per workgroup, each
+// workgroup one share of a tile.
+template <int NB>
+__global__ __launch_bounds__(256) void split_reduce_kernel(const uint16_t *__restrict__ P, uint16_t *__restrict__ C,
+                                                           int64_t M, int64_t N, int64_t ldc, int S, int tiles_x,
+                                                           int tiles, int bpt)
+{
+    const int b = (int)blockIdx.x, tile = b / bpt, k = b - tile * bpt;
+    ilc_sum<NB>(C, P, M, N, ldc, (int64_t)(tile % tiles_x) * RBM, (int64_t)(tile / tiles_x) * (16 * NB), tile, S,
+                (int64_t)tiles * S, S, k, bpt);
+}
+template <int NB>
+hipError_t launch_split_reduce(const uint16_t *P, uint16_t *C, int64_t M, int64_t N, int64_t ldc, int S, int tiles_x,
+                               int tiles_y, hipStream_t s)
+{
+    constexpr int TPU = NB == 1 ? 1 : 2, UPT = RW * RRG * (NB / TPU) * 64, BPT = (UPT + 255) / 256;
+    const int tiles = tiles_x * tiles_y;
+    split_reduce_kernel<NB><<<dim3((unsigned)(tiles * BPT)), dim3(256), 0, s>>>(P, C, M, N, ldc, S, tiles_x, tiles, BPT);
+    return hipGetLastError();
+}
+#ifndef GQ_REDUCE_V2
+#define GQ_REDUCE_V2 1 // (A/B builds: -DGQ_REDUCE_V2=0, gemm_reduce_f16_kernel)
+#endif
+
 template <int NB>
 __device__ __forceinline__ void store_tile(const f32x4 (&acc)[RRG][NB], uint16_t *__restrict__ C,
                                            uint16_t *__restrict__ P, int64_t M, int64_t N, int64_t ldc, int spol,
@@ -873,17 +900,30 @@ template <int F, int NB> constexpr int sgemm_lds()
     return SCfg<F, NB>::LDS;
 }
 
-// ilc_gx > 0: the in-launch split-K combine, as rgemm_kernel's (1-D grid, ilc_tile)
+// The streaming GEMM's default 1-D order (gz1 > 0): split-major positions, dealt to the XCDs in
+// contiguous runs (p as ilc_tile's), so that an XCD holds one or two K splits of every row tile
+// instead of every split of a few row tiles -- its L2 then holds its splits' activations only
+// (8192x28672 x128: one 917 KB slice per XCD instead of all eight, 7.3 MB, against a 4 MB L2)
+__device__ __forceinline__ TileId zmajor_tile(int gx, int gy, int gz)
+{
+    const int nb = (int)gridDim.x, b = (int)blockIdx.x, tiles = gx * gy;
+    const int p = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b, z = p / tiles, t = p - z * tiles;
+    return TileId{t % gx, t / gx, z, gx, gy, gz};
+}
+
+// order (1-D grid of gx x gy tiles x the splits): 1 = the in-launch split-K combine, as
+// rgemm_kernel's (ilc_tile); 2 = the split-major order (zmajor_tile), partials summed by the
+// reduce launch; 0 = the 3-D grid
 template <int F, int NB>
 __global__ __launch_bounds__(64 * RW) void sgemm_kernel(const uint8_t *__restrict__ A, const uint16_t *__restrict__ X,
                                                        uint16_t *__restrict__ C, uint16_t *__restrict__ P, int64_t M,
-                                                       int64_t N, int64_t K, int64_t ldc, int spol, int full, int ilc_gx,
-                                                       int ilc_gy)
+                                                       int64_t N, int64_t K, int64_t ldc, int spol, int full, int gx,
+                                                       int gy, int order)
 {
     __shared__ __attribute__((aligned(1024))) uint8_t lds[sgemm_lds<F, NB>()];
     // split z: super-blocks [z*nsb/S, (z+1)*nsb/S) (split lengths differ by one when S does not divide)
-    const bool ilc = ilc_gx > 0;
-    const TileId id = ilc ? ilc_tile(ilc_gx, ilc_gy) : grid_tile();
+    const bool ilc = order == 1;
+    const TileId id = ilc ? ilc_tile(gx, gy) : (order == 2 ? zmajor_tile(gx, gy, (int)gridDim.x / (gx * gy)) : grid_tile());
     const int64_t nsb = K / 256, s0 = id.z * nsb / id.gz, s1 = (id.z + 1) * nsb / id.gz;
     const uint32_t nonce = ilc_nonce(P, id, 16 * NB, ilc); // (the oldest memory op: see rgemm_kernel)
     const int sp = ilc ? 16 : spol;
@@ -1102,14 +1142,28 @@ hipError_t launch_snb(const uint8_t *A, const uint16_t *X, uint16_t *C, void *P,
     const int64_t blocks = (int64_t)p.tiles_m * p.tiles_n * p.splits;
     if (sgemm_ilc(p) && blocks <= (int64_t)num_cus() * occ) { // one kernel
         sgemm_kernel<F, NB><<<dim3((unsigned)blocks), dim3(64 * RW), 0, s>>>(A, X, C, (uint16_t *)P, M, N, K, ldc, 16,
-                                                                             tuning().sgemm_full != 0, p.tiles_m, p.tiles_n);
+                                                                             tuning().sgemm_full != 0, p.tiles_m, p.tiles_n, 1);
         return hipGetLastError();
     }
-    const dim3 grid((unsigned)p.tiles_m, (unsigned)p.tiles_n, (unsigned)p.splits);
-    sgemm_kernel<F, NB><<<grid, dim3(64 * RW), 0, s>>>(A, X, C, (uint16_t *)P, M, N, K, ldc, kSpol,
-                                                        tuning().sgemm_full != 0, 0, 0);
+    // the split-major order where the activations outgrow an XCD's 4 MiB L2 (each XCD then holds
+    // its splits' slices only; 8192x28672 x128: FETCH / algorithmic bytes 1.39 -> 1.07 at the same
+    // time, 97.9 vs 98.1 us).  Below that the 3-D grid's refetches are Infinity-Cache hits that
+    // cost nothing and the split-major order measured 1.5-5% slower (4096x11008 x128 31.3 vs 30.7 us
+    // -- though 1.80 -> 1.12 traffic --, 28672x8192 106.4 vs 104.8; profiles/r06/sgemm_zorder_ab.txt)
+#ifndef GQ_SGEMM_ZORDER
+#define GQ_SGEMM_ZORDER 1 // (A/B builds: -DGQ_SGEMM_ZORDER=0, the 3-D grid everywhere)
+#endif
+    if (GQ_SGEMM_ZORDER && p.splits > 1 && (blocks & 7) == 0 && N * K * 2 > ((int64_t)4 << 20)) {
+        sgemm_kernel<F, NB><<<dim3((unsigned)blocks), dim3(64 * RW), 0, s>>>(A, X, C, (uint16_t *)P, M, N, K, ldc, kSpol,
+                                                                             tuning().sgemm_full != 0, p.tiles_m, p.tiles_n, 2);
+    } else {
+        const dim3 grid((unsigned)p.tiles_m, (unsigned)p.tiles_n, (unsigned)p.splits);
+        sgemm_kernel<F, NB><<<grid, dim3(64 * RW), 0, s>>>(A, X, C, (uint16_t *)P, M, N, K, ldc, kSpol,
+                                                            tuning().sgemm_full != 0, 0, 0, 0);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.splits == 1) return e;
+    if (GQ_REDUCE_V2) return launch_split_reduce<NB>((const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n, s);
     return launch_gemm_reduce_f16(NB, RRG, (const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n, s);
 }
 
@@ -1133,6 +1187,7 @@ hipError_t launch_nb(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t 
                                                            0, 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.splits == 1) return e;
+    if (GQ_REDUCE_V2) return launch_split_reduce<NB>((const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n, s);
     return launch_gemm_reduce_f16(NB, RRG, (const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n, s);
 }
 

@@ -252,9 +252,10 @@ const char *gq_last_error(void);
 
 /* Library ABI version (major * 100 + minor).  103: gq_gemm_item, gq_mmq_grouped_prepared[_workspace_size],
  * gq_debug_route, and larger workspace sizes for the GEMM routes (round 4).  104: gq_mmq_grouped[_ex]
- * takes 5..32 tokens (the K-chunked streaming MMQ; round 5).  105: the resident GEMM sums its split-K
- * partials inside its own launch where the grid is resident (one kernel, no reduce launch); the
- * GEMM workspace sizes grow by that combine's flag words (round 6). */
+ * takes 5..32 tokens (the K-chunked streaming MMQ; round 5).  105: GEMM workspace sizes grow by the
+ * in-launch split-K combine's flag words (opt-in GQ_RGEMM_ILC=1: the resident and streaming GEMMs
+ * sum their split-K partials inside their own launch; measured slower, off by default) and
+ * gq_debug_sync_timeouts (round 6). */
 int gq_version(void);
 
 /*
