@@ -1174,7 +1174,7 @@ const char *gq_debug_route(gq_type t, gq_act act, int64_t M, int64_t N, int64_t 
     if (rgemm_route(t, r.form, M, N, K, act)) {
         const gq::RGemmPlan p = gq::plan_rgemm(M, N, K);
         return p.splits == 1 ? "rgemm_kernel"
-               : gq::rgemm_ilc(t, p) ? "rgemm_kernel (in-launch split-K sum)" : "rgemm_kernel + split_reduce_kernel";
+               : gq::rgemm_ilc(t, p) ? "rgemm_kernel (in-launch split-K sum)" : "rgemm_kernel + gemm_reduce_f16_kernel";
     }
     if (use_skinny(t, r.form, N, act)) return "skinny_kernel";
     if (use_sgemm(t, r.form, M, N, K)) {
@@ -1183,7 +1183,7 @@ const char *gq_debug_route(gq_type t, gq_act act, int64_t M, int64_t N, int64_t 
         if (sgemm_streamk(t, M, N, K, it, g)) return "sgemm_grouped_kernel + reduce_grouped_kernel (stream-K)";
         const gq::RGemmPlan p = sgemm_plan(M, N, K);
         return p.splits == 1 ? "sgemm_kernel"
-               : gq::sgemm_ilc(p) ? "sgemm_kernel (in-launch split-K sum)" : "sgemm_kernel + split_reduce_kernel";
+               : gq::sgemm_ilc(p) ? "sgemm_kernel (in-launch split-K sum)" : "sgemm_kernel + gemm_reduce_f16_kernel";
     }
     return "gemm_kernel + gemm_reduce_f16_kernel";
 }

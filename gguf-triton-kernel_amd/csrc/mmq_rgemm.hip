@@ -369,33 +369,6 @@ __device__ __forceinline__ void ilc_combine(uint16_t *__restrict__ C, uint16_t *
     ilc_sum<NB>(C, P, M, N, ldc, (int64_t)id.x * RBM, (int64_t)id.y * BN, tile, gz, (int64_t)id.gx * id.gy * gz, gz, z,
                 gz);
 }
-// The split-K sum as its own launch (the default; the in-launch combine is opt-in): ilc_sum's
-// arithmetic -- gemm_reduce_f16_kernel's, the same bits -- with 16-byte units, the exponents read
-// by vector loads and every split of a unit in flight at once (S <= 16; gemm_reduce_f16_kernel:
-// 8-byte items, scalar exponent loads, 8 splits per round).  256 threads per workgroup, each
-// workgroup one share of a tile.
-template <int NB>
-__global__ __launch_bounds__(256) void split_reduce_kernel(const uint16_t *__restrict__ P, uint16_t *__restrict__ C,
-                                                           int64_t M, int64_t N, int64_t ldc, int S, int tiles_x,
-                                                           int tiles, int bpt)
-{
-    const int b = (int)blockIdx.x, tile = b / bpt, k = b - tile * bpt;
-    ilc_sum<NB>(C, P, M, N, ldc, (int64_t)(tile % tiles_x) * RBM, (int64_t)(tile / tiles_x) * (16 * NB), tile, S,
-                (int64_t)tiles * S, S, k, bpt);
-}
-template <int NB>
-hipError_t launch_split_reduce(const uint16_t *P, uint16_t *C, int64_t M, int64_t N, int64_t ldc, int S, int tiles_x,
-                               int tiles_y, hipStream_t s)
-{
-    constexpr int TPU = NB == 1 ? 1 : 2, UPT = RW * RRG * (NB / TPU) * 64, BPT = (UPT + 255) / 256;
-    const int tiles = tiles_x * tiles_y;
-    split_reduce_kernel<NB><<<dim3((unsigned)(tiles * BPT)), dim3(256), 0, s>>>(P, C, M, N, ldc, S, tiles_x, tiles, BPT);
-    return hipGetLastError();
-}
-#ifndef GQ_REDUCE_V2
-#define GQ_REDUCE_V2 1 // (A/B builds: -DGQ_REDUCE_V2=0, gemm_reduce_f16_kernel)
-#endif
-
 template <int NB>
 __device__ __forceinline__ void store_tile(const f32x4 (&acc)[RRG][NB], uint16_t *__restrict__ C,
                                            uint16_t *__restrict__ P, int64_t M, int64_t N, int64_t ldc, int spol,
@@ -1163,7 +1136,6 @@ hipError_t launch_snb(const uint8_t *A, const uint16_t *X, uint16_t *C, void *P,
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.splits == 1) return e;
-    if (GQ_REDUCE_V2) return launch_split_reduce<NB>((const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n, s);
     return launch_gemm_reduce_f16(NB, RRG, (const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n, s);
 }
 
@@ -1187,7 +1159,6 @@ hipError_t launch_nb(const uint8_t *A, const uint16_t *X, int64_t ldx, uint16_t 
                                                            0, 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.splits == 1) return e;
-    if (GQ_REDUCE_V2) return launch_split_reduce<NB>((const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n, s);
     return launch_gemm_reduce_f16(NB, RRG, (const uint16_t *)P, C, M, N, ldc, p.splits, p.tiles_m, p.tiles_n, s);
 }
 

@@ -89,7 +89,7 @@ def test_ilc_bits_equal_two_launch(fmt, M, N, K, tune):
 def test_ilc_route_names(tune):
     import kernels._lib as kl
     kl.reset_tuning()
-    assert kl.route_name(kl.GQ_Q8_0, 4096, 128, 4096) == "rgemm_kernel + split_reduce_kernel"
+    assert kl.route_name(kl.GQ_Q8_0, 4096, 128, 4096) == "rgemm_kernel + gemm_reduce_f16_kernel"
     tune(GQ_RGEMM_ILC=1)
     assert kl.route_name(kl.GQ_Q8_0, 4096, 128, 4096) == "rgemm_kernel (in-launch split-K sum)"
     assert kl.route_name(kl.GQ_Q8_0, 4096, 128, 4096, prepared=True) == "rgemm_kernel (in-launch split-K sum)"
