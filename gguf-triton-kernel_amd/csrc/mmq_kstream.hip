@@ -685,26 +685,8 @@ __global__ __launch_bounds__(256) void kstream_reduce_kernel(const KRed r)
     if (q >= (int64_t)r.N * m4) return;
     const int t = (int)(q / m4), m = 4 * (int)(q % m4);
     const size_t zs = (size_t)r.N * M;
-    const float *src = r.P[i] + (size_t)t * M + m;
-    int S = r.S[i];
-    // every range of a group of 8 loaded at once (clamped, the surplus dropped), then summed in
-    // range order -- a load per iteration behind the previous add waited out S round trips
-    f32x4 v = *(const f32x4 *)src;
-#ifndef GQ_KRED_V2
-#define GQ_KRED_V2 1 // (A/B builds: -DGQ_KRED_V2=0, one range per iteration)
-#endif
-    if (!GQ_KRED_V2) {
-        for (int z = 1; z < S; ++z) v += *(const f32x4 *)(src + (size_t)z * zs);
-        S = 1;
-    }
-    for (int z0 = 1; z0 < S; z0 += 8) {
-        f32x4 w[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) w[k] = *(const f32x4 *)(src + (size_t)(z0 + k < S ? z0 + k : S - 1) * zs);
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            if (z0 + k < S) v += w[k];
-    }
+    f32x4 v = *(const f32x4 *)(r.P[i] + (size_t)t * M + m);
+    for (int z = 1; z < r.S[i]; ++z) v += *(const f32x4 *)(r.P[i] + z * zs + (size_t)t * M + m);
     *(u32x2 *)(r.C[i] + t * r.ldc[i] + m) = (u32x2){(uint32_t)f2h_bits(v[0]) | ((uint32_t)f2h_bits(v[1]) << 16),
                                                     (uint32_t)f2h_bits(v[2]) | ((uint32_t)f2h_bits(v[3]) << 16)};
 }
