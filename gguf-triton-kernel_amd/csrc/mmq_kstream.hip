@@ -76,8 +76,11 @@ template <int F> __device__ __forceinline__ uint32_t ksrc(int q)
 // A task: 16 rows x TSB super-blocks of the wave's chunk (Q4_K 2: 4.75 KiB; Q6_K / Q8_0 1: 3.75 /
 // 4.25 KiB), as 16 image rows PPR pieces apart (odd strides spread a fragment's 16 rows over the
 // banks).  Small tasks, so that a ring of 3-4 slots per wave keeps ~100 KiB per CU in flight.
-template <int F> struct KTask {
-    static constexpr int TSB = F == Q4_K && KWPC == 1 ? 2 : 1; // super-blocks per task
+#ifndef GQ_KSTREAM_NB2_TSB
+#define GQ_KSTREAM_NB2_TSB 2 // Q4_K super-blocks per task at 17..32 tokens (A/B builds: 1)
+#endif
+template <int F, int NB = 1> struct KTask {
+    static constexpr int TSB = F == Q4_K && KWPC == 1 ? (NB == 1 ? 2 : GQ_KSTREAM_NB2_TSB) : 1; // super-blocks per task
     static constexpr int PPR0 = TSB * KImg<F>::PPS;    // pieces of a row's task bytes (18 / 15 / 17)
     static constexpr int PPR = PPR0 | 1;               // image row stride in pieces (odd)
     static constexpr int IRS = 16 * PPR;               // image row stride
@@ -320,7 +323,7 @@ template <int F, int NB, int CWM>
 __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int aq, int slot, int ns, uint8_t *smem,
                                       float *scr, int *sync, int &seq)
 {
-    using T = KTask<F>;
+    using T = KTask<F, NB>;
     constexpr int TSB = T::TSB;
     constexpr int NTG = (CWM + TSB - 1) / TSB; // tasks per row group at most
     constexpr uint32_t SB = sb_bytes<F>();
@@ -748,7 +751,8 @@ hipError_t launch_kstream(const KItem *items, int n, int64_t N, int aq, void *pa
             items_total += ng;
             cwm = p.cw > cwm ? p.cw : cwm;
         }
-        const int k = it.fmt == Q4_K ? KTask<Q4_K>::SLOT : (it.fmt == Q6_K ? KTask<Q6_K>::SLOT : KTask<Q8_0>::SLOT);
+        const int k = it.fmt == Q4_K ? (N <= 16 ? KTask<Q4_K, 1>::SLOT : KTask<Q4_K, 2>::SLOT)
+                                     : (it.fmt == Q6_K ? KTask<Q6_K>::SLOT : KTask<Q8_0>::SLOT);
         kb = k > kb ? k : kb;
     }
     a.n = np;
