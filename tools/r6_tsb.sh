@@ -5,8 +5,12 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 VL=gguf-triton-kernel_amd/lib/libgguf_mmq_tsb1.so
-timeout -k 10 300 python3 tools/lib_check.py --lib=$VL q4_k_4096x4096_m32 q4_k_11008x4096_m24 q4_k_4096x4096_m17 > gpurun_out/r6_tsb_check.txt 2>&1
-rc=$?; cat gpurun_out/r6_tsb_check.txt; [ $rc -eq 0 ] || exit $rc
+# (the task size does not change a wave's summation order: the same bits)
+BC="q4_k_4096x4096_m32 q4_k_11008x4096_m24 q4_k_4096x4096_m17 q4_k_4096x11008_m20 q6_k_4096x4096_m32"
+timeout -k 10 300 python3 tools/lib_bits.py --tune=GQ_KSTREAM=1 $BC > gpurun_out/r6_tsb_bits2.txt 2>&1 &&
+timeout -k 10 300 python3 tools/lib_bits.py --lib=$VL --tune=GQ_KSTREAM=1 $BC > gpurun_out/r6_tsb_bits1.txt 2>&1
+rc=$?; cat gpurun_out/r6_tsb_bits2.txt gpurun_out/r6_tsb_bits1.txt; [ $rc -eq 0 ] || exit $rc
+diff gpurun_out/r6_tsb_bits2.txt gpurun_out/r6_tsb_bits1.txt || { echo "TSB bits differ"; exit 1; }
 C="q4_k_4096x4096_m32 q4_k_22016x4096_m32 q4_k_11008x4096_m24 q4_k_4096x4096_m20"
 for r in 1 2 3; do
   timeout -k 10 300 python3 tools/gemm_tune.py $C | sed "s/^/tsb2 /" || exit $?
