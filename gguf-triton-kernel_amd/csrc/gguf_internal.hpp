@@ -194,10 +194,10 @@ struct DecodeItem {
 bool decode_grouped_ok(const DecodeItem *items, int n, int64_t N, bool fp8 = false);
 hipError_t launch_decode_grouped(const DecodeItem *items, int n, int64_t N, hipStream_t s, bool fp8 = false);
 
-// K-chunked streaming MMQ (mmq_kstream.hip, 5..64 tokens): x~ in VGPRs (each of a workgroup's
+// K-chunked streaming MMQ (mmq_kstream.hip, 5..32 tokens): x~ in VGPRs (each of a workgroup's
 // 8 waves one K chunk), weights streamed per wave through private LDS rings, the waves' tiles
-// summed in LDS: one launch, no partials for K <= 4096 at <= 32 tokens.  A longer K is cut into
-// ranges of 16 super-blocks (8 at 33..64 tokens: kstream_splits) whose fp32 partial tiles (kstream_partial_bytes of workspace) one small launch
+// summed in LDS: one launch, no partials for K <= 4096.  A longer K is cut into ranges of 16
+// super-blocks whose fp32 partial tiles (kstream_partial_bytes of workspace) one small launch
 // sums in range order.  Up to kKMaxParts matrices x ranges (own type, activations, output; the
 // same N) in one launch, workgroups apportioned by weight bytes; a matrix's bits do not depend on
 // the launch it is in.  aq: 0 prepared x~ (X = [N][K], ldx = K, act_quant DEQ / F8DEQ), 1 raw fp16
@@ -212,7 +212,7 @@ struct KItem {
     uint16_t *C;
     int64_t ldc, M, K;
 };
-int kstream_splits(int64_t K, int64_t N);
+int kstream_splits(int64_t K);
 int kstream_cw(int64_t N, int64_t K);
 bool kstream_ok(int fmt, int64_t M, int64_t N, int64_t K);
 size_t kstream_partial_bytes(const KItem *items, int n, int64_t N);

@@ -286,9 +286,8 @@ bool use_kstream(int t, int form, int64_t M, int64_t N, int64_t K, int act, bool
     const int ks = gq::tuning().kstream;
     if (ks == 0 || form != gq::AF_F16 || use_blas(N, K) || !gq::kstream_ok(t, M, N, K)) return false;
     if (N < (act == GQ_ACT_FP8_E4M3 ? 3 : 5)) return false;
-    if (gq::kstream_splits(K, N) > 1 && !split && ks != 1) return false;
+    if (gq::kstream_splits(K) > 1 && !split && ks != 1) return false;
     if (ks == 1) return true;
-    if (N > 32) return false; // (33..64 tokens: GQ_KSTREAM=1 only)
     if (gemm_knob_pinned()) return false; // (as the resident / streaming routes: the pinned GEMM takes the call)
     if (prepared) return true;
     // a raw call quantizes in-kernel (every workgroup its whole K of x): ahead of the resident GEMM
@@ -301,7 +300,7 @@ bool use_kstream(int t, int form, int64_t M, int64_t N, int64_t K, int act, bool
 size_t kstream_ws(int t, int64_t M, int64_t N, int64_t K)
 {
     const gq::KItem it{t, nullptr, nullptr, K, nullptr, M, M, K};
-    return gq::kstream_ok(t, M, N, K) ? gq::kstream_partial_bytes(&it, 1, N) : 0;
+    return gq::kstream_ok(t, M, N, K) && N <= 32 ? gq::kstream_partial_bytes(&it, 1, N) : 0;
 }
 // its 32-bit buffer offsets over the activations (rows ldx apart) and the output (rows ldc apart)
 bool kstream_fits(int64_t M, int64_t N, int64_t K, int64_t ldx, int64_t ldc)
@@ -1011,7 +1010,7 @@ int gq_mmq_grouped_ex(gq_act act, const gq_group_item *items, int n, int64_t N, 
         for (int i = 0; i < m; ++i) {
             const gq::DecodeItem &d = di[i];
             // (the grouped launch's own route: the stream wherever it applies, GQ_KSTREAM=0 refuses)
-            if (!use_kstream(d.fmt, gq::AF_F16, d.M, N, d.K, act, true) || gq::kstream_splits(d.K, N) > 1 || d.ldx % 8 != 0 ||
+            if (!use_kstream(d.fmt, gq::AF_F16, d.M, N, d.K, act, true) || gq::kstream_splits(d.K) > 1 || d.ldx % 8 != 0 ||
                 ((uintptr_t)d.X & 15) != 0 || !kstream_fits(d.M, N, d.K, d.ldx, d.ldc))
                 return fail(GQ_EUNSUPPORTED, "item %d: not a grouped K-chunked-stream shape (N=%lld, M=%lld, K=%lld)", i,
                             (long long)N, (long long)d.M, (long long)d.K);
@@ -1064,7 +1063,7 @@ static void grouped_split(gq_act act, gq::SGroupItem *g, int n, int64_t N, gq::K
     int parts = 0;
     for (int i = 0; i < n; ++i) {
         if (g[i].M <= 0) continue;
-        const int np = gq::kstream_splits(g[i].K, N);
+        const int np = gq::kstream_splits(g[i].K);
         if (use_kstream(g[i].fmt, gq::AF_F16, g[i].M, N, g[i].K, act, true, true) &&
             kstream_fits(g[i].M, N, g[i].K, g[i].K, g[i].ldc) && parts + np <= gq::kKMaxParts && (parts += np, true))
             ks[nk++] = gq::KItem{g[i].fmt, g[i].A, g[i].X, g[i].K, g[i].C, g[i].ldc, g[i].M, g[i].K};
@@ -1171,7 +1170,7 @@ const char *gq_debug_route(gq_type t, gq_act act, int64_t M, int64_t N, int64_t 
     if (r.blas) return "dequant_kernel + hipBLASLt";
     if (r.gemv) return "gemv_kernel";
     if (use_kstream(t, r.form, M, N, K, act, prepared != 0))
-        return gq::kstream_splits(K, N) > 1 ? "kstream_kernel + kstream_reduce_kernel" : "kstream_kernel";
+        return gq::kstream_splits(K) > 1 ? "kstream_kernel + kstream_reduce_kernel" : "kstream_kernel";
     if (rgemm_route(t, r.form, M, N, K, act)) {
         const gq::RGemmPlan p = gq::plan_rgemm(M, N, K);
         return p.splits == 1 ? "rgemm_kernel"

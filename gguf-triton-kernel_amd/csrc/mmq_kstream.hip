@@ -19,7 +19,7 @@
 // Work.  An item is a 16-row group of one matrix ("part"; a launch takes up to 16, e.g. a
 // transformer block's projections).  Each workgroup takes a contiguous range of items, balanced
 // by weight bytes.  For every item each wave streams its chunk of the 16 rows -- tasks of 16 rows
-// x 2 / 1 / 1 super-blocks (4.5 / 3.75 / 4.25 KiB for Q4_K / Q6_K / Q8_0) -- through a private LDS
+// x 2 (1 from 17 tokens) / 1 / 1 super-blocks (4.5 / 3.75 / 4.25 KiB for Q4_K / Q6_K / Q8_0) -- through a private LDS
 // ring of up to 4 slots (the tasks after it in flight while one is multiplied: ~100 KiB per CU;
 // the wave waits on its own vmcnt only), and multiplies it into a 16 x 16*NB fp32 tile.  The 8 waves' tiles of an item are summed in LDS in
 // wave order by the last wave to arrive (an LDS counter; no workgroup barrier) and stored as fp16.
@@ -73,14 +73,14 @@ template <int F> __device__ __forceinline__ uint32_t ksrc(int q)
     if constexpr (F == Q6_K) return q < 13 ? 16u * (uint32_t)q : 194u;
     return 16u * (uint32_t)q;
 }
-// A task: 16 rows x TSB super-blocks of the wave's chunk (Q4_K 2: 4.75 KiB; Q6_K / Q8_0 1: 3.75 /
-// 4.25 KiB), as 16 image rows PPR pieces apart (odd strides spread a fragment's 16 rows over the
-// banks).  Small tasks, so that a ring of 3-4 slots per wave keeps ~100 KiB per CU in flight.
-#ifndef GQ_KSTREAM_NB2_TSB
-#define GQ_KSTREAM_NB2_TSB 2 // Q4_K super-blocks per task at 17..32 tokens (A/B builds: 1)
-#endif
+// A task: 16 rows x TSB super-blocks of the wave's chunk (Q4_K 2 at <= 16 tokens: 4.75 KiB, 1 at
+// 17..32: 2.25 KiB; Q6_K / Q8_0 1: 3.75 / 4.25 KiB), as 16 image rows PPR pieces apart (odd
+// strides spread a fragment's 16 rows over the banks).  Small tasks, so that a ring of 3-4 slots
+// per wave keeps ~100 KiB per CU in flight.  (Q4_K at 17..32 tokens with 2 super-blocks per task:
+// 256 VGPRs + 84 bytes of scratch, 8-10% slower on single matrices -- Q4_K 4096^2 x32 11.33 ->
+// 10.22 us, 22016x4096 x32 30.96 -> 28.19 -- and the 7B layer within 1%; profiles/r06/kstream_tsb_ab.txt.)
 template <int F, int NB = 1> struct KTask {
-    static constexpr int TSB = F == Q4_K && KWPC == 1 && (NB == 1 || (NB == 2 && GQ_KSTREAM_NB2_TSB == 2)) ? 2 : 1; // super-blocks per task
+    static constexpr int TSB = F == Q4_K && KWPC == 1 && NB == 1 ? 2 : 1; // super-blocks per task
     static constexpr int PPR0 = TSB * KImg<F>::PPS;    // pieces of a row's task bytes (18 / 15 / 17)
     static constexpr int PPR = PPR0 | 1;               // image row stride in pieces (odd)
     static constexpr int IRS = 16 * PPR;               // image row stride
@@ -88,13 +88,10 @@ template <int F, int NB = 1> struct KTask {
     static constexpr int SLOT = 16 * IRS;              // ring slot bytes (4864 / 3840 / 4352)
 };
 constexpr int KNSMAX = 4;      // ring slots per wave at most
-// x~ super-blocks per wave at most (a K range: 8 waves of them): 2 at 16 / 32 tokens, 1 at 64 --
-// 128 VGPRs of x~ either way
-constexpr int kcwmax(int nb) { return nb == 4 ? 1 : 2; }
-// LDS per wave: its weight ring, and the activation staging before it (passes of KSPB super-blocks);
-// at NB = 4 the 32 KiB tile scratch leaves 15 KiB per wave (one super-block per staging pass)
-template <int NB> constexpr int KRGN = KWPC == 1 ? (NB == 4 ? 15360 : 16384) : 9200;
-template <int NB> constexpr int KSPB = KWPC == 1 && NB < 4 ? 2 : 1;
+constexpr int KCWMAX = 2;      // x~ super-blocks per wave at most (a K range: 16 super-blocks)
+// LDS per wave: its weight ring, and the activation staging before it (passes of KSPB super-blocks)
+constexpr int KRGN = KWPC == 1 ? 16384 : 9200;
+constexpr int KSPB = KWPC == 1 ? 2 : 1;
 template <int NB> constexpr int KIP = NB == 1 && KWPC == 1 ? 2 : 1; // items per LDS reduce
 template <int F> constexpr uint32_t sb_bytes() { return Layout<F>::BYTES * (256 / Layout<F>::QK); }
 
@@ -340,7 +337,7 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
     const int ntg = (mysb + TSB - 1) / TSB;  // this wave's tasks per row group (0..NTG)
     const int ntask = (j1 - j0) * ntg;
     const uint32_t RB = (uint32_t)nsb * SB;
-    uint8_t *ring = smem + wave * KRGN<NB>;
+    uint8_t *ring = smem + wave * KRGN;
 #ifdef GQ_KSTREAM_STAMPS
     const unsigned long long t_in = __builtin_amdgcn_s_memtime();
     unsigned long long t_wait = 0, t_red = 0;
@@ -392,10 +389,10 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
 #pragma unroll
         for (int t = 0; t < NB; ++t)
 #pragma unroll
-            for (int c0 = 0; c0 < CWM; c0 += KSPB<NB>) {
+            for (int c0 = 0; c0 < CWM; c0 += KSPB) {
                 if (c0 >= mysb) break; // (wave-uniform)
                 // a pass: 16 token rows of KSPB super-blocks (RP = 32 * KSPB pieces each)
-                constexpr int RP = 32 * KSPB<NB>;
+                constexpr int RP = 32 * KSPB;
 #pragma unroll
                 for (int i = 0; i < 16 * RP / 64; ++i) {
                     const int r = (64 * i + lane) / RP, pos = (64 * i + lane) % RP;
@@ -408,7 +405,7 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-                for (int cs = 0; cs < KSPB<NB> && c0 + cs < CWM; ++cs) {
+                for (int cs = 0; cs < KSPB && c0 + cs < CWM; ++cs) {
                     const int c = c0 + cs;
                     u32x4 xr[2][4];
 #pragma unroll
@@ -630,32 +627,27 @@ template <int NB, int CWM> hipError_t run(const KArgs &a, unsigned grid, hipStre
         hipFuncAttributes fa;
         hipError_t e = hipFuncGetAttributes(&fa, (const void *)kstream_kernel<NB, CWM>);
         if (e != hipSuccess) return e;
-        if (KWPC * (fa.sharedSizeBytes + (size_t)KW * KRGN<NB>) > 160 * 1024) return hipErrorInvalidValue;
+        if (KWPC * (fa.sharedSizeBytes + (size_t)KW * KRGN) > 160 * 1024) return hipErrorInvalidValue;
         e = hipFuncSetAttribute((const void *)kstream_kernel<NB, CWM>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                KW * KRGN<NB>);
+                                KW * KRGN);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    kstream_kernel<NB, CWM><<<dim3(grid), dim3(64 * KW), (size_t)KW * KRGN<NB>, s>>>(a);
+    kstream_kernel<NB, CWM><<<dim3(grid), dim3(64 * KW), (size_t)KW * KRGN, s>>>(a);
     return hipGetLastError();
 }
 
 } // namespace
 
-// 16-token tiles of an N-token launch (1, 2 or 4)
-static int kstream_nb(int64_t N) { return N <= 16 ? 1 : (N <= 32 ? 2 : 4); }
+// K split over the 8 waves: cw super-blocks each (the fewest that cover K), or 0 when K is
+// longer than the waves' x~ registers hold (2 super-blocks each: K <= 4096)
 // K ranges (split parts) of a matrix: as few as keep each within the 8 waves' x~ registers
-// (2 super-blocks per wave at <= 32 tokens: 16 per range, K <= 4096 in one; 1 at 33..64: 8 per
-// range); cw = super-blocks per wave of a range
-int kstream_splits(int64_t K, int64_t N)
-{
-    const int c = 8 * kcwmax(kstream_nb(N));
-    return (int)((K / 256 + c - 1) / c);
-}
+// (2 super-blocks per wave: 16 per range); cw = super-blocks per wave of a range
+int kstream_splits(int64_t K) { return (int)((K / 256 + 8 * KCWMAX - 1) / (8 * KCWMAX)); }
 int kstream_cw(int64_t N, int64_t K)
 {
-    if (K % 256 != 0 || N < 1 || N > 64) return 0;
-    const int64_t S = kstream_splits(K, N), per = (K / 256 + S - 1) / S;
+    if (K % 256 != 0 || N < 1 || N > 32) return 0;
+    const int64_t S = kstream_splits(K), per = (K / 256 + S - 1) / S;
     return (int)((per + KW - 1) / KW);
 }
 
@@ -671,7 +663,7 @@ size_t kstream_partial_bytes(const KItem *items, int n, int64_t N)
 {
     size_t b = 0;
     for (int i = 0; i < n; ++i) {
-        const int S = kstream_splits(items[i].K, N);
+        const int S = kstream_splits(items[i].K);
         if (S > 1) b += ((size_t)S * N * items[i].M * 4 + 255) & ~(size_t)255;
     }
     return b;
@@ -705,8 +697,7 @@ __global__ __launch_bounds__(256) void kstream_reduce_kernel(const KRed r)
 
 hipError_t launch_kstream(const KItem *items, int n, int64_t N, int aq, void *partials, hipStream_t s)
 {
-    if (n < 1 || n > kKMaxParts || N < 1 || N > 64) return hipErrorInvalidValue;
-    const int nb = kstream_nb(N);
+    if (n < 1 || n > kKMaxParts || N < 1 || N > 32) return hipErrorInvalidValue;
     KArgs a{};
     KRed rd{};
     a.N = (int)N;
@@ -718,7 +709,7 @@ hipError_t launch_kstream(const KItem *items, int n, int64_t N, int aq, void *pa
     for (int i = 0; i < n; ++i) {
         const KItem &it = items[i];
         if (!kstream_ok(it.fmt, it.M, N, it.K)) return hipErrorInvalidValue;
-        const int S = kstream_splits(it.K, N), nsb = (int)(it.K / 256), per = (nsb + S - 1) / S;
+        const int S = kstream_splits(it.K), nsb = (int)(it.K / 256), per = (nsb + S - 1) / S;
         float *P = nullptr;
         if (S > 1) {
             if (!partials || rd.n == kKMaxParts) return hipErrorInvalidValue;
@@ -760,21 +751,19 @@ hipError_t launch_kstream(const KItem *items, int n, int64_t N, int aq, void *pa
             items_total += ng;
             cwm = p.cw > cwm ? p.cw : cwm;
         }
-        const int k = it.fmt == Q4_K ? (nb == 1 ? KTask<Q4_K, 1>::SLOT : (nb == 2 ? KTask<Q4_K, 2>::SLOT : KTask<Q4_K, 4>::SLOT))
+        const int k = it.fmt == Q4_K ? (N <= 16 ? KTask<Q4_K, 1>::SLOT : KTask<Q4_K, 2>::SLOT)
                                      : (it.fmt == Q6_K ? KTask<Q6_K>::SLOT : KTask<Q8_0>::SLOT);
         kb = k > kb ? k : kb;
     }
     a.n = np;
     a.wtot = wcum;
     a.slot = kb;
-    const int rgn = nb == 4 ? KRGN<4> : KRGN<1>;
-    a.ns = rgn / kb > KNSMAX ? KNSMAX : rgn / kb; // ring slots per wave (3 or 4)
+    a.ns = KRGN / kb > KNSMAX ? KNSMAX : KRGN / kb; // ring slots per wave (3 or 4)
     const int64_t wgs = num_cus() * KWPC;
     const unsigned grid = (unsigned)(items_total < wgs ? items_total : wgs);
     hipError_t e;
-    if (nb == 1) e = cwm <= 1 ? run<1, 1>(a, grid, s) : run<1, 2>(a, grid, s);
-    else if (nb == 2) e = cwm <= 1 ? run<2, 1>(a, grid, s) : run<2, 2>(a, grid, s);
-    else e = cwm <= 1 ? run<4, 1>(a, grid, s) : hipErrorInvalidValue; // (kcwmax(4) = 1)
+    if (N <= 16) e = cwm <= 1 ? run<1, 1>(a, grid, s) : run<1, 2>(a, grid, s);
+    else e = cwm <= 1 ? run<2, 1>(a, grid, s) : run<2, 2>(a, grid, s);
     if (e != hipSuccess || rd.n == 0) return e;
     rd.blk0[rd.n] = (int)rblk;
     kstream_reduce_kernel<<<dim3((unsigned)rblk), dim3(256), 0, s>>>(rd);

@@ -1,12 +1,11 @@
-"""GPU parity of the K-chunked streaming MMQ (csrc/mmq_kstream.hip: 5..64 tokens, x~ in VGPRs with
+"""GPU parity of the K-chunked streaming MMQ (csrc/mmq_kstream.hip: 5..32 tokens, x~ in VGPRs with
 each of a workgroup's 8 waves one K chunk, weights streamed per wave through private LDS rings,
 the waves' tiles summed in LDS by the last arriver; one launch, no split-K partials).
 
-Checked: every format at 5..64 tokens (one, two and four 16-token tiles, ragged N), K from one
+Checked: every format at 5..32 tokens (one and two 16-token tiles, ragged N), K from one
 super-block to the longest one launch holds (K = 4096) including K that leaves waves idle or short
 (K = 768, 1280, 2816), and longer K in ranges of 16 super-blocks whose fp32 partials a second
-launch sums (K = 4352: a one-super-block range; 8192, 11008, 28672; at 33..64 tokens ranges of 8
-super-blocks: K = 4096 in two, 11008 in six); the in-kernel quantization
+launch sums (K = 4352: a one-super-block range; 8192, 11008, 28672); the in-kernel quantization
 (gq_mmq_ex) and
 the prepared call (act_quant DEQ + the kernel) agree bit for bit; a grouped launch
 (gq_mmq_grouped_ex, mixed formats and K) gives every item's own bits; repeated calls give the
@@ -50,10 +49,7 @@ CASES = [(4096, 16, 4096), (256, 5, 4096), (1024, 13, 3072), (512, 8, 256), (768
          (1024, 16, 8192), (512, 7, 11008), (256, 32, 4352), (128, 20, 28672),
          # edges: one 16-row item, one super-block (seven of the eight waves idle), the fewest
          # and the most tokens of the two token-group kernels
-         (16, 5, 256), (16, 32, 256), (48, 31, 512), (32, 17, 4096),
-         # four 16-token tiles (33..64 tokens, one super-block per wave, 8 per K range): one range
-         # (K = 2048), one super-block, ranges of 8 + 8 / 8 x 5 + 3, ragged N
-         (4096, 64, 4096), (512, 33, 2048), (48, 48, 256), (2048, 57, 2816), (512, 64, 11008), (64, 40, 1280)]
+         (16, 5, 256), (16, 32, 256), (48, 31, 512), (32, 17, 4096)]
 
 
 @pytest.mark.parametrize("fmt", ["q8_0", "q4_k", "q6_k"])
@@ -80,15 +76,12 @@ def test_kstream_parity(fmt, M, N, K, tune):
     _check_rows(fmt, qA, B, got, M, N, K, seed=M)
 
 
-@pytest.mark.parametrize("N", [16, 48])
-def test_kstream_grouped_prepared_layer(N, tune):
-    """The 7B Q4_K_M layer's projections at 16 / 48 tokens through gq_mmq_grouped_prepared: the
-    K = 4096 items and ffn_down (K = 11008, three / six K ranges) in one K-chunked stream launch +
-    its range sum; every output equals the item's own prepared call, and the oracle within TIGHT on
-    sampled rows.  (33..64 tokens take the stream under GQ_KSTREAM=1 only.)"""
+def test_kstream_grouped_prepared_layer(tune):
+    """The 7B Q4_K_M layer's projections at 16 tokens through gq_mmq_grouped_prepared: the K = 4096
+    items and ffn_down (K = 11008, three K ranges) in one K-chunked stream launch + its range sum;
+    every output equals the item's own prepared call, and the oracle within TIGHT on sampled rows."""
     import kernels._lib as kl
-    if N > 32:
-        tune(GQ_KSTREAM=1)
+    N = 16
     spec = [("q4_k", 4096, 4096), ("q4_k", 1024, 4096), ("q6_k", 2048, 4096), ("q6_k", 4096, 11008)]
     items, wss, Bs, qAs = [], [], [], []
     for i, (fmt, M, K) in enumerate(spec):
@@ -136,8 +129,7 @@ def test_kstream_fp8_matches_prepared_f8deq(tune):
     """The fp8 variant (in-kernel e4m3 quantization) gives the bits of the prepared F8DEQ x~."""
     import kernels._lib as kl
     tune(GQ_KSTREAM=1)
-    for fmt, M, N, K in (("q4_k", 2048, 16, 4096), ("q6_k", 1024, 3, 4096), ("q8_0", 512, 32, 4096),
-                         ("q4_k", 1024, 64, 2048)):
+    for fmt, M, N, K in (("q4_k", 2048, 16, 4096), ("q6_k", 1024, 3, 4096), ("q8_0", 512, 32, 4096)):
         t = kl.TYPES[fmt]
         qA = random_blocks(fmt, M, K, seed=7)
         B = random_activations(N, K, seed=8)

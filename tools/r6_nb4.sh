@@ -1,4 +1,5 @@
 #!/bin/bash
+# (measured and removed: profiles/r06/kstream_nb4_ab.txt -- this script needs the round-6 commit 37193c3 tree)
 # Round 6: the K-chunked stream at 33..64 tokens (four 16-token tiles, one super-block per wave,
 # K ranges of 8 super-blocks; GQ_KSTREAM=1) -- parity first, then A/B against the default routes
 # (resident / streaming GEMM) per matrix and on the 7B layer; then the NB=2 task-size A/B.

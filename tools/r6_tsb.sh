@@ -1,4 +1,5 @@
 #!/bin/bash
+# (adopted: one super-block per task at 17..32 tokens is the product since this A/B; profiles/r06/kstream_tsb_ab.txt)
 # Round 6: the K-chunked stream at 17..32 tokens with one Q4_K super-block per task (no register
 # spill: 253 VGPRs, 0 scratch; lib/libgguf_mmq_tsb1.so) against two (the product: 256 VGPRs +
 # 84 bytes of scratch): parity of the variant (lib_check), then interleaved A/B.
