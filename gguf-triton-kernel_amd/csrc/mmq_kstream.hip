@@ -78,7 +78,9 @@ template <int F> __device__ __forceinline__ uint32_t ksrc(int q)
 // strides spread a fragment's 16 rows over the banks).  Small tasks, so that a ring of 3-4 slots
 // per wave keeps ~100 KiB per CU in flight.  (Q4_K at 17..32 tokens with 2 super-blocks per task:
 // 256 VGPRs + 84 bytes of scratch, 8-10% slower on single matrices -- Q4_K 4096^2 x32 11.33 ->
-// 10.22 us, 22016x4096 x32 30.96 -> 28.19 -- and the 7B layer within 1%; profiles/r06/kstream_tsb_ab.txt.)
+// 10.22 us, 22016x4096 x32 30.96 -> 28.19 -- and the 7B layer within 1%; profiles/r06/kstream_tsb_ab.txt.
+// At <= 16 tokens one super-block per task is the slower one: 4096^2 x16 8.46 -> 8.76, 11008x4096
+// x16 13.93 -> 14.80, the layer x5-16 49.8-50.1 -> 51.4-52.7; kstream_tsb_nb1_ab.txt.)
 template <int F, int NB = 1> struct KTask {
     static constexpr int TSB = F == Q4_K && KWPC == 1 && NB == 1 ? 2 : 1; // super-blocks per task
     static constexpr int PPR0 = TSB * KImg<F>::PPS;    // pieces of a row's task bytes (18 / 15 / 17)
