@@ -43,7 +43,7 @@ namespace gq {
 __device__ unsigned int g_kstream_timeouts;
 
 #ifdef GQ_KSTREAM_STAMPS // diagnostic build: per-wave phase ticks (never the product)
-__device__ unsigned long long g_kstamps[65536][8];
+__device__ unsigned long long g_kstamps[65536][10];
 #endif
 
 namespace {
@@ -91,9 +91,15 @@ template <int F, int NB = 1> struct KTask {
 };
 constexpr int KNSMAX = 4;      // ring slots per wave at most
 constexpr int KCWMAX = 2;      // x~ super-blocks per wave at most (a K range: 16 super-blocks)
+// item-tile scratch buffers of the cross-wave sum: 2 lets a wave run a hand-off further ahead of
+// the summing wave (A/B builds: -DGQ_KSTREAM_DBUF=1)
+#ifndef GQ_KSTREAM_DBUF
+#define GQ_KSTREAM_DBUF 0
+#endif
+constexpr int KDB = GQ_KSTREAM_DBUF ? 2 : 1;
 // LDS per wave: its weight ring, and the activation staging before it (passes of KSPB super-blocks)
-constexpr int KRGN = KWPC == 1 ? 16384 : 9200;
-constexpr int KSPB = KWPC == 1 ? 2 : 1;
+constexpr int KRGN = KWPC == 1 ? (KDB == 2 ? 15360 : 16384) : 9200;
+constexpr int KSPB = KWPC == 1 && KDB == 1 ? 2 : 1;
 template <int NB> constexpr int KIP = NB == 1 && KWPC == 1 ? 2 : 1; // items per LDS reduce
 template <int F> constexpr uint32_t sb_bytes() { return Layout<F>::BYTES * (256 / Layout<F>::QK); }
 
@@ -342,7 +348,7 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
     uint8_t *ring = smem + wave * KRGN;
 #ifdef GQ_KSTREAM_STAMPS
     const unsigned long long t_in = __builtin_amdgcn_s_memtime();
-    unsigned long long t_wait = 0, t_red = 0;
+    unsigned long long t_wait = 0, t_red = 0, t_spin = 0;
 #endif
 
     const __amdgpu_buffer_rsrc_t wrs =
@@ -452,11 +458,22 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
         // of items ahead of the summing wave before it waits here)
         // (bounded: a broken hand-off ends the kernel with wrong bits, counted in
         // g_kstream_timeouts -- gq_debug_sync_timeouts -- never hangs the GPU).
+#ifdef GQ_KSTREAM_STAMPS
+        const unsigned long long ts = __builtin_amdgcn_s_memtime();
+#endif
         int spin = 0;
-        for (; spin < (1 << 22) && __hip_atomic_load(&sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < seq; ++spin)
+        // hand-off seq uses buffer b for the use-th time: free once use b's earlier uses are summed;
+        // per buffer an arrival counter and a summed-uses word (sync[2b], sync[2b + 1])
+        const int b = KDB == 2 ? (seq & 1) : 0, use = KDB == 2 ? (seq >> 1) : seq;
+        int *arr = sync + 2 * b, *done = sync + 2 * b + 1;
+        float *sb = scr + b * (KW * IP * NB * 256);
+        for (; spin < (1 << 22) && __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < use; ++spin)
             __builtin_amdgcn_s_sleep(1);
         if (spin == (1 << 22) && lane == 0)
             __hip_atomic_fetch_add(&g_kstream_timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef GQ_KSTREAM_STAMPS
+        t_spin += __builtin_amdgcn_s_memtime() - ts;
+#endif
         // Ordering: a wave's LDS operations execute in issue order, so only the compiler could
         // move the scratch accesses across the hand-off words; an empty asm with a memory clobber
         // at each edge forbids that.  (Not a fence: any acquire / release, even one restricted to
@@ -466,12 +483,12 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
 #pragma unroll
         for (int ip = 0; ip < IP; ++ip)
 #pragma unroll
-            for (int t = 0; t < NB; ++t) *(f32x4 *)(scr + ((wave * IP + ip) * NB + t) * 256 + 4 * lane) = acc[ip][t];
+            for (int t = 0; t < NB; ++t) *(f32x4 *)(sb + ((wave * IP + ip) * NB + t) * 256 + 4 * lane) = acc[ip][t];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         int old = 0;
         // (the lgkmcnt(0) above: this wave's scratch stores have landed before its arrival; the
         // summing wave's reads below stay after the arrival)
-        if (lane == 0) old = __hip_atomic_fetch_add(&sync[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0) old = __hip_atomic_fetch_add(arr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         asm volatile("" ::: "memory");
         old = __builtin_amdgcn_readfirstlane(old);
         ++seq;
@@ -480,9 +497,9 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
         for (int ip = 0; ip < IP; ++ip)
 #pragma unroll
             for (int t = 0; t < NB; ++t) {
-                f32x4 v = *(const f32x4 *)(scr + (ip * NB + t) * 256 + 4 * lane);
+                f32x4 v = *(const f32x4 *)(sb + (ip * NB + t) * 256 + 4 * lane);
 #pragma unroll
-                for (int w = 1; w < KW; ++w) v += *(const f32x4 *)(scr + ((w * IP + ip) * NB + t) * 256 + 4 * lane);
+                for (int w = 1; w < KW; ++w) v += *(const f32x4 *)(sb + ((w * IP + ip) * NB + t) * 256 + 4 * lane);
                 const int tok = 16 * t + l16, row = 16 * (grp + ip) + 4 * gl; // (M % 16 == 0: 4 rows exist)
                 const bool real = tok < N && ip < np;
                 if (P.P) { // a split part: its fp32 partial
@@ -497,7 +514,7 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
                 }
             }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the scratch reads are done
-        if (lane == 0) __hip_atomic_store(&sync[1], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0) __hip_atomic_store(done, use + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         return true;
     };
 
@@ -592,6 +609,10 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
         g_kstamps[id][3] += t_out - t_pro;
         g_kstamps[id][4] += (unsigned long long)ntask;
         g_kstamps[id][5] += (unsigned long long)(j1 - j0);
+        // this wave's 16-row super-block tasks by format (Q4_K in 6, the others in 7)
+        g_kstamps[id][F == Q4_K ? 6 : 7] += (unsigned long long)((j1 - j0) * mysb);
+        g_kstamps[id][8] += t_spin; // (of t_red: waiting for the previous hand-off's sum)
+        g_kstamps[id][9] += 1;      // parts
     }
 #endif
 }
@@ -600,9 +621,9 @@ template <int NB, int CWM>
 __global__ __launch_bounds__(64 * KW, KWPC * KW / 4) void kstream_kernel(const KArgs a)
 {
     extern __shared__ __attribute__((aligned(1024))) uint8_t smem[]; // the waves' rings (KRGN each)
-    __shared__ __attribute__((aligned(16))) float scr[KW * KIP<NB> * NB * 256]; // the waves' item tiles
-    __shared__ int sync[2]; // arrivals, hand-offs summed
-    if (threadIdx.x < 2) sync[threadIdx.x] = 0;
+    __shared__ __attribute__((aligned(16))) float scr[KDB * KW * KIP<NB> * NB * 256]; // the waves' item tiles
+    __shared__ int sync[2 * KDB]; // per scratch buffer: arrivals, uses summed
+    if (threadIdx.x < 2 * KDB) sync[threadIdx.x] = 0;
     __syncthreads();
     // this workgroup's items: those whose first weight byte (the parts' bytes in order) falls in
     // [t0, t1), an equal share of the launch's cost (weight bytes, weighted per format: launch_kstream)
@@ -786,7 +807,7 @@ extern "C" int gq_debug_kstream_stamps(void *host, size_t bytes)
     if (bytes > sizeof(gq::g_kstamps)) bytes = sizeof(gq::g_kstamps);
     hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(gq::g_kstamps), bytes, 0, hipMemcpyDeviceToHost);
     if (e == hipSuccess) {
-        static unsigned long long zeros[65536][8];
+        static unsigned long long zeros[65536][10];
         e = hipMemcpyToSymbol(HIP_SYMBOL(gq::g_kstamps), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice);
     }
     return e == hipSuccess ? 0 : -1;

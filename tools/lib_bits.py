@@ -30,6 +30,22 @@ kl.reset_tuning()
 for k, v in tune:
     kl.set_tuning(k, int(v))
 for cfg in args:
+    if cfg.startswith("layer_m"):  # the 7B Q4_K_M layer (LayerMix, grouped), every projection's output
+        import bench
+        from gguf import LLAMA_LAYER_SHAPES, q4_k_m_layer_types
+        from kernels.layer_mix import GGUFLinear, LayerMix
+        N = int(cfg[7:])
+        types = q4_k_m_layer_types(0, 32)
+        lin = {n: GGUFLinear(types[n], bench.device_random_blocks(types[n], M, K, dev, seed=i), M, K)
+               for i, (n, (M, K)) in enumerate(LLAMA_LAYER_SHAPES.items())}
+        g = torch.Generator(device=dev).manual_seed(7)
+        x = torch.randn(N, 4096, device=dev, generator=g).to(torch.float16)
+        h = torch.randn(N, 11008, device=dev, generator=g).to(torch.float16)
+        outs = LayerMix(lin, act="q8_1", fuse=True, grouped=True).forward(x, h)
+        torch.cuda.synchronize()
+        print(cfg, *(f"{n}:{hashlib.sha1(o.contiguous().cpu().numpy().tobytes()).hexdigest()[:12]}" for n, o in sorted(outs.items())),
+              flush=True)
+        continue
     fmt = cfg[:4]
     mk, n = cfg[5:].split("_m")
     M, K = map(int, mk.split("x"))
