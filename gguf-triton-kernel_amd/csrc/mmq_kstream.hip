@@ -97,10 +97,14 @@ constexpr int KCWMAX = 2;      // x~ super-blocks per wave at most (a K range: 1
 #define GQ_KSTREAM_DBUF 0
 #endif
 constexpr int KDB = GQ_KSTREAM_DBUF ? 2 : 1;
-// LDS per wave: its weight ring, and the activation staging before it (passes of KSPB super-blocks)
-constexpr int KRGN = KWPC == 1 ? (KDB == 2 ? 15360 : 16384) : 9200;
-constexpr int KSPB = KWPC == 1 && KDB == 1 ? 2 : 1;
-template <int NB> constexpr int KIP = NB == 1 && KWPC == 1 ? 2 : 1; // items per LDS reduce
+#ifndef GQ_KSTREAM_IP2
+#define GQ_KSTREAM_IP2 0 // (A/B builds: 1 -- two items per hand-off at 17..32 tokens too)
+#endif
+template <int NB> constexpr int KIP = (NB == 1 || GQ_KSTREAM_IP2) && KWPC == 1 ? 2 : 1; // items per LDS reduce
+// LDS per wave: its weight ring, and the activation staging before it (passes of KSPB
+// super-blocks); 15 KiB where the tile scratch is 32 KiB
+template <int NB> constexpr int KRGN = KWPC == 1 ? (KDB * KIP<NB> * NB > 2 ? 15360 : 16384) : 9200;
+template <int NB> constexpr int KSPB = KWPC == 1 && KRGN<NB> == 16384 ? 2 : 1;
 template <int F> constexpr uint32_t sb_bytes() { return Layout<F>::BYTES * (256 / Layout<F>::QK); }
 
 // s_waitcnt vmcnt(n) for a wave-uniform n in [LO, HI] (the immediate is an encoding field): a
@@ -345,7 +349,7 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
     const int ntg = (mysb + TSB - 1) / TSB;  // this wave's tasks per row group (0..NTG)
     const int ntask = (j1 - j0) * ntg;
     const uint32_t RB = (uint32_t)nsb * SB;
-    uint8_t *ring = smem + wave * KRGN;
+    uint8_t *ring = smem + wave * KRGN<NB>;
 #ifdef GQ_KSTREAM_STAMPS
     const unsigned long long t_in = __builtin_amdgcn_s_memtime();
     unsigned long long t_wait = 0, t_red = 0, t_spin = 0;
@@ -397,10 +401,10 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
 #pragma unroll
         for (int t = 0; t < NB; ++t)
 #pragma unroll
-            for (int c0 = 0; c0 < CWM; c0 += KSPB) {
+            for (int c0 = 0; c0 < CWM; c0 += KSPB<NB>) {
                 if (c0 >= mysb) break; // (wave-uniform)
                 // a pass: 16 token rows of KSPB super-blocks (RP = 32 * KSPB pieces each)
-                constexpr int RP = 32 * KSPB;
+                constexpr int RP = 32 * KSPB<NB>;
 #pragma unroll
                 for (int i = 0; i < 16 * RP / 64; ++i) {
                     const int r = (64 * i + lane) / RP, pos = (64 * i + lane) % RP;
@@ -413,7 +417,7 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-                for (int cs = 0; cs < KSPB && c0 + cs < CWM; ++cs) {
+                for (int cs = 0; cs < KSPB<NB> && c0 + cs < CWM; ++cs) {
                     const int c = c0 + cs;
                     u32x4 xr[2][4];
 #pragma unroll
@@ -497,9 +501,16 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
         for (int ip = 0; ip < IP; ++ip)
 #pragma unroll
             for (int t = 0; t < NB; ++t) {
-                f32x4 v = *(const f32x4 *)(sb + (ip * NB + t) * 256 + 4 * lane);
+                // the KW tiles read together, one wait (left to itself the compiler waits after
+                // every read here -- 14 serialized LDS round trips on the summing wave, which the
+                // other waves then wait for at their next hand-off), summed in wave order
+                f32x4 r[KW];
 #pragma unroll
-                for (int w = 1; w < KW; ++w) v += *(const f32x4 *)(sb + ((w * IP + ip) * NB + t) * 256 + 4 * lane);
+                for (int w = 0; w < KW; ++w) r[w] = *(const f32x4 *)(sb + ((w * IP + ip) * NB + t) * 256 + 4 * lane);
+                asm volatile("" ::"v"(r[0]), "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), "v"(r[7]));
+                f32x4 v = r[0];
+#pragma unroll
+                for (int w = 1; w < KW; ++w) v += r[w];
                 const int tok = 16 * t + l16, row = 16 * (grp + ip) + 4 * gl; // (M % 16 == 0: 4 rows exist)
                 const bool real = tok < N && ip < np;
                 if (P.P) { // a split part: its fp32 partial
@@ -650,13 +661,13 @@ template <int NB, int CWM> hipError_t run(const KArgs &a, unsigned grid, hipStre
         hipFuncAttributes fa;
         hipError_t e = hipFuncGetAttributes(&fa, (const void *)kstream_kernel<NB, CWM>);
         if (e != hipSuccess) return e;
-        if (KWPC * (fa.sharedSizeBytes + (size_t)KW * KRGN) > 160 * 1024) return hipErrorInvalidValue;
+        if (KWPC * (fa.sharedSizeBytes + (size_t)KW * KRGN<NB>) > 160 * 1024) return hipErrorInvalidValue;
         e = hipFuncSetAttribute((const void *)kstream_kernel<NB, CWM>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                KW * KRGN);
+                                KW * KRGN<NB>);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    kstream_kernel<NB, CWM><<<dim3(grid), dim3(64 * KW), (size_t)KW * KRGN, s>>>(a);
+    kstream_kernel<NB, CWM><<<dim3(grid), dim3(64 * KW), (size_t)KW * KRGN<NB>, s>>>(a);
     return hipGetLastError();
 }
 
@@ -781,7 +792,8 @@ hipError_t launch_kstream(const KItem *items, int n, int64_t N, int aq, void *pa
     a.n = np;
     a.wtot = wcum;
     a.slot = kb;
-    a.ns = KRGN / kb > KNSMAX ? KNSMAX : KRGN / kb; // ring slots per wave (3 or 4)
+    const int rgn = N <= 16 ? KRGN<1> : KRGN<2>;
+    a.ns = rgn / kb > KNSMAX ? KNSMAX : rgn / kb; // ring slots per wave (3 or 4)
     const int64_t wgs = num_cus() * KWPC;
     const unsigned grid = (unsigned)(items_total < wgs ? items_total : wgs);
     hipError_t e;
