@@ -43,7 +43,7 @@ namespace gq {
 __device__ unsigned int g_kstream_timeouts;
 
 #ifdef GQ_KSTREAM_STAMPS // diagnostic build: per-wave phase ticks (never the product)
-__device__ unsigned long long g_kstamps[65536][10];
+__device__ unsigned long long g_kstamps[65536][12];
 #endif
 
 namespace {
@@ -97,6 +97,12 @@ constexpr int KCWMAX = 2;      // x~ super-blocks per wave at most (a K range: 1
 #define GQ_KSTREAM_DBUF 0
 #endif
 constexpr int KDB = GQ_KSTREAM_DBUF ? 2 : 1;
+// the cross-wave sum: 0 = the last wave to arrive sums the whole tile; 1 = every wave sums 1/8 of
+// it once all have arrived (A/B builds: -DGQ_KSTREAM_DSUM=1; one scratch buffer)
+#ifndef GQ_KSTREAM_DSUM
+#define GQ_KSTREAM_DSUM 0
+#endif
+constexpr bool KDS = GQ_KSTREAM_DSUM && !GQ_KSTREAM_DBUF;
 #ifndef GQ_KSTREAM_IP2
 #define GQ_KSTREAM_IP2 0 // (A/B builds: 1 -- two items per hand-off at 17..32 tokens too)
 #endif
@@ -352,7 +358,7 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
     uint8_t *ring = smem + wave * KRGN<NB>;
 #ifdef GQ_KSTREAM_STAMPS
     const unsigned long long t_in = __builtin_amdgcn_s_memtime();
-    unsigned long long t_wait = 0, t_red = 0, t_spin = 0;
+    unsigned long long t_wait = 0, t_red = 0, t_spin = 0, t_sum = 0, n_sum = 0;
 #endif
 
     const __amdgpu_buffer_rsrc_t wrs =
@@ -458,6 +464,73 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
             : __builtin_amdgcn_make_buffer_rsrc((void *)P.C, 0, (int)(uint32_t)(((int64_t)(N - 1) * P.ldc + M) * 2),
                                                 0x00020000);
     auto reduce_store = [&](int grp, int np, const f32x4 (&acc)[IP][NB]) __attribute__((always_inline)) -> bool {
+        if constexpr (KDS) {
+            // every wave: (1) the scratch is free once all KW slices of the previous hand-off are
+            // summed (sync[1] counts slices); (2) its tiles in, arrival (sync[0]); (3) all KW
+            // arrivals; (4) its slice -- UPW 16-byte units of the IP*NB tiles, the same wave-order
+            // sum as the last-arriver form, so the same bits -- stored by one instruction.
+            constexpr int UPW = IP * NB * 64 / KW;
+            auto wait_ge = [&](int *w, int v) __attribute__((always_inline)) {
+                int spin = 0;
+                for (; spin < (1 << 22) && __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < v; ++spin)
+                    __builtin_amdgcn_s_sleep(1);
+                if (spin == (1 << 22) && lane == 0)
+                    __hip_atomic_fetch_add(&g_kstream_timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            };
+#ifdef GQ_KSTREAM_STAMPS
+            const unsigned long long ts = __builtin_amdgcn_s_memtime();
+#endif
+            wait_ge(&sync[1], KW * seq);
+#ifdef GQ_KSTREAM_STAMPS
+            t_spin += __builtin_amdgcn_s_memtime() - ts;
+#endif
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int ip = 0; ip < IP; ++ip)
+#pragma unroll
+                for (int t = 0; t < NB; ++t) *(f32x4 *)(scr + ((wave * IP + ip) * NB + t) * 256 + 4 * lane) = acc[ip][t];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) __hip_atomic_fetch_add(&sync[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            asm volatile("" ::: "memory");
+#ifdef GQ_KSTREAM_STAMPS
+            const unsigned long long ta = __builtin_amdgcn_s_memtime();
+#endif
+            wait_ge(&sync[0], KW * (seq + 1));
+#ifdef GQ_KSTREAM_STAMPS
+            t_spin += __builtin_amdgcn_s_memtime() - ta;
+            const unsigned long long tsum = __builtin_amdgcn_s_memtime();
+            ++n_sum;
+#endif
+            asm volatile("" ::: "memory");
+            const int u = wave * UPW + (lane % UPW); // (lanes past UPW repeat a unit, store nothing)
+            const int ti = u >> 6, ln = u & 63, ip = ti / NB, t = ti - ip * NB;
+            f32x4 r[KW];
+#pragma unroll
+            for (int w = 0; w < KW; ++w) r[w] = *(const f32x4 *)(scr + ((w * IP + ip) * NB + t) * 256 + 4 * ln);
+            asm volatile("" ::"v"(r[0]), "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), "v"(r[7]));
+            f32x4 v = r[0];
+#pragma unroll
+            for (int w = 1; w < KW; ++w) v += r[w];
+            const int tok = 16 * t + (ln & 15), row = 16 * (grp + ip) + 4 * (ln >> 4);
+            const bool real = lane < UPW && tok < N && ip < np;
+            if (P.P) {
+                const uint32_t off = real ? 4u * ((uint32_t)tok * (uint32_t)P.ldc + (uint32_t)row) : 0x80000000u;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), crs, off, 0, 0);
+            } else {
+                const uint32_t off = real ? 2u * ((uint32_t)tok * (uint32_t)P.ldc + (uint32_t)row) : 0x80000000u;
+                __builtin_amdgcn_raw_buffer_store_b64(
+                    (u32x2){(uint32_t)f2h_bits(v[0]) | ((uint32_t)f2h_bits(v[1]) << 16),
+                            (uint32_t)f2h_bits(v[2]) | ((uint32_t)f2h_bits(v[3]) << 16)},
+                    crs, off, 0, 0);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // this wave's scratch reads are done
+            if (lane == 0) __hip_atomic_fetch_add(&sync[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef GQ_KSTREAM_STAMPS
+            t_sum += __builtin_amdgcn_s_memtime() - tsum;
+#endif
+            ++seq;
+            return true;
+        }
         // the scratch is free once the previous hand-off has been summed (a wave is a whole round
         // of items ahead of the summing wave before it waits here)
         // (bounded: a broken hand-off ends the kernel with wrong bits, counted in
@@ -497,6 +570,10 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
         old = __builtin_amdgcn_readfirstlane(old);
         ++seq;
         if ((old & (KW - 1)) != KW - 1) return false;
+#ifdef GQ_KSTREAM_STAMPS
+        const unsigned long long tsum = __builtin_amdgcn_s_memtime();
+        ++n_sum;
+#endif
 #pragma unroll
         for (int ip = 0; ip < IP; ++ip)
 #pragma unroll
@@ -526,6 +603,9 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
             }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the scratch reads are done
         if (lane == 0) __hip_atomic_store(done, use + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef GQ_KSTREAM_STAMPS
+        t_sum += __builtin_amdgcn_s_memtime() - tsum;
+#endif
         return true;
     };
 
@@ -603,7 +683,7 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
 #pragma unroll
                 for (int t = 0; t < NB; ++t) asm volatile("" ::"v"(acc[ip][t]));
         } else if (reduce_store(j0 + gi, np, acc)) {
-            stq += (uint32_t)(IP * NB) * 0x01010101u;
+            stq += (uint32_t)(KDS ? 1 : IP * NB) * 0x01010101u; // (the stores it issued)
         }
 #ifdef GQ_KSTREAM_STAMPS
         t_red += __builtin_amdgcn_s_memtime() - tr;
@@ -624,6 +704,8 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
         g_kstamps[id][F == Q4_K ? 6 : 7] += (unsigned long long)((j1 - j0) * mysb);
         g_kstamps[id][8] += t_spin; // (of t_red: waiting for the previous hand-off's sum)
         g_kstamps[id][9] += 1;      // parts
+        g_kstamps[id][10] += n_sum; // hand-offs this wave summed (the last to arrive)
+        g_kstamps[id][11] += t_sum; // and the ticks it spent summing them
     }
 #endif
 }
@@ -778,7 +860,10 @@ hipError_t launch_kstream(const KItem *items, int n, int64_t N, int aq, void *pa
             // Q6_K 155, Q8_0 217 -- a Q6_K super-block's dequantization costs more per byte than the
             // bytes alone say; the 7B layer 3-4% faster than a deal by bytes at 5..32 tokens (x16
             // 52.7 -> 50.8 us; profiles/r05/kstream_deal_ab.txt).  Any deal gives the same bits.
-            p.w = (int)(16 * p.nsbp * (sbb - 55));
+#ifndef GQ_KSTREAM_SBW_OFF
+#define GQ_KSTREAM_SBW_OFF 55 // (A/B builds: other offsets)
+#endif
+            p.w = (int)(16 * p.nsbp * (sbb - GQ_KSTREAM_SBW_OFF));
             p.wcum = wcum;
             const int64_t ng = it.M / 16;
             wcum += ng * p.w;
@@ -819,7 +904,7 @@ extern "C" int gq_debug_kstream_stamps(void *host, size_t bytes)
     if (bytes > sizeof(gq::g_kstamps)) bytes = sizeof(gq::g_kstamps);
     hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(gq::g_kstamps), bytes, 0, hipMemcpyDeviceToHost);
     if (e == hipSuccess) {
-        static unsigned long long zeros[65536][10];
+        static unsigned long long zeros[65536][12];
         e = hipMemcpyToSymbol(HIP_SYMBOL(gq::g_kstamps), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice);
     }
     return e == hipSuccess ? 0 : -1;

@@ -31,7 +31,7 @@ def main():
     lin = {n: GGUFLinear(types[n], bench.device_random_blocks(types[n], M, K, dev, seed=i), M, K)
            for i, (n, (M, K)) in enumerate(LLAMA_LAYER_SHAPES.items())}
     layer = LayerMix(lin, act="q8_1", fuse=True, grouped=True)
-    buf = np.zeros((65536, 10), np.uint64)
+    buf = np.zeros((65536, 12), np.uint64)
     for N in [int(a) for a in sys.argv[1:]] or [16, 32]:
         g = torch.Generator(device=dev).manual_seed(7)
         x = torch.randn(N, 4096, device=dev, generator=g).to(torch.float16)
@@ -46,7 +46,7 @@ def main():
         ids = np.nonzero(buf[:, 5] > 0)[0]
         u = buf[ids].astype(np.float64)
         pro, wait, red, loop, items, q4, q6 = u[:, 0], u[:, 1], u[:, 2], u[:, 3], u[:, 5], u[:, 6], u[:, 7]
-        spin, parts = u[:, 8], u[:, 9]
+        spin, parts, nsum, tsum = u[:, 8], u[:, 9], u[:, 10], u[:, 11]
         os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
         np.savez(os.path.join(ROOT, "gpurun_out", f"klayer_stamps_n{N}.npz"), ids=ids, u=u)
         wg = ids // 8
@@ -70,6 +70,13 @@ def main():
         print(f"   fit workgroup time = {coef[0]:.0f} * Q4_K task + {coef[1]:.0f} * Q6_K task + {coef[2]:.0f} * item "
               f"+ {coef[3]:.0f} * part  (per wave; Q6_K / Q4_K {coef[1] / coef[0]:.2f}, deal weights 155 / 89 = 1.74); "
               f"residual rms {np.sqrt(np.mean(resid ** 2)):.0f}")
+        # who sums: per workgroup, the share of its hand-offs summed by its most frequent summer
+        # (1/8 if the last arrival rotates, 1 if one wave is always last)
+        share = np.array([nsum[wg == w].max() / max(nsum[wg == w].sum(), 1) for w in wgs])
+        wv = ids % 8
+        print(f"   summing: ticks per summed hand-off med {np.median(tsum[nsum > 0] / nsum[nsum > 0]):.0f}; "
+              f"top summer's share per workgroup med {np.median(share):.2f} p90 {np.percentile(share, 90):.2f}; "
+              f"hand-offs summed by wave index 0..7: {[int(nsum[wv == k].sum()) for k in range(8)]}")
         for name, sel in (("Q4_K-only", wq6 == 0), ("Q6_K-only", wq4 == 0), ("mixed", (wq4 > 0) & (wq6 > 0))):
             if sel.any():
                 print(f"   {name} workgroups {sel.sum()}: time mean {wt[sel].mean():.0f} max {wt[sel].max():.0f}, "

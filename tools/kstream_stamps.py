@@ -35,7 +35,7 @@ def main():
         prepared = mode == "prepared"
         if prepared:
             r.prepare()
-        buf = np.zeros((65536, 10), np.uint64)
+        buf = np.zeros((65536, 12), np.uint64)
         for i in range(3):  # warm, then the stamped call alone
             (r.kernel if prepared else r.step)(i, i % r.ncopies)
         torch.cuda.synchronize()
