@@ -103,6 +103,13 @@ constexpr int KDB = GQ_KSTREAM_DBUF ? 2 : 1;
 #define GQ_KSTREAM_DSUM 0
 #endif
 constexpr bool KDS = GQ_KSTREAM_DSUM && !GQ_KSTREAM_DBUF;
+// issue priority (A/B builds): 0 none (age: waves 4-7, dispatched second, lose every arbitration
+// and one of them is always the last to arrive); 1 = waves 4-7 at priority 1; 2 = by position --
+// a wave that arrived and is not the last yields (0), the last arriver leads (2) until its next
+// hand-off, every wave past a hand-off wait is at 1
+#ifndef GQ_KSTREAM_PRIO
+#define GQ_KSTREAM_PRIO 0
+#endif
 #ifndef GQ_KSTREAM_IP2
 #define GQ_KSTREAM_IP2 0 // (A/B builds: 1 -- two items per hand-off at 17..32 tokens too)
 #endif
@@ -551,6 +558,7 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
 #ifdef GQ_KSTREAM_STAMPS
         t_spin += __builtin_amdgcn_s_memtime() - ts;
 #endif
+        if (GQ_KSTREAM_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         // Ordering: a wave's LDS operations execute in issue order, so only the compiler could
         // move the scratch accesses across the hand-off words; an empty asm with a memory clobber
         // at each edge forbids that.  (Not a fence: any acquire / release, even one restricted to
@@ -569,6 +577,10 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
         asm volatile("" ::: "memory");
         old = __builtin_amdgcn_readfirstlane(old);
         ++seq;
+        if (GQ_KSTREAM_PRIO == 2) {
+            if ((old & (KW - 1)) != KW - 1) __builtin_amdgcn_s_setprio(0);
+            else __builtin_amdgcn_s_setprio(2);
+        }
         if ((old & (KW - 1)) != KW - 1) return false;
 #ifdef GQ_KSTREAM_STAMPS
         const unsigned long long tsum = __builtin_amdgcn_s_memtime();
@@ -717,6 +729,8 @@ __global__ __launch_bounds__(64 * KW, KWPC * KW / 4) void kstream_kernel(const K
     __shared__ __attribute__((aligned(16))) float scr[KDB * KW * KIP<NB> * NB * 256]; // the waves' item tiles
     __shared__ int sync[2 * KDB]; // per scratch buffer: arrivals, uses summed
     if (threadIdx.x < 2 * KDB) sync[threadIdx.x] = 0;
+    if (GQ_KSTREAM_PRIO == 1 && threadIdx.x >= 256) __builtin_amdgcn_s_setprio(1); // (wave-uniform)
+    if (GQ_KSTREAM_PRIO == 2) __builtin_amdgcn_s_setprio(1);
     __syncthreads();
     // this workgroup's items: those whose first weight byte (the parts' bytes in order) falls in
     // [t0, t1), an equal share of the launch's cost (weight bytes, weighted per format: launch_kstream)
