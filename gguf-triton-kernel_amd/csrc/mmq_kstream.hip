@@ -91,33 +91,13 @@ template <int F, int NB = 1> struct KTask {
 };
 constexpr int KNSMAX = 4;      // ring slots per wave at most
 constexpr int KCWMAX = 2;      // x~ super-blocks per wave at most (a K range: 16 super-blocks)
-// item-tile scratch buffers of the cross-wave sum: 2 lets a wave run a hand-off further ahead of
-// the summing wave (A/B builds: -DGQ_KSTREAM_DBUF=1)
-#ifndef GQ_KSTREAM_DBUF
-#define GQ_KSTREAM_DBUF 0
-#endif
-constexpr int KDB = GQ_KSTREAM_DBUF ? 2 : 1;
-// the cross-wave sum: 0 = the last wave to arrive sums the whole tile; 1 = every wave sums 1/8 of
-// it once all have arrived (A/B builds: -DGQ_KSTREAM_DSUM=1; one scratch buffer)
-#ifndef GQ_KSTREAM_DSUM
-#define GQ_KSTREAM_DSUM 0
-#endif
-constexpr bool KDS = GQ_KSTREAM_DSUM && !GQ_KSTREAM_DBUF;
-// issue priority (A/B builds): 0 none (age: waves 4-7, dispatched second, lose every arbitration
-// and one of them is always the last to arrive); 1 = waves 4-7 at priority 1; 2 = by position --
-// a wave that arrived and is not the last yields (0), the last arriver leads (2) until its next
-// hand-off, every wave past a hand-off wait is at 1
-#ifndef GQ_KSTREAM_PRIO
-#define GQ_KSTREAM_PRIO 0
-#endif
-#ifndef GQ_KSTREAM_IP2
-#define GQ_KSTREAM_IP2 0 // (A/B builds: 1 -- two items per hand-off at 17..32 tokens too)
-#endif
-template <int NB> constexpr int KIP = (NB == 1 || GQ_KSTREAM_IP2) && KWPC == 1 ? 2 : 1; // items per LDS reduce
-// LDS per wave: its weight ring, and the activation staging before it (passes of KSPB
-// super-blocks); 15 KiB where the tile scratch is 32 KiB
-template <int NB> constexpr int KRGN = KWPC == 1 ? (KDB * KIP<NB> * NB > 2 ? 15360 : 16384) : 9200;
-template <int NB> constexpr int KSPB = KWPC == 1 && KRGN<NB> == 16384 ? 2 : 1;
+template <int NB> constexpr int KIP = NB == 1 && KWPC == 1 ? 2 : 1; // items per LDS reduce
+// LDS per wave: its weight ring, and the activation staging before it (passes of KSPB super-blocks)
+// (a 32 KiB tile scratch -- two buffers, or two items per hand-off at 17..32 tokens -- leaves 15
+// KiB rings and one-super-block staging passes: measured slower, profiles/r06/kstream_dbuf_ab.txt,
+// kstream_ip2_ab.txt)
+constexpr int KRGN = KWPC == 1 ? 16384 : 9200;
+constexpr int KSPB = KWPC == 1 ? 2 : 1;
 template <int F> constexpr uint32_t sb_bytes() { return Layout<F>::BYTES * (256 / Layout<F>::QK); }
 
 // s_waitcnt vmcnt(n) for a wave-uniform n in [LO, HI] (the immediate is an encoding field): a
@@ -362,7 +342,7 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
     const int ntg = (mysb + TSB - 1) / TSB;  // this wave's tasks per row group (0..NTG)
     const int ntask = (j1 - j0) * ntg;
     const uint32_t RB = (uint32_t)nsb * SB;
-    uint8_t *ring = smem + wave * KRGN<NB>;
+    uint8_t *ring = smem + wave * KRGN;
 #ifdef GQ_KSTREAM_STAMPS
     const unsigned long long t_in = __builtin_amdgcn_s_memtime();
     unsigned long long t_wait = 0, t_red = 0, t_spin = 0, t_sum = 0, n_sum = 0;
@@ -414,10 +394,10 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
 #pragma unroll
         for (int t = 0; t < NB; ++t)
 #pragma unroll
-            for (int c0 = 0; c0 < CWM; c0 += KSPB<NB>) {
+            for (int c0 = 0; c0 < CWM; c0 += KSPB) {
                 if (c0 >= mysb) break; // (wave-uniform)
                 // a pass: 16 token rows of KSPB super-blocks (RP = 32 * KSPB pieces each)
-                constexpr int RP = 32 * KSPB<NB>;
+                constexpr int RP = 32 * KSPB;
 #pragma unroll
                 for (int i = 0; i < 16 * RP / 64; ++i) {
                     const int r = (64 * i + lane) / RP, pos = (64 * i + lane) % RP;
@@ -430,7 +410,7 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-                for (int cs = 0; cs < KSPB<NB> && c0 + cs < CWM; ++cs) {
+                for (int cs = 0; cs < KSPB && c0 + cs < CWM; ++cs) {
                     const int c = c0 + cs;
                     u32x4 xr[2][4];
 #pragma unroll
@@ -471,73 +451,6 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
             : __builtin_amdgcn_make_buffer_rsrc((void *)P.C, 0, (int)(uint32_t)(((int64_t)(N - 1) * P.ldc + M) * 2),
                                                 0x00020000);
     auto reduce_store = [&](int grp, int np, const f32x4 (&acc)[IP][NB]) __attribute__((always_inline)) -> bool {
-        if constexpr (KDS) {
-            // every wave: (1) the scratch is free once all KW slices of the previous hand-off are
-            // summed (sync[1] counts slices); (2) its tiles in, arrival (sync[0]); (3) all KW
-            // arrivals; (4) its slice -- UPW 16-byte units of the IP*NB tiles, the same wave-order
-            // sum as the last-arriver form, so the same bits -- stored by one instruction.
-            constexpr int UPW = IP * NB * 64 / KW;
-            auto wait_ge = [&](int *w, int v) __attribute__((always_inline)) {
-                int spin = 0;
-                for (; spin < (1 << 22) && __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < v; ++spin)
-                    __builtin_amdgcn_s_sleep(1);
-                if (spin == (1 << 22) && lane == 0)
-                    __hip_atomic_fetch_add(&g_kstream_timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            };
-#ifdef GQ_KSTREAM_STAMPS
-            const unsigned long long ts = __builtin_amdgcn_s_memtime();
-#endif
-            wait_ge(&sync[1], KW * seq);
-#ifdef GQ_KSTREAM_STAMPS
-            t_spin += __builtin_amdgcn_s_memtime() - ts;
-#endif
-            asm volatile("" ::: "memory");
-#pragma unroll
-            for (int ip = 0; ip < IP; ++ip)
-#pragma unroll
-                for (int t = 0; t < NB; ++t) *(f32x4 *)(scr + ((wave * IP + ip) * NB + t) * 256 + 4 * lane) = acc[ip][t];
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (lane == 0) __hip_atomic_fetch_add(&sync[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            asm volatile("" ::: "memory");
-#ifdef GQ_KSTREAM_STAMPS
-            const unsigned long long ta = __builtin_amdgcn_s_memtime();
-#endif
-            wait_ge(&sync[0], KW * (seq + 1));
-#ifdef GQ_KSTREAM_STAMPS
-            t_spin += __builtin_amdgcn_s_memtime() - ta;
-            const unsigned long long tsum = __builtin_amdgcn_s_memtime();
-            ++n_sum;
-#endif
-            asm volatile("" ::: "memory");
-            const int u = wave * UPW + (lane % UPW); // (lanes past UPW repeat a unit, store nothing)
-            const int ti = u >> 6, ln = u & 63, ip = ti / NB, t = ti - ip * NB;
-            f32x4 r[KW];
-#pragma unroll
-            for (int w = 0; w < KW; ++w) r[w] = *(const f32x4 *)(scr + ((w * IP + ip) * NB + t) * 256 + 4 * ln);
-            asm volatile("" ::"v"(r[0]), "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), "v"(r[7]));
-            f32x4 v = r[0];
-#pragma unroll
-            for (int w = 1; w < KW; ++w) v += r[w];
-            const int tok = 16 * t + (ln & 15), row = 16 * (grp + ip) + 4 * (ln >> 4);
-            const bool real = lane < UPW && tok < N && ip < np;
-            if (P.P) {
-                const uint32_t off = real ? 4u * ((uint32_t)tok * (uint32_t)P.ldc + (uint32_t)row) : 0x80000000u;
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), crs, off, 0, 0);
-            } else {
-                const uint32_t off = real ? 2u * ((uint32_t)tok * (uint32_t)P.ldc + (uint32_t)row) : 0x80000000u;
-                __builtin_amdgcn_raw_buffer_store_b64(
-                    (u32x2){(uint32_t)f2h_bits(v[0]) | ((uint32_t)f2h_bits(v[1]) << 16),
-                            (uint32_t)f2h_bits(v[2]) | ((uint32_t)f2h_bits(v[3]) << 16)},
-                    crs, off, 0, 0);
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // this wave's scratch reads are done
-            if (lane == 0) __hip_atomic_fetch_add(&sync[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#ifdef GQ_KSTREAM_STAMPS
-            t_sum += __builtin_amdgcn_s_memtime() - tsum;
-#endif
-            ++seq;
-            return true;
-        }
         // the scratch is free once the previous hand-off has been summed (a wave is a whole round
         // of items ahead of the summing wave before it waits here)
         // (bounded: a broken hand-off ends the kernel with wrong bits, counted in
@@ -546,19 +459,14 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
         const unsigned long long ts = __builtin_amdgcn_s_memtime();
 #endif
         int spin = 0;
-        // hand-off seq uses buffer b for the use-th time: free once use b's earlier uses are summed;
-        // per buffer an arrival counter and a summed-uses word (sync[2b], sync[2b + 1])
-        const int b = KDB == 2 ? (seq & 1) : 0, use = KDB == 2 ? (seq >> 1) : seq;
-        int *arr = sync + 2 * b, *done = sync + 2 * b + 1;
-        float *sb = scr + b * (KW * IP * NB * 256);
-        for (; spin < (1 << 22) && __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < use; ++spin)
+        for (; spin < (1 << 22) && __hip_atomic_load(&sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < seq; ++spin)
             __builtin_amdgcn_s_sleep(1);
         if (spin == (1 << 22) && lane == 0)
             __hip_atomic_fetch_add(&g_kstream_timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef GQ_KSTREAM_STAMPS
         t_spin += __builtin_amdgcn_s_memtime() - ts;
 #endif
-        if (GQ_KSTREAM_PRIO == 2) __builtin_amdgcn_s_setprio(1);
+        __builtin_amdgcn_s_setprio(1); // (issue priority: see the arrival below)
         // Ordering: a wave's LDS operations execute in issue order, so only the compiler could
         // move the scratch accesses across the hand-off words; an empty asm with a memory clobber
         // at each edge forbids that.  (Not a fence: any acquire / release, even one restricted to
@@ -568,20 +476,27 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
 #pragma unroll
         for (int ip = 0; ip < IP; ++ip)
 #pragma unroll
-            for (int t = 0; t < NB; ++t) *(f32x4 *)(sb + ((wave * IP + ip) * NB + t) * 256 + 4 * lane) = acc[ip][t];
+            for (int t = 0; t < NB; ++t) *(f32x4 *)(scr + ((wave * IP + ip) * NB + t) * 256 + 4 * lane) = acc[ip][t];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         int old = 0;
         // (the lgkmcnt(0) above: this wave's scratch stores have landed before its arrival; the
         // summing wave's reads below stay after the arrival)
-        if (lane == 0) old = __hip_atomic_fetch_add(arr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0) old = __hip_atomic_fetch_add(&sync[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         asm volatile("" ::: "memory");
         old = __builtin_amdgcn_readfirstlane(old);
         ++seq;
-        if (GQ_KSTREAM_PRIO == 2) {
-            if ((old & (KW - 1)) != KW - 1) __builtin_amdgcn_s_setprio(0);
-            else __builtin_amdgcn_s_setprio(2);
+        // Issue priority by position: a wave that has arrived while others have not yields (0) to
+        // them; the last to arrive -- the summing wave, behind all the others -- leads (2) until
+        // its next hand-off wait; past a wait every wave is at 1.  Without it the waves dispatched
+        // second (4-7) lose every arbitration against their SIMD partners, one of them arrives
+        // last at every hand-off of the workgroup and sums it, and the other seven wait for it:
+        // the 7B layer x16 / x32 50.2 / 61.6 -> 47.5 / 56.3 us, same bits
+        // (profiles/r06/kstream_prio_ab.txt; a static priority for waves 4-7 did nothing).
+        if ((old & (KW - 1)) != KW - 1) {
+            __builtin_amdgcn_s_setprio(0);
+            return false;
         }
-        if ((old & (KW - 1)) != KW - 1) return false;
+        __builtin_amdgcn_s_setprio(2);
 #ifdef GQ_KSTREAM_STAMPS
         const unsigned long long tsum = __builtin_amdgcn_s_memtime();
         ++n_sum;
@@ -595,7 +510,7 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
                 // other waves then wait for at their next hand-off), summed in wave order
                 f32x4 r[KW];
 #pragma unroll
-                for (int w = 0; w < KW; ++w) r[w] = *(const f32x4 *)(sb + ((w * IP + ip) * NB + t) * 256 + 4 * lane);
+                for (int w = 0; w < KW; ++w) r[w] = *(const f32x4 *)(scr + ((w * IP + ip) * NB + t) * 256 + 4 * lane);
                 asm volatile("" ::"v"(r[0]), "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), "v"(r[7]));
                 f32x4 v = r[0];
 #pragma unroll
@@ -614,7 +529,7 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
                 }
             }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the scratch reads are done
-        if (lane == 0) __hip_atomic_store(done, use + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0) __hip_atomic_store(&sync[1], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #ifdef GQ_KSTREAM_STAMPS
         t_sum += __builtin_amdgcn_s_memtime() - tsum;
 #endif
@@ -695,7 +610,7 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
 #pragma unroll
                 for (int t = 0; t < NB; ++t) asm volatile("" ::"v"(acc[ip][t]));
         } else if (reduce_store(j0 + gi, np, acc)) {
-            stq += (uint32_t)(KDS ? 1 : IP * NB) * 0x01010101u; // (the stores it issued)
+            stq += (uint32_t)(IP * NB) * 0x01010101u;
         }
 #ifdef GQ_KSTREAM_STAMPS
         t_red += __builtin_amdgcn_s_memtime() - tr;
@@ -726,11 +641,10 @@ template <int NB, int CWM>
 __global__ __launch_bounds__(64 * KW, KWPC * KW / 4) void kstream_kernel(const KArgs a)
 {
     extern __shared__ __attribute__((aligned(1024))) uint8_t smem[]; // the waves' rings (KRGN each)
-    __shared__ __attribute__((aligned(16))) float scr[KDB * KW * KIP<NB> * NB * 256]; // the waves' item tiles
-    __shared__ int sync[2 * KDB]; // per scratch buffer: arrivals, uses summed
-    if (threadIdx.x < 2 * KDB) sync[threadIdx.x] = 0;
-    if (GQ_KSTREAM_PRIO == 1 && threadIdx.x >= 256) __builtin_amdgcn_s_setprio(1); // (wave-uniform)
-    if (GQ_KSTREAM_PRIO == 2) __builtin_amdgcn_s_setprio(1);
+    __shared__ __attribute__((aligned(16))) float scr[KW * KIP<NB> * NB * 256]; // the waves' item tiles
+    __shared__ int sync[2]; // arrivals, hand-offs summed
+    if (threadIdx.x < 2) sync[threadIdx.x] = 0;
+    __builtin_amdgcn_s_setprio(1);
     __syncthreads();
     // this workgroup's items: those whose first weight byte (the parts' bytes in order) falls in
     // [t0, t1), an equal share of the launch's cost (weight bytes, weighted per format: launch_kstream)
@@ -757,13 +671,13 @@ template <int NB, int CWM> hipError_t run(const KArgs &a, unsigned grid, hipStre
         hipFuncAttributes fa;
         hipError_t e = hipFuncGetAttributes(&fa, (const void *)kstream_kernel<NB, CWM>);
         if (e != hipSuccess) return e;
-        if (KWPC * (fa.sharedSizeBytes + (size_t)KW * KRGN<NB>) > 160 * 1024) return hipErrorInvalidValue;
+        if (KWPC * (fa.sharedSizeBytes + (size_t)KW * KRGN) > 160 * 1024) return hipErrorInvalidValue;
         e = hipFuncSetAttribute((const void *)kstream_kernel<NB, CWM>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                KW * KRGN<NB>);
+                                KW * KRGN);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    kstream_kernel<NB, CWM><<<dim3(grid), dim3(64 * KW), (size_t)KW * KRGN<NB>, s>>>(a);
+    kstream_kernel<NB, CWM><<<dim3(grid), dim3(64 * KW), (size_t)KW * KRGN, s>>>(a);
     return hipGetLastError();
 }
 
@@ -891,8 +805,7 @@ hipError_t launch_kstream(const KItem *items, int n, int64_t N, int aq, void *pa
     a.n = np;
     a.wtot = wcum;
     a.slot = kb;
-    const int rgn = N <= 16 ? KRGN<1> : KRGN<2>;
-    a.ns = rgn / kb > KNSMAX ? KNSMAX : rgn / kb; // ring slots per wave (3 or 4)
+    a.ns = KRGN / kb > KNSMAX ? KNSMAX : KRGN / kb; // ring slots per wave (3 or 4)
     const int64_t wgs = num_cus() * KWPC;
     const unsigned grid = (unsigned)(items_total < wgs ? items_total : wgs);
     hipError_t e;
