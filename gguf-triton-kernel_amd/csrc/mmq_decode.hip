@@ -49,6 +49,12 @@ typedef __attribute__((address_space(3))) void lds_void;
 #define GQ_DECODE_DW 8
 #endif
 constexpr int DW = GQ_DECODE_DW; // waves per workgroup (two per SIMD)
+// issue priority of the two waves of a SIMD (A/B builds): 0 none (by age: waves 0..DW/2-1 win
+// every arbitration); 1 = the second half leads for the first half of its tasks, the first half
+// for the rest; 3 = the second half at priority 1 throughout
+#ifndef GQ_DECODE_PRIO
+#define GQ_DECODE_PRIO 0
+#endif
 #ifndef GQ_DECODE_NI
 #define GQ_DECODE_NI 7
 #endif
@@ -534,10 +540,15 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
         unit(l, u, i, acc);
     };
 
+    if ((GQ_DECODE_PRIO == 1 || GQ_DECODE_PRIO == 3) && wave >= DW / 2) __builtin_amdgcn_s_setprio(1);
     for (int j = 0; j < ntask; ++j) {
 #ifdef GQ_DECODE_STAMPS
         const unsigned long long ta = __builtin_amdgcn_s_memtime();
 #endif
+        if (GQ_DECODE_PRIO == 1 && j == ntask / 2) {
+            if (wave >= DW / 2) __builtin_amdgcn_s_setprio(0);
+            else __builtin_amdgcn_s_setprio(1);
+        }
         // slot (j - 1) % NS was freed by the previous multiply: refill it, then wait for task j
         // with the tasks issued after it still in flight (counted vmcnt; stores only add to it)
         if (j > 0 && issued < ntask) {

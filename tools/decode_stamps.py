@@ -25,7 +25,8 @@ for cfg in sys.argv[1:] or ["q6_k_28672x8192_m1"]:
     torch.cuda.synchronize()
     buf = np.zeros((65536, 13), np.uint64)
     assert kl.lib().gq_debug_decode_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes) == 0
-    used = buf[buf[:, 3] > 0].astype(np.float64)
+    ids = np.nonzero(buf[:, 3] > 0)[0]
+    used = buf[ids].astype(np.float64)
     pro, wait, loop, nt = used[:, 0], used[:, 1], used[:, 2], used[:, 3]
     xw, qd, t0, t1 = used[:, 4], used[:, 5], used[:, 6], used[:, 7]
     tot = pro + loop
@@ -49,6 +50,14 @@ for cfg in sys.argv[1:] or ["q6_k_28672x8192_m1"]:
           f"{np.percentile(wmax, 90):.0f}/{wmax.max():.0f};  workgroup mean med={np.median([tot[bx == b].mean() for b in np.unique(bx)]):.0f}")
     print("   per XCC: med/max duration " + "  ".join(
         f"{x}:{np.median(tot[xcc == x]):.0f}/{tot[xcc == x].max():.0f}" for x in np.unique(xcc)))
+    # by the wave's index in its workgroup (waves i and i + DW/2 share a SIMD): duration against the
+    # workgroup mean, and how often that index is the workgroup's slowest
+    DW = int(os.environ.get("GQ_DECODE_DW", "8"))
+    widx = ids % DW
+    rel = np.array([tot[i] / tot[bx == bx[i]].mean() for i in range(len(tot))])
+    slow = np.array([ids[bx == b][np.argmax(tot[bx == b])] % DW for b in np.unique(bx)])
+    print("   by wave index: duration / workgroup mean " + " ".join(f"{k}:{rel[widx == k].mean():.3f}" for k in range(DW))
+          + ";  slowest-wave share " + " ".join(f"{k}:{(slow == k).mean():.2f}" for k in range(DW)))
     for q in (10, 50, 90):
         print(f"   p{q}: start={np.percentile(t0 - T0, q):.0f} barrier={np.percentile(tp - T0, q):.0f} "
               f"dma0={np.percentile(w0 - T0, q):.0f} end={np.percentile(t1 - T0, q):.0f}")
