@@ -56,12 +56,13 @@ namespace {
 constexpr int ABL = GQ_RGEMM_ABL;
 
 constexpr int RW = 8;                 // waves per workgroup (two per SIMD)
-// issue priority of the two waves of a SIMD (A/B builds): 0 none (by age: waves 0-3 win every
-// arbitration); 1 (resident GEMM) = waves 4-7 lead until the second half multiply, waves 0-3
-// after it; 3 = waves 4-7 at priority 1 throughout (resident and streaming GEMMs)
-#ifndef GQ_RGEMM_PRIO
-#define GQ_RGEMM_PRIO 0
-#endif
+// Issue priority: waves 4-7 -- dispatched second, so the losers of every VALU / MFMA arbitration
+// against their SIMD partners by age (MI355X_MICROARCH.md, two waves per SIMD, item 4) -- run at
+// s_setprio 1 in the resident and streaming GEMMs: the 7B layer x64 / x128 / x512 73.9 / 99.4 /
+// 331.8 -> 72.3 / 98.3 / 329.0 us, Q4_K 11008x4096x128 33.5 -> 32.8, the headline unchanged
+// (16.13), same bits; swapping the halves at the resident GEMM's second half multiply did
+// nothing (profiles/r06/gemm_prio_ab.txt).
+constexpr int RPRIO_WAVE = RW / 2;
 constexpr int RRG = 2;                // 16-row groups per wave
 constexpr int RBM = 16 * RW * RRG;    // 256 rows per tile
 constexpr int LDS_CAP = 160 * 1024;
@@ -480,7 +481,7 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool ilc = ilc_gx > 0;
-    if ((GQ_RGEMM_PRIO == 1 || GQ_RGEMM_PRIO == 3) && wave >= RW / 2) __builtin_amdgcn_s_setprio(1);
+    if (wave >= RPRIO_WAVE) __builtin_amdgcn_s_setprio(1);
     const TileId tile = ilc ? ilc_tile(ilc_gx, ilc_gy) : grid_tile();
     const int64_t m0 = (int64_t)tile.x * RBM, n0 = (int64_t)tile.y * G::BN, sb = tile.z;
     const int64_t row_bytes = (K / Layout<F>::QK) * Layout<F>::BYTES;
@@ -597,10 +598,6 @@ __global__ __launch_bounds__(64 * RW) void rgemm_kernel(const uint8_t *__restric
 #pragma unroll
     for (int u = 0; u < 4 && !(ABL & 4); ++u) {
         if (u == 2) { // the second half
-            if (GQ_RGEMM_PRIO == 1) {
-                if (wave >= RW / 2) __builtin_amdgcn_s_setprio(0);
-                else __builtin_amdgcn_s_setprio(1);
-            }
 #ifdef GQ_RGEMM_STAMPS
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             for (int rg = 0; rg < RRG; ++rg)
@@ -726,7 +723,7 @@ __device__ __forceinline__ void sgemm_body(const uint8_t *__restrict__ A, const 
     using G = SCfg<F, NB>;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if (GQ_RGEMM_PRIO == 3 && wave >= RW / 2) __builtin_amdgcn_s_setprio(1);
+    if (wave >= RPRIO_WAVE) __builtin_amdgcn_s_setprio(1);
     const int64_t m0 = (int64_t)id.x * RBM, n0 = (int64_t)id.y * G::BN;
     const int64_t row_bytes = (K / Layout<F>::QK) * Layout<F>::BYTES;
     // super-blocks [sb0, sb1) of the tile; the partial (or C when id.gz == 1) as split id.z
@@ -809,7 +806,7 @@ __device__ __forceinline__ void sgemm_full_body(const uint8_t *__restrict__ A, c
     using G = SFull<NB>;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if (GQ_RGEMM_PRIO == 3 && wave >= RW / 2) __builtin_amdgcn_s_setprio(1);
+    if (wave >= RPRIO_WAVE) __builtin_amdgcn_s_setprio(1);
     const int g = lane >> 4, l16 = lane & 15;
     const int64_t m0 = (int64_t)id.x * RBM, n0 = (int64_t)id.y * G::BN;
     const int64_t row_bytes = (K / 256) * 144;
