@@ -466,7 +466,10 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
 #ifdef GQ_KSTREAM_STAMPS
         t_spin += __builtin_amdgcn_s_memtime() - ts;
 #endif
-        __builtin_amdgcn_s_setprio(1); // (issue priority: see the arrival below)
+#ifndef GQ_KSTREAM_PRANK
+#define GQ_KSTREAM_PRANK 0 // (A/B builds: 1 -- priority by arrival rank, kept until the next arrival)
+#endif
+        if (!GQ_KSTREAM_PRANK) __builtin_amdgcn_s_setprio(1); // (issue priority: see the arrival below)
         // Ordering: a wave's LDS operations execute in issue order, so only the compiler could
         // move the scratch accesses across the hand-off words; an empty asm with a memory clobber
         // at each edge forbids that.  (Not a fence: any acquire / release, even one restricted to
@@ -492,6 +495,10 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
         // last at every hand-off of the workgroup and sums it, and the other seven wait for it:
         // the 7B layer x16 / x32 50.2 / 61.6 -> 47.5 / 56.3 us, same bits
         // (profiles/r06/kstream_prio_ab.txt; a static priority for waves 4-7 did nothing).
+        if (GQ_KSTREAM_PRANK && (old & (KW - 1)) >= KW / 2 && (old & (KW - 1)) != KW - 1) {
+            __builtin_amdgcn_s_setprio(1); // (arrived in the second half: behind, favoured next item)
+            return false;
+        }
         if ((old & (KW - 1)) != KW - 1) {
             __builtin_amdgcn_s_setprio(0);
             return false;
