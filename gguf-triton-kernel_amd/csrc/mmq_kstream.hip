@@ -391,6 +391,30 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
         const uint32_t xbytes = (uint32_t)(((int64_t)(N - 1) * P.ldx + P.K) * 2);
         const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void *)P.X, 0, (int)xbytes, 0x00020000);
         const int frow = ((l16 & 1) << 3) | ((l16 & 2) << 1) | ((l16 & 4) >> 1) | ((l16 & 8) >> 3); // bitrev4
+#ifndef GQ_KSTREAM_XDIRECT
+#define GQ_KSTREAM_XDIRECT 0 // (A/B builds: 1 -- prepared x~ loaded straight into the fragments)
+#endif
+        if (GQ_KSTREAM_XDIRECT && aq == 0) {
+            // every fragment piece by its own 16-byte load (a lane's 8 pieces of a super-block are
+            // two 64-byte runs of its token row; the 4 lane groups of a token cover the row's 512
+            // bytes), all in flight at once, one wait; super-blocks past the chunk re-read its first
+#pragma unroll
+            for (int t = 0; t < NB; ++t)
+#pragma unroll
+                for (int c = 0; c < CWM; ++c) {
+                    const int tok = 16 * t + l16 < N ? 16 * t + l16 : N - 1;
+                    const uint32_t sb = (uint32_t)(c < mysb ? sb0 + c : sb0);
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const uint32_t off = 2u * ((uint32_t)tok * (uint32_t)P.ldx + 256u * sb +
+                                                       (uint32_t)(elem_a<F>(gl) + h * elem_b_off<F>() + 8 * i));
+                            xf[c][4 * h + i][t] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+                        }
+                }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else
 #pragma unroll
         for (int t = 0; t < NB; ++t)
 #pragma unroll
@@ -466,10 +490,6 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
 #ifdef GQ_KSTREAM_STAMPS
         t_spin += __builtin_amdgcn_s_memtime() - ts;
 #endif
-#ifndef GQ_KSTREAM_PRANK
-#define GQ_KSTREAM_PRANK 0 // (A/B builds: 1 -- priority by arrival rank, kept until the next arrival)
-#endif
-        if (!GQ_KSTREAM_PRANK) __builtin_amdgcn_s_setprio(1); // (issue priority: see the arrival below)
         // Ordering: a wave's LDS operations execute in issue order, so only the compiler could
         // move the scratch accesses across the hand-off words; an empty asm with a memory clobber
         // at each edge forbids that.  (Not a fence: any acquire / release, even one restricted to
@@ -488,19 +508,18 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
         asm volatile("" ::: "memory");
         old = __builtin_amdgcn_readfirstlane(old);
         ++seq;
-        // Issue priority by position: a wave that has arrived while others have not yields (0) to
-        // them; the last to arrive -- the summing wave, behind all the others -- leads (2) until
-        // its next hand-off wait; past a wait every wave is at 1.  Without it the waves dispatched
-        // second (4-7) lose every arbitration against their SIMD partners, one of them arrives
-        // last at every hand-off of the workgroup and sums it, and the other seven wait for it:
-        // the 7B layer x16 / x32 50.2 / 61.6 -> 47.5 / 56.3 us, same bits
-        // (profiles/r06/kstream_prio_ab.txt; a static priority for waves 4-7 did nothing).
-        if (GQ_KSTREAM_PRANK && (old & (KW - 1)) >= KW / 2 && (old & (KW - 1)) != KW - 1) {
-            __builtin_amdgcn_s_setprio(1); // (arrived in the second half: behind, favoured next item)
-            return false;
-        }
-        if ((old & (KW - 1)) != KW - 1) {
-            __builtin_amdgcn_s_setprio(0);
+        // Issue priority by arrival rank, held until the wave's next arrival: the first half to
+        // arrive at 0, the second half at 1, the last -- the summing wave, behind all the others
+        // -- at 2.  Without it the waves dispatched second (4-7) lose every arbitration against
+        // their SIMD partners, one of them arrives last at every hand-off of the workgroup and
+        // sums it, and the other seven wait for it: the 7B layer x16 / x32 50.2 / 61.6 -> 47.5 /
+        // 56.3 us with a first form (0 once arrived, 2 last, 1 past the next wait), single
+        // matrices 1-2% faster again with the rank form; same bits (profiles/r06/kstream_prio_ab.txt,
+        // kstream_prank_ab.txt; a static priority for waves 4-7 did nothing).
+        const int rank = old & (KW - 1);
+        if (rank != KW - 1) {
+            if (rank >= KW / 2) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
             return false;
         }
         __builtin_amdgcn_s_setprio(2);
