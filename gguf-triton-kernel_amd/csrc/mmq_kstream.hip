@@ -385,36 +385,14 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
     //      super-blocks (1 KiB, one fully coalesced DMA instruction per token row; 16-byte piece Q
     //      of row r at piece Q ^ bitrev4(r), so the fragment reads of 16 rows hit distinct banks),
     //      then the lane's two q8_1 blocks per super-block read back (8 pieces) and quantized
-    //      (aq 1 / 2) or taken as they are (aq 0: prepared x~, the fragment order already) ----
+    //      (aq 1 / 2) or taken as they are (aq 0: prepared x~, the fragment order already).
+    //      (Loading the prepared x~ straight into the fragments instead -- 16-byte loads, 64-byte
+    //      runs per lane group -- is 30-50% slower: profiles/r06/kstream_xdirect_ab.txt) ----
     f16x8 xf[CWM][8][NB];
     {
         const uint32_t xbytes = (uint32_t)(((int64_t)(N - 1) * P.ldx + P.K) * 2);
         const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void *)P.X, 0, (int)xbytes, 0x00020000);
         const int frow = ((l16 & 1) << 3) | ((l16 & 2) << 1) | ((l16 & 4) >> 1) | ((l16 & 8) >> 3); // bitrev4
-#ifndef GQ_KSTREAM_XDIRECT
-#define GQ_KSTREAM_XDIRECT 0 // (A/B builds: 1 -- prepared x~ loaded straight into the fragments)
-#endif
-        if (GQ_KSTREAM_XDIRECT && aq == 0) {
-            // every fragment piece by its own 16-byte load (a lane's 8 pieces of a super-block are
-            // two 64-byte runs of its token row; the 4 lane groups of a token cover the row's 512
-            // bytes), all in flight at once, one wait; super-blocks past the chunk re-read its first
-#pragma unroll
-            for (int t = 0; t < NB; ++t)
-#pragma unroll
-                for (int c = 0; c < CWM; ++c) {
-                    const int tok = 16 * t + l16 < N ? 16 * t + l16 : N - 1;
-                    const uint32_t sb = (uint32_t)(c < mysb ? sb0 + c : sb0);
-#pragma unroll
-                    for (int h = 0; h < 2; ++h)
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            const uint32_t off = 2u * ((uint32_t)tok * (uint32_t)P.ldx + 256u * sb +
-                                                       (uint32_t)(elem_a<F>(gl) + h * elem_b_off<F>() + 8 * i));
-                            xf[c][4 * h + i][t] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
-                        }
-                }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else
 #pragma unroll
         for (int t = 0; t < NB; ++t)
 #pragma unroll
