@@ -34,6 +34,9 @@ GROUPED_MAX_TOKENS = {"auto": 4, True: 4, False: 0}
 # grouped= setting -> the fewest tokens LayerMix runs as one grouped streaming-GEMM launch (the
 # stream-K plan: a 7B layer at 8 tokens 64.1 vs 66.3 us one call per set; profiles/r04/ab9_layer.txt)
 GEMM_GROUPED_MIN_TOKENS = {"auto": 5, True: 5, False: 1 << 62}
+# activation format -> the fewest tokens whose calls take prepared activations (one quantization
+# per input group) instead of quantizing in the decode kernel
+PREPARED_MIN_TOKENS = {"q8_1": 5, "fp8": 3}
 
 
 class GGUFLinear:
@@ -148,7 +151,7 @@ class LayerMix:
                         if i not in sub:
                             res[keys[i]] = _lib.mmq(g, A, inp, M, N, K, out=buf, act=self.act)
                     done = True
-        if not done and all(inp.shape[0] == x.shape[0] for inp in inputs) and x.shape[0] > (4 if self.act == "q8_1" else 2):
+        if not done and all(inp.shape[0] == x.shape[0] for inp in inputs) and x.shape[0] >= PREPARED_MIN_TOKENS[self.act]:
             # every input group's activations quantized in ONE launch (gq_act_prepare_grouped),
             # then every call prepared -- bit-identical to each call quantizing its own input
             N = x.shape[0]
@@ -179,7 +182,7 @@ class LayerMix:
         if not done:
             for calls, inp in zip(self.calls, inputs):
                 N, K = inp.shape
-                if N <= (4 if self.act == "q8_1" else 2) or len(calls) == 1:
+                if N < PREPARED_MIN_TOKENS[self.act] or len(calls) == 1:
                     # decode (each call quantizes its tokens in-kernel), or a single call
                     for key, L in calls:
                         res[key] = _lib.mmq(L.gtype, L.A, inp, L.M, N, K, out=self._out(key, L, N, inp.device, out),

@@ -21,10 +21,16 @@ if "--tune" in args:  # library tuning overrides (gq_debug_set_tuning)
     for kv in filter(None, args[args.index("--tune") + 1].split(",")):
         k, v = kv.split("=")
         kl.set_tuning(k, int(v))
+if "--decode-max" in args:  # q8_1: the grouped decode up to D tokens, prepared + grouped GEMM / stream from D + 1
+    import kernels.layer_mix as lm
+    D = int(args[args.index("--decode-max") + 1])
+    lm.GROUPED_MAX_TOKENS[True] = D
+    lm.GEMM_GROUPED_MIN_TOKENS[True] = D + 1
+    lm.PREPARED_MIN_TOKENS["q8_1"] = D + 1
 act = args[args.index("--act") + 1] if "--act" in args else "q8_1"
 gmin = int(args[args.index("--gemm-min") + 1]) if "--gemm-min" in args else None  # LayerMix gemm_grouped_min
 pos = [a for i, a in enumerate(args)
-       if not a.startswith("--") and (i == 0 or args[i - 1] not in ("--lib", "--tune", "--act", "--gemm-min"))]
+       if not a.startswith("--") and (i == 0 or args[i - 1] not in ("--lib", "--tune", "--act", "--gemm-min", "--decode-max"))]
 Ns = tuple(int(n) for n in (pos[0] if pos else "1,2,3,4").split(","))
 for grouped in ((True,) if "--grouped-only" in args else (True, False)):  # (True: grouped at 1..4 tokens)
     r = bench.bench_layer(Ns, (act,), 50, 5, dev, fuse=True, grouped=grouped, gemm_grouped_min=gmin)
