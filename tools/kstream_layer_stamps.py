@@ -15,7 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "gguf-triton-kernel_amd")]
 import kernels._lib as kl  # noqa: E402
 
-kl.LIB_PATH = os.path.join(ROOT, "gguf-triton-kernel_amd", "lib", "libgguf_mmq_kstamps.so")
+kl.LIB_PATH = os.path.join(ROOT, "gguf-triton-kernel_amd", "lib",
+                           "libgguf_mmq_%s.so" % os.environ.get("GQ_KSTAMPS_SO", "kstamps"))
 import torch  # noqa: E402
 
 import bench  # noqa: E402
