@@ -51,7 +51,8 @@ typedef __attribute__((address_space(3))) void lds_void;
 constexpr int DW = GQ_DECODE_DW; // waves per workgroup (two per SIMD)
 // issue priority of the two waves of a SIMD (A/B builds): 0 none (by age: waves 0..DW/2-1 win
 // every arbitration); 1 = the second half leads for the first half of its tasks, the first half
-// for the rest; 3 = the second half at priority 1 throughout
+// for the rest; 3 = the second half at priority 1 throughout; 4 = the second half at priority 1
+// until the activation barrier (the waves it waits for), none after it
 #ifndef GQ_DECODE_PRIO
 #define GQ_DECODE_PRIO 0
 #endif
@@ -192,6 +193,7 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
     constexpr int UPC = UPC_OF<F, NT>;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (GQ_DECODE_PRIO == 4 && wave >= DW / 2) __builtin_amdgcn_s_setprio(1);
 #ifdef GQ_DECODE_STAMPS
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
     unsigned long long t_wait = 0, t_w0 = 0, t_c0 = 0;
@@ -408,6 +410,7 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
 #endif
     // raw barrier: __syncthreads() would also wait vmcnt(0), draining the weight DMAs in flight
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (GQ_DECODE_PRIO == 4 && wave >= DW / 2) __builtin_amdgcn_s_setprio(0);
 #ifdef GQ_DECODE_STAMPS
     const unsigned long long t_pro = __builtin_amdgcn_s_memtime();
 #endif
