@@ -387,67 +387,14 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
     //      then the lane's two q8_1 blocks per super-block read back (8 pieces) and quantized
     //      (aq 1 / 2) or taken as they are (aq 0: prepared x~, the fragment order already).
     //      (Loading the prepared x~ straight into the fragments instead -- 16-byte loads, 64-byte
-    //      runs per lane group -- is 30-50% slower: profiles/r06/kstream_xdirect_ab.txt) ----
+    //      runs per lane group -- is 30-50% slower: profiles/r06/kstream_xdirect_ab.txt; one-
+    //      super-block passes with the next in flight leave the prologue's ticks unchanged and the
+    //      layer 2-5% slower at 24-32 tokens: kstream_xpipe_ab.txt) ----
     f16x8 xf[CWM][8][NB];
     {
         const uint32_t xbytes = (uint32_t)(((int64_t)(N - 1) * P.ldx + P.K) * 2);
         const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void *)P.X, 0, (int)xbytes, 0x00020000);
         const int frow = ((l16 & 1) << 3) | ((l16 & 2) << 1) | ((l16 & 4) >> 1) | ((l16 & 8) >> 3); // bitrev4
-#ifndef GQ_KSTREAM_XPIPE
-#define GQ_KSTREAM_XPIPE 0 // (A/B builds: 1 -- one-super-block passes, the next in flight while one is read)
-#endif
-        if constexpr (GQ_KSTREAM_XPIPE && KWPC == 1) {
-            // passes (t, c) of 16 token rows x one super-block (8 KiB, 8 DMA instructions) into the
-            // two halves of the wave's region alternately: pass p + 1 in flight while p is read.
-            // Every pass runs (a super-block past the chunk re-reads the chunk's first -- or, on a
-            // wave without one, whatever the clamped offset holds: never multiplied)
-            constexpr int NP = NB * CWM;
-            auto xdma = [&](int p) __attribute__((always_inline)) {
-                const int t = p / CWM, c = p % CWM;
-                const uint32_t sb = (uint32_t)(sb0 + (c < mysb ? c : 0));
-                uint8_t *buf = ring + 8192 * (p & 1);
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const int r = (64 * i + lane) >> 5, pos = (64 * i + lane) & 31;
-                    const int tok = 16 * t + r < N ? 16 * t + r : N - 1;
-                    const int q = pos ^ (((r & 1) << 3) | ((r & 2) << 1) | ((r & 4) >> 1) | ((r & 8) >> 3));
-                    dma16(xrs, buf + 1024 * i, 2u * ((uint32_t)tok * (uint32_t)P.ldx + 256u * sb + 8u * (uint32_t)q), 0);
-                }
-            };
-            xdma(0);
-#pragma unroll
-            for (int p = 0; p < NP; ++p) {
-                const int t = p / CWM, c = p % CWM;
-                if (p + 1 < NP) {
-                    xdma(p + 1); // (into the half pass p - 1 was read from: its reads are done)
-                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-                } else {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
-                const uint8_t *buf = ring + 8192 * (p & 1);
-                u32x4 xr[2][4];
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int qp = (elem_a<F>(gl) + h * elem_b_off<F>()) / 8 + i;
-                        xr[h][i] = *(const u32x4 *)(buf + 512 * l16 + 16 * (qp ^ frow));
-                    }
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    u32x4 o[4];
-                    if (aq == 1) deq_lane32(xr[h], o);
-                    else if (aq == 2) f8_lane32(xr[h], o);
-                    else {
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) o[i] = xr[h][i];
-                    }
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) xf[c][4 * h + i][t] = __builtin_bit_cast(f16x8, o[i]);
-                }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the half is free again
-            }
-        } else
 #pragma unroll
         for (int t = 0; t < NB; ++t)
 #pragma unroll
