@@ -285,8 +285,8 @@ bool use_kstream(int t, int form, int64_t M, int64_t N, int64_t K, int act, bool
 {
     const int ks = gq::tuning().kstream;
     if (ks == 0 || form != gq::AF_F16 || use_blas(N, K) || !gq::kstream_ok(t, M, N, K)) return false;
-    // (q8_1 at 3..4 tokens: the grouped decode; the stream there measured 1.6x slower on the 7B
-    // layer, profiles/r06/kstream_nmin3_ab.txt)
+    // (q8_1 at 3..4 tokens: the grouped decode -- the prepared workspace holds the decode's SOA
+    // q8_1 form there, not the fp16 x~ the stream reads; profiles/r06/kstream_nmin3_ab.txt)
     if (N < (act == GQ_ACT_FP8_E4M3 ? 3 : 5)) return false;
     if (gq::kstream_splits(K) > 1 && !split && ks != 1) return false;
     if (ks == 1) return true;
