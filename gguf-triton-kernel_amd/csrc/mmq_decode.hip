@@ -49,13 +49,10 @@ typedef __attribute__((address_space(3))) void lds_void;
 #define GQ_DECODE_DW 8
 #endif
 constexpr int DW = GQ_DECODE_DW; // waves per workgroup (two per SIMD)
-// issue priority of the two waves of a SIMD (A/B builds): 0 none (by age: waves 0..DW/2-1 win
-// every arbitration); 1 = the second half leads for the first half of its tasks, the first half
-// for the rest; 3 = the second half at priority 1 throughout; 4 = the second half at priority 1
-// until the activation barrier (the waves it waits for), none after it
-#ifndef GQ_DECODE_PRIO
-#define GQ_DECODE_PRIO 0
-#endif
+// (issue priority between a SIMD's two waves -- waves 4-7 lose by age and are every workgroup's
+// slowest -- balanced by a swap at the middle of the task list, or favouring waves 4-7 until the
+// activation barrier or throughout: the steps move -2.4..+1.6%, the stream sets the time;
+// profiles/r06/decode_prio_ab.txt, decode_prio4_ab.txt.  Not kept.)
 #ifndef GQ_DECODE_NI
 #define GQ_DECODE_NI 7
 #endif
@@ -193,7 +190,6 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
     constexpr int UPC = UPC_OF<F, NT>;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if (GQ_DECODE_PRIO == 4 && wave >= DW / 2) __builtin_amdgcn_s_setprio(1);
 #ifdef GQ_DECODE_STAMPS
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
     unsigned long long t_wait = 0, t_w0 = 0, t_c0 = 0;
@@ -410,7 +406,6 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
 #endif
     // raw barrier: __syncthreads() would also wait vmcnt(0), draining the weight DMAs in flight
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (GQ_DECODE_PRIO == 4 && wave >= DW / 2) __builtin_amdgcn_s_setprio(0);
 #ifdef GQ_DECODE_STAMPS
     const unsigned long long t_pro = __builtin_amdgcn_s_memtime();
 #endif
@@ -543,15 +538,10 @@ __device__ __forceinline__ void decode_body(const uint8_t *__restrict__ A, const
         unit(l, u, i, acc);
     };
 
-    if ((GQ_DECODE_PRIO == 1 || GQ_DECODE_PRIO == 3) && wave >= DW / 2) __builtin_amdgcn_s_setprio(1);
     for (int j = 0; j < ntask; ++j) {
 #ifdef GQ_DECODE_STAMPS
         const unsigned long long ta = __builtin_amdgcn_s_memtime();
 #endif
-        if (GQ_DECODE_PRIO == 1 && j == ntask / 2) {
-            if (wave >= DW / 2) __builtin_amdgcn_s_setprio(0);
-            else __builtin_amdgcn_s_setprio(1);
-        }
         // slot (j - 1) % NS was freed by the previous multiply: refill it, then wait for task j
         // with the tasks issued after it still in flight (counted vmcnt; stores only add to it)
         if (j > 0 && issued < ntask) {
