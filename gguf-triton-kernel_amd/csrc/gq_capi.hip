@@ -280,17 +280,14 @@ bool rgemm_route(int t, int form, int64_t M, int64_t N, int64_t K, int act)
 // A K longer than 4096 is cut into ranges summed by a second launch (fp32 partials in the
 // workspace): by default only inside a grouped launch (the layer's ffn_down beside the K = 4096
 // projections); split = false asks for the one-launch form.
-#ifndef GQ_KSTREAM_RAWG_NMIN
-#define GQ_KSTREAM_RAWG_NMIN 5 // fewest q8_1 tokens of the raw grouped launch's stream (A/B builds: 3)
-#endif
 bool use_kstream(int t, int form, int64_t M, int64_t N, int64_t K, int act, bool prepared = false,
-                 bool split = false, bool raw_grouped = false)
+                 bool split = false)
 {
     const int ks = gq::tuning().kstream;
     if (ks == 0 || form != gq::AF_F16 || use_blas(N, K) || !gq::kstream_ok(t, M, N, K)) return false;
     // (q8_1 at 3..4 tokens: the grouped decode -- the prepared workspace holds the decode's SOA
     // q8_1 form there, not the fp16 x~ the stream reads; profiles/r06/kstream_nmin3_ab.txt)
-    if (N < (act == GQ_ACT_FP8_E4M3 ? 3 : raw_grouped ? GQ_KSTREAM_RAWG_NMIN : 5)) return false;
+    if (N < (act == GQ_ACT_FP8_E4M3 ? 3 : 5)) return false;
     if (gq::kstream_splits(K) > 1 && !split && ks != 1) return false;
     if (ks == 1) return true;
     if (gemm_knob_pinned()) return false; // (as the resident / streaming routes: the pinned GEMM takes the call)
@@ -1009,20 +1006,15 @@ int gq_mmq_grouped_ex(gq_act act, const gq_group_item *items, int n, int64_t N, 
                                  it.ldc, it.M, it.K};
     }
     if (m == 0) return GQ_OK;
-    // (raw_grouped: in-kernel quantization, no prepared form needed -- the stream from
-    // GQ_KSTREAM_RAWG_NMIN tokens when every item is one K range, else the decode below)
-    bool ks_all = N >= (fp8 ? 3 : GQ_KSTREAM_RAWG_NMIN) && N < (fp8 ? 3 : 5);
-    for (int i = 0; ks_all && i < m; ++i)
-        ks_all = use_kstream(di[i].fmt, gq::AF_F16, di[i].M, N, di[i].K, act, true, false, true) &&
-                 gq::kstream_splits(di[i].K) == 1 && di[i].ldx % 8 == 0 && ((uintptr_t)di[i].X & 15) == 0 &&
-                 kstream_fits(di[i].M, N, di[i].K, di[i].ldx, di[i].ldc);
-    if (N >= (fp8 ? 3 : 5) || ks_all) {
+    // (3..4 q8_1 tokens stay on the grouped decode: the stream for the K <= 4096 items with the
+    // long-K item on its own measured 13% slower on the 7B layer, profiles/r06/kstream_rawg3_ab.txt)
+    if (N >= (fp8 ? 3 : 5)) {
         // 5..32 tokens (fp8: 3..32): the K-chunked streaming MMQ, every item in one launch
         gq::KItem ki[16];
         for (int i = 0; i < m; ++i) {
             const gq::DecodeItem &d = di[i];
             // (the grouped launch's own route: the stream wherever it applies, GQ_KSTREAM=0 refuses)
-            if (!use_kstream(d.fmt, gq::AF_F16, d.M, N, d.K, act, true, false, true) || gq::kstream_splits(d.K) > 1 || d.ldx % 8 != 0 ||
+            if (!use_kstream(d.fmt, gq::AF_F16, d.M, N, d.K, act, true) || gq::kstream_splits(d.K) > 1 || d.ldx % 8 != 0 ||
                 ((uintptr_t)d.X & 15) != 0 || !kstream_fits(d.M, N, d.K, d.ldx, d.ldc))
                 return fail(GQ_EUNSUPPORTED, "item %d: not a grouped K-chunked-stream shape (N=%lld, M=%lld, K=%lld)", i,
                             (long long)N, (long long)d.M, (long long)d.K);

@@ -37,10 +37,6 @@ GEMM_GROUPED_MIN_TOKENS = {"auto": 5, True: 5, False: 1 << 62}
 # activation format -> the fewest tokens whose calls take prepared activations (one quantization
 # per input group) instead of quantizing in the decode kernel
 PREPARED_MIN_TOKENS = {"q8_1": 5, "fp8": 3}
-# (A/B) from this many tokens the grouped decode launch takes only the K <= 4096 calls (as one
-# raw grouped launch: the K-chunked stream where the library routes it there) and the longer-K
-# calls run on their own; None: one grouped launch for all
-RAW_SPLIT_MIN_TOKENS = None
 
 
 class GGUFLinear:
@@ -140,17 +136,7 @@ class LayerMix:
                 for key, L in calls:
                     keys.append(key)
                     items.append((L.gtype, L.A, inp, L.M, inp.shape[1], self._out(key, L, N, inp.device, out)))
-            if RAW_SPLIT_MIN_TOKENS is not None and N >= RAW_SPLIT_MIN_TOKENS:
-                short = [i for i, it in enumerate(items) if it[4] <= 4096]
-                o = _lib.mmq_grouped([items[i] for i in short], N, act=self.act)
-                if o is not None:
-                    res.update(zip([keys[i] for i in short], o))
-                    for i, (g, A, inp, M, K, buf) in enumerate(items):
-                        if i not in short:
-                            res[keys[i]] = _lib.mmq(g, A, inp, M, N, K, out=buf, act=self.act)
-                    items = []
-                    done = True
-            outs = _lib.mmq_grouped(items, N, act=self.act) if items else None
+            outs = _lib.mmq_grouped(items, N, act=self.act)
             if outs is not None:
                 res.update(zip(keys, outs))
                 done = True

@@ -27,13 +27,10 @@ if "--decode-max" in args:  # q8_1: the grouped decode up to D tokens, prepared 
     lm.GROUPED_MAX_TOKENS[True] = D
     lm.GEMM_GROUPED_MIN_TOKENS[True] = D + 1
     lm.PREPARED_MIN_TOKENS["q8_1"] = D + 1
-if "--raw-split" in args:  # LayerMix: the grouped decode launch for the K <= 4096 calls only, from this many tokens
-    import kernels.layer_mix as lm
-    lm.RAW_SPLIT_MIN_TOKENS = int(args[args.index("--raw-split") + 1])
 act = args[args.index("--act") + 1] if "--act" in args else "q8_1"
 gmin = int(args[args.index("--gemm-min") + 1]) if "--gemm-min" in args else None  # LayerMix gemm_grouped_min
 pos = [a for i, a in enumerate(args)
-       if not a.startswith("--") and (i == 0 or args[i - 1] not in ("--lib", "--tune", "--act", "--gemm-min", "--decode-max", "--raw-split"))]
+       if not a.startswith("--") and (i == 0 or args[i - 1] not in ("--lib", "--tune", "--act", "--gemm-min", "--decode-max"))]
 Ns = tuple(int(n) for n in (pos[0] if pos else "1,2,3,4").split(","))
 for grouped in ((True,) if "--grouped-only" in args else (True, False)):  # (True: grouped at 1..4 tokens)
     r = bench.bench_layer(Ns, (act,), 50, 5, dev, fuse=True, grouped=grouped, gemm_grouped_min=gmin)

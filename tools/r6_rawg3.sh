@@ -1,4 +1,5 @@
 #!/bin/bash
+# (measured, not taken: profiles/r06/kstream_rawg3_ab.txt; needs the round-6 tree of commit 21ac05f..e0e596f)
 # Round 6: 3..4 q8_1 tokens on the 7B layer with the raw grouped launch's K-chunked stream for the
 # K = 4096 calls (lib/libgguf_mmq_rawg3.so: -DGQ_KSTREAM_RAWG_NMIN=3; LayerMix --raw-split 3: the
 # K = 11008 call on its own) against the one grouped decode launch (the product).
@@ -7,7 +8,7 @@ mkdir -p gpurun_out
 VL=gguf-triton-kernel_amd/lib/libgguf_mmq_rawg3.so
 timeout -k 10 300 python3 - <<'PY' > gpurun_out/r6_rawg3_check.txt 2>&1 || exit $?
 import os, sys
-sys.path[:0] = [".", "gguf-triton-kernel_amd"]
+sys.path[:0] = ["oracle", "gguf-triton-kernel_amd", "."]
 import kernels._lib as kl
 kl.LIB_PATH = os.path.abspath("gguf-triton-kernel_amd/lib/libgguf_mmq_rawg3.so")
 import numpy as np, torch
