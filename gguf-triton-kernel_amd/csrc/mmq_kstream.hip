@@ -497,25 +497,12 @@ __device__ __forceinline__ void kbody(const KPart &P, int j0, int j1, int N, int
         // matrices 1-2% faster again with the rank form; same bits (profiles/r06/kstream_prio_ab.txt,
         // kstream_prank_ab.txt; a static priority for waves 4-7 did nothing).
         const int rank = old & (KW - 1);
-#ifndef GQ_KSTREAM_PFINE
-#define GQ_KSTREAM_PFINE 0 // (A/B builds: 1 -- priority rank / 2 (0..3), the last arriver 3)
-#endif
-        if (GQ_KSTREAM_PFINE) {
-            if (rank != KW - 1) {
-                if (rank >= 6) __builtin_amdgcn_s_setprio(2);
-                else if (rank >= 4) __builtin_amdgcn_s_setprio(1);
-                else __builtin_amdgcn_s_setprio(0);
-                return false;
-            }
-            __builtin_amdgcn_s_setprio(3);
-        } else {
-            if (rank != KW - 1) {
-                if (rank >= KW / 2) __builtin_amdgcn_s_setprio(1);
-                else __builtin_amdgcn_s_setprio(0);
-                return false;
-            }
-            __builtin_amdgcn_s_setprio(2);
+        if (rank != KW - 1) {
+            if (rank >= KW / 2) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+            return false;
         }
+        __builtin_amdgcn_s_setprio(2); // (four levels -- rank / 2, the last 3 -- measured no better)
 #ifdef GQ_KSTREAM_STAMPS
         const unsigned long long tsum = __builtin_amdgcn_s_memtime();
         ++n_sum;
